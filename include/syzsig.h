@@ -1,0 +1,211 @@
+/*
+ * syzsig.h -- C-ABI of the MI355X coverage-signal triage engine (libsyzsig.so).
+ *
+ * This is the drop-in boundary for syzkaller's coverage-signal path.  Every
+ * entry point names the reference interface it replaces (paths relative to the
+ * syzkaller checkout).  The Go side binds it through cgo; INTEGRATION.md shows
+ * the binding.  Plain pointers and sizes only.
+ *
+ * Conventions
+ *  - Every function returning int returns SG_OK (0) or a negative SG_E* code;
+ *    sg_last_error() gives the message (thread-local).  The Go adapter panics
+ *    on failure, as the reference callers do (syz-fuzzer/fuzzer.go:389-391).
+ *  - "host" entry points take caller-owned host memory and never retain it
+ *    (cgo pointer rules).  "_dev" entry points take device pointers already
+ *    resident in HBM and are stream-ordered on the context's stream: they do
+ *    not synchronise, and their outputs are valid after sg_ctx_sync().
+ *  - Signal / cover values are uint32_t, any value allowed.  Sorted-slice ops
+ *    follow pkg/cover/cover.go exactly: multiset semantics; 0xFFFFFFFF
+ *    (`sent`, cover.go:17) is dropped by every foreach op (cover.go:97), and
+ *    by Canonicalize only when no smaller value precedes it (`last` starts at
+ *    sent, cover.go:31).
+ *  - A context owns one HIP stream on one device and all device memory it
+ *    allocates.  Calls on one context must be serialised by the caller (the
+ *    reference already holds signalMu / mgr.mu around them).
+ *  - There is no CPU fallback: without a usable gfx950 device every call that
+ *    computes returns SG_ENODEV.
+ */
+#ifndef SYZSIG_H
+#define SYZSIG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_EINVAL (-1)
+#define SG_EHIP (-2)
+#define SG_ENOMEM (-3)
+#define SG_ENODEV (-4)
+
+typedef struct sg_ctx sg_ctx;
+typedef struct sg_set sg_set;
+
+/* Library identification and error reporting. */
+const char* sg_version(void);
+const char* sg_last_error(void);
+
+/* ---- context ------------------------------------------------------------ */
+/* One per fuzzer / manager process (or per GPU rank).  `device` is the HIP
+ * device ordinal. */
+int sg_ctx_create(int device, sg_ctx** out);
+void sg_ctx_destroy(sg_ctx* ctx);
+/* Wait for all work queued on the context's stream. */
+int sg_ctx_sync(sg_ctx* ctx);
+/* Use an external HIP stream (e.g. torch's current stream); NULL restores the
+ * context's own stream. */
+int sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream);
+void* sg_ctx_stream(sg_ctx* ctx);
+/* Per-kernel device timing with HIP events on the context's stream.
+ * enable != 0 starts recording (and resets the tallies). */
+int sg_ctx_timing(sg_ctx* ctx, int enable);
+/* Total device milliseconds and launch count recorded for kernel `name`
+ * (e.g. "triage_claim"); syncs the stream. */
+int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* launches);
+
+/* ---- signal sets: replace map[uint32]struct{} ---------------------------- */
+/* maxSignal / corpusSignal / newSignal (syz-fuzzer/fuzzer.go:65-68) and
+ * corpusSignal / maxSignal / corpusCover (syz-manager/manager.go:71-73): a
+ * direct-indexed 2^32-bit bitmap (512 MiB) resident in HBM. */
+int sg_set_create(sg_ctx* ctx, sg_set** out);
+void sg_set_destroy(sg_set* set);
+int sg_set_clear(sg_set* set);
+/* len(map) */
+int sg_set_count(sg_set* set, uint64_t* out);
+/* All members ascending (the reference iterates map order; payloads of
+ * ConnectRes.MaxSignal / PollArgs.MaxSignal, pkg/rpctype/rpctype.go).  Writes
+ * min(count, cap) values; *n = count. */
+int sg_set_export(sg_set* set, uint32_t* out, size_t cap, size_t* n);
+/* pkg/cover/cover.go:178-182  SignalAdd(base, signal) */
+int sg_set_add(sg_set* set, const uint32_t* sig, size_t n);
+/* pkg/cover/cover.go:160-167  SignalNew(base, signal) -> *out 0/1 */
+int sg_set_new(sg_set* set, const uint32_t* sig, size_t n, int* out);
+/* pkg/cover/cover.go:169-176  SignalDiff(base, signal): members of sig not in
+ * base, in order, duplicates kept.  out capacity n; *nout = count. */
+int sg_set_diff(sg_set* set, const uint32_t* sig, size_t n, uint32_t* out, size_t* nout);
+/* Device bitmap (2^27 uint32 words) for collectives (OR-reduce across ranks). */
+void* sg_set_device_words(sg_set* set);
+/* Wrap caller-owned device memory (2^27 uint32 words, e.g. a torch tensor)
+ * as a set without copying; sg_set_destroy then frees only the handle. */
+int sg_set_wrap_dev(sg_ctx* ctx, void* d_words, sg_set** out);
+/* set |= words (device pointer to 2^27 uint32 words). */
+int sg_set_or_dev(sg_set* set, const uint32_t* d_words);
+/* dst = src (both sets of the same context). */
+int sg_set_copy(sg_set* dst, sg_set* src);
+/* *out = number of the n device-resident values not in set (duplicates
+ * counted), i.e. the candidates a triage of them would test; syncs. */
+int sg_set_count_missing_dev(sg_set* set, const uint32_t* d_vals, uint64_t n, uint64_t* out);
+
+/* ---- batched new-signal triage (THE hot path) ----------------------------- */
+/* syz-fuzzer/fuzzer.go:645-693 execute(): for call records r = 0..nrec-1 in
+ * sequential (program-major, call-index) order, record r's signal is
+ * vals[rec_off[r] .. rec_off[r+1]).  Exactly as the sequential loop:
+ *   rec_new[r] = SignalNew(maxSignal, S_r) at its turn (fuzzer.go:666);
+ *   diff_r     = SignalDiff(maxSignal, S_r) at its turn (fuzzer.go:669);
+ *   maxSignal ∪= diff_r; newSignal ∪= diff_r (fuzzer.go:673-674).
+ * diff_r is written to diff_vals[diff_off[r] .. diff_off[r+1]) when diff_vals /
+ * diff_off are non-NULL (capacity = rec_off[nrec]).  newsig may be NULL.
+ * *n_diff (nullable) = total diff elements. */
+int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* vals, const uint64_t* rec_off,
+		    size_t nrec, uint8_t* rec_new, uint32_t* diff_vals, uint64_t* diff_off, uint64_t* n_diff);
+/* Same, device-resident: d_vals (nvals = rec_off[nrec] elements), d_rec_off
+ * (nrec+1), outputs d_rec_new (nrec bytes), optional d_diff_vals (capacity
+ * nvals), d_diff_off (nrec+1).  Stream-ordered, no host synchronisation. */
+int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_vals,
+			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec, uint8_t* d_rec_new,
+			uint32_t* d_diff_vals, uint64_t* d_diff_off);
+
+/* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:
+ * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */
+int sg_add_inputs(sg_ctx* ctx, sg_set* corpus, sg_set* maxsig, const uint32_t* vals, const uint64_t* off, size_t n);
+
+/* syz-manager/manager.go:907-912 NewInput() signal part, over n RPCs in
+ * arrival order: accepted[k] = SignalNew(corpusSignal, S_k) at its turn; on
+ * accept corpusSignal ∪= S_k and corpusCover ∪= Cov_k.  cover may be NULL. */
+int sg_accept_batch(sg_ctx* ctx, sg_set* corpus_sig, sg_set* corpus_cov, const uint32_t* sig_vals,
+		    const uint64_t* sig_off, const uint32_t* cov_vals, const uint64_t* cov_off, size_t n,
+		    uint8_t* accepted);
+
+/* syz-manager/manager.go:949-956 Poll() maxSignal merge over npoll polls in
+ * arrival order: poll k's newMaxSignal = members of A_k not yet in maxSignal,
+ * first occurrences, in A_k order.  new_vals capacity a_off[npoll]; new_off
+ * (npoll+1) gives each poll's slice. */
+int sg_merge_poll(sg_ctx* ctx, sg_set* mgr_max, const uint32_t* a_vals, const uint64_t* a_off, size_t npoll,
+		  uint32_t* new_vals, uint64_t* new_off);
+
+/* pkg/cover/cover.go:120-146 Minimize() over corpus CSR (vals/off, n inputs)
+ * processed in `order` (order[k] = input index processed k-th; the reference
+ * takes it from sort.Sort of minInputArray, cover.go:128).  out_idx gets the
+ * selected input indices in processing order; *nout their count. */
+int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, const uint32_t* order,
+		uint32_t* out_idx, size_t* nout);
+/* order of cover.Minimize: Go's sort.Sort over minInputArray (Less = longer
+ * first, cover.go:157), restated from the Go 1.8/1.9 sort package. */
+int sg_minimize_order(const uint64_t* off, size_t n, uint32_t* order);
+
+/* ---- sorted-slice algebra (pkg/cover/cover.go:28-117) ---------------------- */
+/* Canonicalize (cover.go:28-40): in place, *nout = canonical length. */
+int sg_canonicalize(sg_ctx* ctx, uint32_t* v, size_t n, size_t* nout);
+/* Batched Canonicalize of CSR segments in place: segment k is
+ * vals[off[k] .. off[k+1]); its canonical form is written at its own start,
+ * out_len[k] = its length (Go returns cov[:n], aliasing the input). */
+int sg_canonicalize_batch(sg_ctx* ctx, uint32_t* vals, const uint64_t* off, size_t nseg, uint64_t* out_len);
+
+#define SG_OP_DIFFERENCE 0 /* cover.go:42-49 */
+#define SG_OP_SYMDIFF 1    /* cover.go:51-61 */
+#define SG_OP_UNION 2      /* cover.go:63-70 */
+#define SG_OP_INTERSECT 3  /* cover.go:72-79 */
+/* op(a, b) for sorted a, b; out capacity na+nb; *nout = result length. */
+int sg_merge(sg_ctx* ctx, int op, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+	     size_t* nout);
+/* Batched op over npair pairs: pair k is a[a_beg[k] .. +a_len[k]) op
+ * b[b_beg[k] .. +b_len[k]) (pairs may share b, e.g. one corpus signal);
+ * result k is written at out[out_beg[k] ..) (capacity a_len[k]+b_len[k]),
+ * out_len[k] = its length.  Arrays are host pointers; a/b/out too. */
+int sg_merge_batch(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+		   const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+		   const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
+		   uint64_t* out_len);
+/* HasDifference (cover.go:106-117): *out = 1 iff a has an element (multiset,
+ * no sentinel special case) not matched in b. */
+int sg_has_difference(sg_ctx* ctx, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, int* out);
+
+/* ---- executor edge signal (executor/executor.h:389-401, :497-526) --------- */
+/* Raw per-call u32 PC traces -> per-call signal, executor-exact: edge
+ * sig = pc ^ hash(prev pc) (prev = 0 at each call start), filtered through the
+ * executor's lossy 8192-slot / 4-probe dedup table, one fresh table per
+ * program shared by its calls in call order.  Programs own calls
+ * [prog_off[p], prog_off[p+1]); call c owns pcs[call_off[c] .. call_off[c+1]).
+ * Output: sig_vals (capacity call_off[ncalls]) and sig_off (ncalls+1). */
+int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, const uint64_t* prog_off,
+		   size_t nprog, uint32_t* sig_vals, uint64_t* sig_off);
+int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
+		       uint64_t nprog, uint64_t ncalls, uint64_t npcs, uint32_t* d_sig_vals, uint64_t* d_sig_off);
+
+/* ---- synthetic Zipf traces (bench / test input generator) ----------------- */
+/* Zipf(s) over `nranks` PC ranks mapped through a permutation seeded by
+ * universe_seed (the "kernel text": shared by every batch) to
+ * pc = 0x81000000 + 16*perm(rank); draws are counter-based
+ * (splitmix64 of trace_seed and the global PC index), so any slice is
+ * reproducible.  Fills d_pcs with nprog*calls*pcs_per_call PCs of programs
+ * prog_base .. prog_base+nprog-1, program-major. */
+int sg_gen_zipf_traces_dev(sg_ctx* ctx, uint64_t universe_seed, uint64_t trace_seed, double zipf_s, uint32_t nranks,
+			   uint64_t prog_base, uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs);
+
+/* ---- cover report (syz-manager/cover.go:91-103, :257-307) ----------------- */
+/* pcs[i] = RestorePC(cov[i], base) - 5; returns the uncovered PC set of
+ * uncoveredPcsInFuncs, ascending (the reference returns map order).
+ * sym_start/sym_end sorted by start; all_pcs sorted (objdump call sites).
+ * out capacity nall; *nout = count. */
+int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t base, const uint64_t* sym_start,
+		       const uint64_t* sym_end, size_t nsym, const uint64_t* all_pcs, size_t nall, uint64_t* out,
+		       size_t* nout);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYZSIG_H */

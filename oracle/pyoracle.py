@@ -1,0 +1,269 @@
+"""oracle/pyoracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes front-end of oracle/libsigoracle.so (the C restatement of the
+reference, oracle/sigoracle.c) and of oracle/_ref/libref_executor.so (the
+reference executor compiled from its own sources).  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this; the
+product (syzkaller_amd/) never does.
+"""
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "libsigoracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_executor.so")
+
+P32 = POINTER(c_uint32)
+P64 = POINTER(c_uint64)
+P8 = POINTER(c_uint8)
+
+DIFF, SYMDIFF, UNION, INTER = 0, 1, 2, 3
+
+
+def build():
+    """Compile the oracle (and, where the reference checkout exists, _ref)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _load():
+    if not os.path.exists(ORACLE_SO):
+        build()
+    L = ctypes.CDLL(ORACLE_SO)
+    sig = {
+        "orc_canonicalize": (c_size_t, [P32, c_size_t]),
+        "orc_foreach": (c_size_t, [c_int, P32, c_size_t, P32, c_size_t, P32]),
+        "orc_has_difference": (c_int, [P32, c_size_t, P32, c_size_t]),
+        "orc_set_new": (c_void_p, []),
+        "orc_set_free": (None, [c_void_p]),
+        "orc_set_count": (c_size_t, [c_void_p]),
+        "orc_set_has": (c_int, [c_void_p, c_uint32]),
+        "orc_set_export": (c_size_t, [c_void_p, P32]),
+        "orc_signal_new": (c_int, [c_void_p, P32, c_size_t]),
+        "orc_signal_diff": (c_size_t, [c_void_p, P32, c_size_t, P32]),
+        "orc_signal_add": (None, [c_void_p, P32, c_size_t]),
+        "orc_triage_batch": (c_uint64, [c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64]),
+        "orc_add_inputs": (None, [c_void_p, c_void_p, P32, P64, c_size_t]),
+        "orc_accept_batch": (None, [c_void_p, c_void_p, P32, P64, P32, P64, c_size_t, P8]),
+        "orc_merge_poll": (c_uint64, [c_void_p, P32, P64, c_size_t, P32, P64]),
+        "orc_minimize_order": (None, [P64, c_size_t, P32]),
+        "orc_minimize_ordered": (c_size_t, [P32, P64, c_size_t, P32, P32]),
+        "orc_exec_hash": (c_uint32, [c_uint32]),
+        "orc_exec_signal_batch": (c_uint64, [P32, P64, P64, c_size_t, P32, P64]),
+        "orc_cover_uncovered": (c_size_t, [P32, c_size_t, c_uint32, P64, P64, c_size_t, P64, c_size_t, P64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+L = _load()
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))
+
+
+def _u64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1))
+
+
+def p32(a):
+    return a.ctypes.data_as(P32)
+
+
+def p64(a):
+    return a.ctypes.data_as(P64)
+
+
+def p8(a):
+    return a.ctypes.data_as(P8)
+
+
+class OSet:
+    """Go map[uint32]struct{} restated (open addressing)."""
+
+    def __init__(self, values=None):
+        self.h = L.orc_set_new()
+        if values is not None:
+            self.add(values)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            L.orc_set_free(self.h)
+            self.h = None
+
+    def __len__(self):
+        return L.orc_set_count(self.h)
+
+    def add(self, values):
+        v = _u32(values)
+        L.orc_signal_add(self.h, p32(v), v.size)
+
+    def has(self, x):
+        return bool(L.orc_set_has(self.h, int(x)))
+
+    def export(self):
+        out = np.empty(max(len(self), 1), dtype=np.uint32)
+        n = L.orc_set_export(self.h, p32(out))
+        return out[:n]
+
+
+def canonicalize(v):
+    a = _u32(v).copy()
+    n = L.orc_canonicalize(p32(a), a.size)
+    return a, n  # full in-place array (Go semantics) and canonical length
+
+
+def foreach(op, a, b):
+    a, b = _u32(a), _u32(b)
+    out = np.empty(a.size + b.size + 1, dtype=np.uint32)
+    n = L.orc_foreach(op, p32(a), a.size, p32(b), b.size, p32(out))
+    return out[:n].copy()
+
+
+def has_difference(a, b):
+    a, b = _u32(a), _u32(b)
+    return bool(L.orc_has_difference(p32(a), a.size, p32(b), b.size))
+
+
+def signal_new(s, sig):
+    v = _u32(sig)
+    return bool(L.orc_signal_new(s.h, p32(v), v.size))
+
+
+def signal_diff(s, sig):
+    v = _u32(sig)
+    out = np.empty(max(v.size, 1), dtype=np.uint32)
+    n = L.orc_signal_diff(s.h, p32(v), v.size, p32(out))
+    return out[:n].copy()
+
+
+def triage_batch(maxset, newset, vals, off):
+    vals, off = _u32(vals), _u64(off)
+    nrec = off.size - 1
+    rec_new = np.zeros(nrec, dtype=np.uint8)
+    dv = np.empty(max(vals.size, 1), dtype=np.uint32)
+    do = np.empty(nrec + 1, dtype=np.uint64)
+    nd = L.orc_triage_batch(maxset.h, newset.h if newset is not None else None, p32(vals), p64(off), nrec, p8(rec_new), p32(dv),
+                            p64(do))
+    return rec_new, dv[:nd].copy(), do
+
+
+def triage_flags_only(maxset, newset, vals, off):
+    vals, off = _u32(vals), _u64(off)
+    nrec = off.size - 1
+    rec_new = np.zeros(nrec, dtype=np.uint8)
+    L.orc_triage_batch(maxset.h, newset.h if newset is not None else None, p32(vals), p64(off), nrec, p8(rec_new), None, None)
+    return rec_new
+
+
+def add_inputs(corpus, maxset, vals, off):
+    vals, off = _u32(vals), _u64(off)
+    L.orc_add_inputs(corpus.h, maxset.h, p32(vals), p64(off), off.size - 1)
+
+
+def accept_batch(corpus_sig, corpus_cov, sv, so, cv=None, co=None):
+    sv, so = _u32(sv), _u64(so)
+    n = so.size - 1
+    acc = np.zeros(n, dtype=np.uint8)
+    if corpus_cov is not None and cv is not None:
+        cv, co = _u32(cv), _u64(co)
+        L.orc_accept_batch(corpus_sig.h, corpus_cov.h, p32(sv), p64(so), p32(cv), p64(co), n, p8(acc))
+    else:
+        L.orc_accept_batch(corpus_sig.h, None, p32(sv), p64(so), None, None, n, p8(acc))
+    return acc
+
+
+def merge_poll(mgr_max, av, ao):
+    av, ao = _u32(av), _u64(ao)
+    npoll = ao.size - 1
+    nv = np.empty(max(av.size, 1), dtype=np.uint32)
+    no = np.empty(npoll + 1, dtype=np.uint64)
+    m = L.orc_merge_poll(mgr_max.h, p32(av), p64(ao), npoll, p32(nv), p64(no))
+    return nv[:m].copy(), no
+
+
+def minimize_order(off):
+    off = _u64(off)
+    n = off.size - 1
+    order = np.empty(max(n, 1), dtype=np.uint32)
+    L.orc_minimize_order(p64(off), n, p32(order))
+    return order[:n].copy()
+
+
+def minimize(vals, off, order=None):
+    vals, off = _u32(vals), _u64(off)
+    n = off.size - 1
+    order = minimize_order(off) if order is None else _u32(order)
+    out = np.empty(max(n, 1), dtype=np.uint32)
+    m = L.orc_minimize_ordered(p32(vals), p64(off), n, p32(order), p32(out))
+    return out[:m].copy()
+
+
+def exec_hash(a):
+    return L.orc_exec_hash(int(a))
+
+
+def exec_signal(pcs, call_off, prog_off):
+    p, co, po = _u32(pcs), _u64(call_off), _u64(prog_off)
+    ncalls = co.size - 1
+    out = np.empty(max(p.size, 1), dtype=np.uint32)
+    so = np.empty(ncalls + 1, dtype=np.uint64)
+    m = L.orc_exec_signal_batch(p32(p), p64(co), p64(po), po.size - 1, p32(out), p64(so))
+    return out[:m].copy(), so
+
+
+def cover_uncovered(cov, base, sym_start, sym_end, all_pcs):
+    c, ss, se, ap = _u32(cov), _u64(sym_start), _u64(sym_end), _u64(all_pcs)
+    out = np.empty(max(ap.size, 1), dtype=np.uint64)
+    n = L.orc_cover_uncovered(p32(c), c.size, base, p64(ss), p64(se), ss.size, p64(ap), ap.size, p64(out))
+    return out[:n].copy()
+
+
+# ---- the compiled reference executor (oracle/_ref) ------------------------------
+_ref = None
+
+
+def ref_executor():
+    """ctypes handle of the reference executor, or None if it was not built."""
+    global _ref
+    if _ref is None and os.path.exists(REF_SO):
+        R = ctypes.CDLL(REF_SO)
+        R.ref_exec_hash.restype = c_uint32
+        R.ref_exec_hash.argtypes = [c_uint32]
+        R.ref_exec_reset.restype = None
+        R.ref_exec_reset.argtypes = []
+        R.ref_exec_dedup.restype = c_int
+        R.ref_exec_dedup.argtypes = [c_uint32]
+        R.ref_exec_call_signal.restype = c_uint32
+        R.ref_exec_call_signal.argtypes = [P32, c_uint32, P32]
+        _ref = R
+    return _ref
+
+
+def ref_exec_signal(pcs, call_off, prog_off):
+    """Per-call signal from the reference executor's own hash()/dedup()."""
+    R = ref_executor()
+    if R is None:
+        raise RuntimeError("oracle/_ref/libref_executor.so not built (needs the reference checkout)")
+    p, co, po = _u32(pcs), _u64(call_off), _u64(prog_off)
+    out = np.empty(max(p.size, 1), dtype=np.uint32)
+    so = np.zeros(co.size, dtype=np.uint64)
+    m = 0
+    for prog in range(po.size - 1):
+        R.ref_exec_reset()  # fresh table per program (fork per program)
+        for c in range(int(po[prog]), int(po[prog + 1])):
+            so[c] = m
+            seg = p[int(co[c]): int(co[c + 1])]
+            tmp = np.empty(max(seg.size, 1), dtype=np.uint32)
+            k = R.ref_exec_call_signal(p32(np.ascontiguousarray(seg)), seg.size, p32(tmp))
+            out[m: m + k] = tmp[:k]
+            m += k
+    so[-1] = m
+    return out[:m].copy(), so

@@ -1,0 +1,107 @@
+"""ctypes binding of libsyzsig.so (include/syzsig.h).
+
+The library is the product: HIP kernels for gfx950 behind a C-ABI.  There is
+no CPU fallback -- if the shared object is missing or no MI355X is present,
+calls fail loudly (ImportError here, SyzSigError from compute calls).
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsyzsig.so")
+
+SG_OK = 0
+SG_EINVAL = -1
+SG_EHIP = -2
+SG_ENOMEM = -3
+SG_ENODEV = -4
+
+OP_DIFFERENCE = 0
+OP_SYMDIFF = 1
+OP_UNION = 2
+OP_INTERSECT = 3
+
+P32 = POINTER(c_uint32)
+P64 = POINTER(c_uint64)
+P8 = POINTER(c_uint8)
+PSZ = POINTER(c_size_t)
+PINT = POINTER(c_int)
+
+# name -> (restype, argtypes); mirrors include/syzsig.h one to one.
+SIGNATURES = {
+    "sg_version": (c_char_p, []),
+    "sg_last_error": (c_char_p, []),
+    "sg_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "sg_ctx_destroy": (None, [c_void_p]),
+    "sg_ctx_sync": (c_int, [c_void_p]),
+    "sg_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "sg_ctx_stream": (c_void_p, [c_void_p]),
+    "sg_ctx_timing": (c_int, [c_void_p, c_int]),
+    "sg_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), P64]),
+    "sg_set_create": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "sg_set_destroy": (None, [c_void_p]),
+    "sg_set_clear": (c_int, [c_void_p]),
+    "sg_set_count": (c_int, [c_void_p, P64]),
+    "sg_set_export": (c_int, [c_void_p, P32, c_size_t, PSZ]),
+    "sg_set_add": (c_int, [c_void_p, P32, c_size_t]),
+    "sg_set_new": (c_int, [c_void_p, P32, c_size_t, PINT]),
+    "sg_set_diff": (c_int, [c_void_p, P32, c_size_t, P32, PSZ]),
+    "sg_set_device_words": (c_void_p, [c_void_p]),
+    "sg_set_wrap_dev": (c_int, [c_void_p, c_void_p, POINTER(c_void_p)]),
+    "sg_set_or_dev": (c_int, [c_void_p, c_void_p]),
+    "sg_set_copy": (c_int, [c_void_p, c_void_p]),
+    "sg_set_count_missing_dev": (c_int, [c_void_p, c_void_p, c_uint64, P64]),
+    "sg_triage_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64, P64]),
+    "sg_triage_batch_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
+                                    c_void_p, c_void_p, c_void_p]),
+    "sg_add_inputs": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t]),
+    "sg_accept_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, P32, P64, c_size_t, P8]),
+    "sg_merge_poll": (c_int, [c_void_p, c_void_p, P32, P64, c_size_t, P32, P64]),
+    "sg_minimize": (c_int, [c_void_p, P32, P64, c_size_t, P32, P32, PSZ]),
+    "sg_minimize_order": (c_int, [P64, c_size_t, P32]),
+    "sg_canonicalize": (c_int, [c_void_p, P32, c_size_t, PSZ]),
+    "sg_canonicalize_batch": (c_int, [c_void_p, P32, P64, c_size_t, P64]),
+    "sg_merge": (c_int, [c_void_p, c_int, P32, c_size_t, P32, c_size_t, P32, PSZ]),
+    "sg_merge_batch": (c_int, [c_void_p, c_int, P32, c_size_t, P64, P64, P32, c_size_t, P64, P64, c_size_t, P32,
+                               c_size_t, P64, P64]),
+    "sg_has_difference": (c_int, [c_void_p, P32, c_size_t, P32, c_size_t, PINT]),
+    "sg_exec_signal": (c_int, [c_void_p, P32, P64, P64, c_size_t, P32, P64]),
+    "sg_exec_signal_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
+                                   c_void_p]),
+    "sg_gen_zipf_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_double, c_uint32, c_uint64, c_uint64, c_uint32,
+                                       c_uint32, c_void_p]),
+    "sg_cover_uncovered": (c_int, [c_void_p, P32, c_size_t, c_uint32, P64, P64, c_size_t, P64, c_size_t, P64, PSZ]),
+}
+
+
+class SyzSigError(RuntimeError):
+    def __init__(self, fn, rc, msg):
+        super().__init__(f"{fn} failed ({rc}): {msg}")
+        self.rc = rc
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C syzkaller_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(fn_name, rc):
+    if rc != SG_OK:
+        msg = lib.sg_last_error()
+        raise SyzSigError(fn_name, rc, msg.decode() if msg else "")
+    return rc
+
+
+def call(fn_name, *args):
+    return check(fn_name, getattr(lib, fn_name)(*args))

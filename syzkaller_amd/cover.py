@@ -1,0 +1,329 @@
+"""Host-side mirror of syzkaller's pkg/cover API and the fuzzer/manager signal
+loops, running on the MI355X through libsyzsig.so.
+
+Names, argument meaning and results follow the reference
+(pkg/cover/cover.go:11-182, syz-fuzzer/fuzzer.go:467-489 and :645-693,
+syz-manager/manager.go:769-784, :907-912, :949-956) so the parity tests read
+like pkg/cover/cover_test.go.  Arrays are numpy uint32 (PCs / signal).  A Go
+`map[uint32]struct{}` is a SignalSet (a 2^32-bit bitmap in HBM).
+
+Empty results are returned as empty arrays (Go returns nil; callers only use
+len, and cover_test.go:54 treats two empty results as equal).
+"""
+import ctypes
+from ctypes import byref, c_double, c_int, c_size_t, c_uint64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, lib
+
+U32 = np.uint32
+U64 = np.uint64
+
+
+def _p32(a):
+    return a.ctypes.data_as(_lib.P32)
+
+
+def _p64(a):
+    return a.ctypes.data_as(_lib.P64)
+
+
+def _p8(a):
+    return a.ctypes.data_as(_lib.P8)
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=U32).reshape(-1))
+
+
+def _u64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=U64).reshape(-1))
+
+
+class Context:
+    """One HIP stream on one MI355X plus the device memory it owns."""
+
+    def __init__(self, device=0):
+        h = c_void_p()
+        call("sg_ctx_create", device, byref(h))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib.sg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        call("sg_ctx_sync", self.h)
+
+    def set_stream(self, hip_stream):
+        call("sg_ctx_set_stream", self.h, c_void_p(hip_stream) if hip_stream else None)
+
+    def timing(self, enable):
+        call("sg_ctx_timing", self.h, 1 if enable else 0)
+
+    def kernel_time(self, name):
+        ms = c_double()
+        n = c_uint64()
+        call("sg_ctx_kernel_time", self.h, name.encode(), byref(ms), byref(n))
+        return ms.value, n.value
+
+
+_default = None
+
+
+def default_context():
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default
+
+
+def _ctx(ctx):
+    return ctx if ctx is not None else default_context()
+
+
+class SignalSet:
+    """map[uint32]struct{} (syz-fuzzer/fuzzer.go:65-68, syz-manager/manager.go:71-73)."""
+
+    def __init__(self, ctx=None):
+        self.ctx = _ctx(ctx)
+        h = c_void_p()
+        call("sg_set_create", self.ctx.h, byref(h))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib.sg_set_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        n = c_uint64()
+        call("sg_set_count", self.h, byref(n))
+        return n.value
+
+    def clear(self):
+        call("sg_set_clear", self.h)
+
+    def export(self):
+        n = c_size_t()
+        call("sg_set_export", self.h, None, 0, byref(n))
+        out = np.empty(n.value, dtype=U32)
+        if n.value:
+            call("sg_set_export", self.h, _p32(out), out.size, byref(n))
+        return out
+
+    def device_words(self):
+        return lib.sg_set_device_words(self.h)
+
+    def or_device(self, ptr):
+        call("sg_set_or_dev", self.h, c_void_p(ptr))
+
+
+# ---- pkg/cover/cover.go:160-182 -------------------------------------------------
+def SignalNew(base, signal):
+    s = _u32(signal)
+    out = c_int()
+    call("sg_set_new", base.h, _p32(s), s.size, byref(out))
+    return bool(out.value)
+
+
+def SignalDiff(base, signal):
+    s = _u32(signal)
+    out = np.empty(s.size, dtype=U32)
+    n = c_size_t()
+    call("sg_set_diff", base.h, _p32(s), s.size, _p32(out), byref(n))
+    return out[: n.value]
+
+
+def SignalAdd(base, signal):
+    s = _u32(signal)
+    call("sg_set_add", base.h, _p32(s), s.size)
+
+
+# ---- pkg/cover/cover.go:28-117 --------------------------------------------------
+def Canonicalize(cov, ctx=None):
+    """In place on a uint32 numpy array (like Go's slice); returns cov[:n]."""
+    if not (isinstance(cov, np.ndarray) and cov.dtype == U32 and cov.flags.c_contiguous):
+        cov = _u32(cov)
+    n = c_size_t()
+    call("sg_canonicalize", _ctx(ctx).h, _p32(cov), cov.size, byref(n))
+    return cov[: n.value]
+
+
+def _merge(op, a, b, ctx):
+    a, b = _u32(a), _u32(b)
+    out = np.empty(a.size + b.size, dtype=U32)
+    n = c_size_t()
+    call("sg_merge", _ctx(ctx).h, op, _p32(a), a.size, _p32(b), b.size, _p32(out), byref(n))
+    return out[: n.value]
+
+
+def Difference(cov0, cov1, ctx=None):
+    return _merge(_lib.OP_DIFFERENCE, cov0, cov1, ctx)
+
+
+def SymmetricDifference(cov0, cov1, ctx=None):
+    return _merge(_lib.OP_SYMDIFF, cov0, cov1, ctx)
+
+
+def Union(cov0, cov1, ctx=None):
+    return _merge(_lib.OP_UNION, cov0, cov1, ctx)
+
+
+def Intersection(cov0, cov1, ctx=None):
+    return _merge(_lib.OP_INTERSECT, cov0, cov1, ctx)
+
+
+def HasDifference(cov0, cov1, ctx=None):
+    a, b = _u32(cov0), _u32(cov1)
+    out = c_int()
+    call("sg_has_difference", _ctx(ctx).h, _p32(a), a.size, _p32(b), b.size, byref(out))
+    return bool(out.value)
+
+
+def to_csr(lists):
+    lens = np.array([len(x) for x in lists], dtype=U64)
+    off = np.zeros(len(lists) + 1, dtype=U64)
+    np.cumsum(lens, out=off[1:])
+    vals = np.concatenate([_u32(x) for x in lists]) if lists else np.empty(0, dtype=U32)
+    return _u32(vals), off
+
+
+def minimize_order(off):
+    off = _u64(off)
+    n = off.size - 1
+    order = np.empty(n, dtype=U32)
+    call("sg_minimize_order", _p64(off), n, _p32(order))
+    return order
+
+
+def minimize_csr(vals, off, order=None, ctx=None):
+    vals, off = _u32(vals), _u64(off)
+    n = off.size - 1
+    order = minimize_order(off) if order is None else _u32(order)
+    out = np.empty(n, dtype=U32)
+    m = c_size_t()
+    call("sg_minimize", _ctx(ctx).h, _p32(vals), _p64(off), n, _p32(order), _p32(out), byref(m))
+    return out[: m.value]
+
+
+def Minimize(corpus, ctx=None):
+    """pkg/cover/cover.go:120-146, including its sort.Sort order."""
+    vals, off = to_csr(corpus)
+    return [int(i) for i in minimize_csr(vals, off, None, ctx)]
+
+
+# ---- batched hot path -------------------------------------------------------------
+def triage_batch(maxset, newset, vals, rec_off, want_diff=True, ctx=None):
+    """syz-fuzzer/fuzzer.go:645-693 over a batch of call records.
+
+    Returns (rec_new uint8[nrec], diff_vals, diff_off) -- diff_* None if not
+    requested."""
+    vals, off = _u32(vals), _u64(rec_off)
+    nrec = off.size - 1
+    rec_new = np.zeros(nrec, dtype=np.uint8)
+    c = maxset.ctx if ctx is None else ctx
+    if want_diff:
+        dv = np.empty(max(vals.size, 1), dtype=U32)
+        do = np.empty(nrec + 1, dtype=U64)
+        nd = c_uint64()
+        call("sg_triage_batch", c.h, maxset.h, newset.h if newset is not None else None, _p32(vals), _p64(off), nrec,
+             _p8(rec_new), _p32(dv), _p64(do), byref(nd))
+        return rec_new, dv[: nd.value], do
+    call("sg_triage_batch", c.h, maxset.h, newset.h if newset is not None else None, _p32(vals), _p64(off), nrec, _p8(rec_new),
+         None, None, None)
+    return rec_new, None, None
+
+
+def add_inputs(corpus, maxset, vals, off, ctx=None):
+    """syz-fuzzer/fuzzer.go:467-489 addInput over a batch of inputs."""
+    vals, off = _u32(vals), _u64(off)
+    c = corpus.ctx if ctx is None else ctx
+    call("sg_add_inputs", c.h, corpus.h, maxset.h, _p32(vals), _p64(off), off.size - 1)
+
+
+def accept_batch(corpus_sig, corpus_cov, sig_vals, sig_off, cov_vals=None, cov_off=None, ctx=None):
+    """syz-manager/manager.go:907-912 NewInput acceptance over a batch."""
+    sv, so = _u32(sig_vals), _u64(sig_off)
+    n = so.size - 1
+    acc = np.zeros(n, dtype=np.uint8)
+    c = corpus_sig.ctx if ctx is None else ctx
+    if corpus_cov is not None and cov_vals is not None:
+        cv, co = _u32(cov_vals), _u64(cov_off)
+        call("sg_accept_batch", c.h, corpus_sig.h, corpus_cov.h, _p32(sv), _p64(so), _p32(cv), _p64(co), n, _p8(acc))
+    else:
+        call("sg_accept_batch", c.h, corpus_sig.h, None, _p32(sv), _p64(so), None, None, n, _p8(acc))
+    return acc
+
+
+def merge_poll(mgr_max, a_vals, a_off, ctx=None):
+    """syz-manager/manager.go:949-956 over polls in arrival order."""
+    av, ao = _u32(a_vals), _u64(a_off)
+    npoll = ao.size - 1
+    nv = np.empty(max(av.size, 1), dtype=U32)
+    no = np.empty(npoll + 1, dtype=U64)
+    c = mgr_max.ctx if ctx is None else ctx
+    call("sg_merge_poll", c.h, mgr_max.h, _p32(av), _p64(ao), npoll, _p32(nv), _p64(no))
+    return nv[: int(no[-1])], no
+
+
+def canonicalize_batch(vals, off, ctx=None):
+    """Batched Canonicalize in place; returns per-segment canonical lengths."""
+    if not (isinstance(vals, np.ndarray) and vals.dtype == U32 and vals.flags.c_contiguous):
+        raise TypeError("canonicalize_batch works in place on a contiguous uint32 array")
+    off = _u64(off)
+    n = off.size - 1
+    lens = np.zeros(n, dtype=U64)
+    call("sg_canonicalize_batch", _ctx(ctx).h, _p32(vals), _p64(off), n, _p64(lens))
+    return lens
+
+
+def merge_batch(op, a, a_beg, a_len, b, b_beg, b_len, ctx=None):
+    a, b = _u32(a), _u32(b)
+    ab, al, bb, bl = _u64(a_beg), _u64(a_len), _u64(b_beg), _u64(b_len)
+    npair = ab.size
+    ob = np.zeros(npair, dtype=U64)
+    if npair > 1:
+        np.cumsum(al[:-1] + bl[:-1], out=ob[1:])
+    total = int((al + bl).sum())
+    out = np.empty(max(total, 1), dtype=U32)
+    ol = np.zeros(npair, dtype=U64)
+    call("sg_merge_batch", _ctx(ctx).h, op, _p32(a), a.size, _p64(ab), _p64(al), _p32(b), b.size, _p64(bb),
+         _p64(bl), npair, _p32(out), out.size, _p64(ob), _p64(ol))
+    return [out[int(ob[k]): int(ob[k] + ol[k])] for k in range(npair)]
+
+
+def exec_signal(pcs, call_off, prog_off, ctx=None):
+    """executor/executor.h:389-401 + :497-526 over a batch of programs."""
+    p, co, po = _u32(pcs), _u64(call_off), _u64(prog_off)
+    ncalls = co.size - 1
+    sv = np.empty(max(p.size, 1), dtype=U32)
+    so = np.empty(ncalls + 1, dtype=U64)
+    call("sg_exec_signal", _ctx(ctx).h, _p32(p), _p64(co), _p64(po), po.size - 1, _p32(sv), _p64(so))
+    return sv[: int(so[-1])], so
+
+
+def cover_uncovered(cov, base, sym_start, sym_end, all_pcs, ctx=None):
+    """syz-manager/cover.go:91-103 + uncoveredPcsInFuncs (:257-307); ascending."""
+    c, ss, se, ap = _u32(cov), _u64(sym_start), _u64(sym_end), _u64(all_pcs)
+    out = np.empty(max(ap.size, 1), dtype=U64)
+    n = c_size_t()
+    call("sg_cover_uncovered", _ctx(ctx).h, _p32(c), c.size, base, _p64(ss), _p64(se), ss.size, _p64(ap), ap.size,
+         _p64(out), byref(n))
+    return out[: n.value]

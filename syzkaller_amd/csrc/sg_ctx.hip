@@ -1,0 +1,665 @@
+// sg_ctx.hip -- context, workspace, timing, device scan and the signal-set
+// (map[uint32]struct{} replacement) entry points of libsyzsig.so.
+//
+// Reference: the Go maps maxSignal / corpusSignal / newSignal
+// (syz-fuzzer/fuzzer.go:65-68, syz-manager/manager.go:71-73) and the map
+// helpers SignalNew / SignalDiff / SignalAdd (pkg/cover/cover.go:160-182).
+// A set is a 2^32-bit bitmap in HBM: membership of s is bit s of word s>>5.
+#include "sg_internal.h"
+
+#include <cstring>
+
+namespace sg {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  set_error("HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+  if (e == hipErrorOutOfMemory) return SG_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorNoBinaryForGpu) return SG_ENODEV;
+  return SG_EHIP;
+}
+
+int ensure_device(sg_ctx* ctx) {
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  return SG_OK;
+}
+
+int ws_reserve(sg_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->ws_cap) return SG_OK;
+  size_t cap = ctx->ws_cap ? ctx->ws_cap : (64u << 20);
+  while (cap < bytes) cap *= 2;
+  if (ctx->ws) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    SG_HIP(hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_cap = 0;
+  }
+  SG_HIP(hipMalloc(&ctx->ws, cap));
+  ctx->ws_cap = cap;
+  return SG_OK;
+}
+
+int pin_reserve(sg_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->pin_cap) return SG_OK;
+  size_t cap = ctx->pin_cap ? ctx->pin_cap : (16u << 20);
+  while (cap < bytes) cap *= 2;
+  if (ctx->pin) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    SG_HIP(hipHostFree(ctx->pin));
+    ctx->pin = nullptr;
+    ctx->pin_cap = 0;
+  }
+  SG_HIP(hipHostMalloc(&ctx->pin, cap, hipHostMallocDefault));
+  ctx->pin_cap = cap;
+  return SG_OK;
+}
+
+int owner_keys(sg_ctx* ctx, uint64_t nkeys, uint32_t* key_lo) {
+  if (nkeys >= kOwnerInf) {
+    set_error("batch of %llu keys exceeds the 32-bit first-owner key space", (unsigned long long)nkeys);
+    return SG_EINVAL;
+  }
+  if (!ctx->owner) {
+    SG_HIP(hipMalloc(&ctx->owner, kOwnerEntries * sizeof(uint32_t)));
+    SG_HIP(hipMemsetAsync(ctx->owner, 0xFF, kOwnerEntries * sizeof(uint32_t), ctx->stream));
+    ctx->owner_floor = kOwnerInf;
+  }
+  if (ctx->owner_floor < nkeys) {
+    // Key space exhausted (after ~4G keys): start a fresh generation.
+    SG_HIP(hipMemsetAsync(ctx->owner, 0xFF, kOwnerEntries * sizeof(uint32_t), ctx->stream));
+    ctx->owner_floor = kOwnerInf;
+  }
+  ctx->owner_floor -= nkeys;
+  *key_lo = (uint32_t)ctx->owner_floor;
+  return SG_OK;
+}
+
+// ---- kernel timing ---------------------------------------------------------
+void timer_begin(sg_ctx* ctx, const char* name, int* slot) {
+  KernelTimer& t = ctx->timer;
+  *slot = -1;
+  if (!t.enabled) return;
+  auto it = t.ids.find(name);
+  int id;
+  if (it == t.ids.end()) {
+    id = (int)t.names.size();
+    t.ids[name] = id;
+    t.names.push_back(name);
+    t.ms.push_back(0);
+    t.count.push_back(0);
+  } else {
+    id = it->second;
+  }
+  hipEvent_t a, b;
+  if (t.pool.size() >= 2) {
+    a = t.pool.back();
+    t.pool.pop_back();
+    b = t.pool.back();
+    t.pool.pop_back();
+  } else {
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+  }
+  hipEventRecord(a, ctx->stream);
+  t.pending.push_back({id, a, b});
+  *slot = (int)t.pending.size() - 1;
+}
+
+void timer_end(sg_ctx* ctx, int slot) {
+  if (slot < 0) return;
+  hipEventRecord(ctx->timer.pending[slot].b, ctx->stream);
+}
+
+static void timer_collect(sg_ctx* ctx) {
+  KernelTimer& t = ctx->timer;
+  for (auto& r : t.pending) {
+    hipEventSynchronize(r.b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, r.a, r.b);
+    t.ms[r.id] += ms;
+    t.count[r.id] += 1;
+    t.pool.push_back(r.a);
+    t.pool.push_back(r.b);
+  }
+  t.pending.clear();
+}
+
+// ---- device scan: exclusive prefix of u32 counts into u64 offsets ----------
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kBlock * kScanItems;  // 4096
+
+__global__ __launch_bounds__(kBlock) void k_scan_tile(const uint32_t* __restrict__ in, uint64_t n,
+                                                      uint64_t* __restrict__ out, uint64_t* __restrict__ tile_sum) {
+  __shared__ uint64_t part[kBlock];
+  uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; i++) {
+    uint64_t idx = base + i;
+    v[i] = idx < n ? in[idx] : 0u;
+    s += v[i];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  // Hillis-Steele over 256 partials (inclusive)
+  for (int d = 1; d < kBlock; d <<= 1) {
+    uint64_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; i++) {
+    uint64_t idx = base + i;
+    if (idx < n) out[idx] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == kBlock - 1) tile_sum[blockIdx.x] = part[kBlock - 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_u64_tile(uint64_t* __restrict__ data, uint64_t n,
+                                                          uint64_t* __restrict__ tile_sum) {
+  // in-place exclusive scan of u64 values, per 4096-tile
+  __shared__ uint64_t part[kBlock];
+  uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint64_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; i++) {
+    uint64_t idx = base + i;
+    v[i] = idx < n ? data[idx] : 0u;
+    s += v[i];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < kBlock; d <<= 1) {
+    uint64_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; i++) {
+    uint64_t idx = base + i;
+    if (idx < n) data[idx] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == kBlock - 1) tile_sum[blockIdx.x] = part[kBlock - 1];
+}
+
+__global__ void k_scan_add(uint64_t* __restrict__ out, uint64_t n, const uint64_t* __restrict__ tile_base) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += tile_base[i / kScanTile];
+}
+
+__global__ void k_scan_total(uint64_t* out, uint64_t n, const uint64_t* tile_base, const uint64_t* tile_sum,
+                             uint64_t ntiles) {
+  out[n] = ntiles ? tile_base[ntiles - 1] + tile_sum[ntiles - 1] : 0;
+}
+
+size_t scan_ws_bytes(uint64_t n) {
+  size_t b = 0;
+  while (n > 1) {
+    uint64_t t = (n + kScanTile - 1) / kScanTile;
+    b += 2 * ((t * 8 + 255) & ~255ull);
+    n = t;
+  }
+  return b + 512;
+}
+
+static int scan_u64_inplace(sg_ctx* ctx, uint64_t* data, uint64_t n, char* scratch) {
+  // exclusive in-place scan of n u64 values (used for tile sums)
+  if (n == 0) return SG_OK;
+  uint64_t nt = (n + kScanTile - 1) / kScanTile;
+  uint64_t* sums = (uint64_t*)scratch;
+  char* next = scratch + ((nt * 8 + 255) & ~255ull);
+  hipLaunchKernelGGL(k_scan_u64_tile, dim3((uint32_t)nt), dim3(kBlock), 0, ctx->stream, data, n, sums);
+  if (nt > 1) {
+    int rc = scan_u64_inplace(ctx, sums, nt, next);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, data, n, sums);
+  }
+  return SG_OK;
+}
+
+int scan_counts(sg_ctx* ctx, const uint32_t* d_in, uint64_t* d_out, uint64_t n, size_t ws_used) {
+  ScopedTimer tm(ctx, "scan");
+  char* scratch = (char*)ctx->ws + ws_used;
+  uint64_t nt = n ? (n + kScanTile - 1) / kScanTile : 0;
+  uint64_t* sums = (uint64_t*)scratch;
+  uint64_t* bases = (uint64_t*)(scratch + ((nt * 8 + 255) & ~255ull));
+  char* next = (char*)bases + ((nt * 8 + 255) & ~255ull);
+  if (n == 0) {
+    SG_HIP(hipMemsetAsync(d_out, 0, 8, ctx->stream));
+    return SG_OK;
+  }
+  hipLaunchKernelGGL(k_scan_tile, dim3((uint32_t)nt), dim3(kBlock), 0, ctx->stream, d_in, n, d_out, sums);
+  SG_HIP(hipMemcpyAsync(bases, sums, nt * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  int rc = scan_u64_inplace(ctx, bases, nt, next);
+  if (rc) return rc;
+  if (nt > 1) hipLaunchKernelGGL(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_out, n, bases);
+  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, ctx->stream, d_out, n, bases, sums, nt);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+// ---- set kernels -----------------------------------------------------------
+__global__ void k_set_add(uint32_t* __restrict__ words, const uint32_t* __restrict__ sig, uint64_t n) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    sgd::set_bit(words, sig[i]);
+}
+
+__global__ void k_set_or(uint32_t* __restrict__ words, const uint32_t* __restrict__ other) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kSetWords / 4; i += stride) {
+    uint4 a = reinterpret_cast<uint4*>(words)[i];
+    uint4 b = reinterpret_cast<const uint4*>(other)[i];
+    a.x |= b.x;
+    a.y |= b.y;
+    a.z |= b.z;
+    a.w |= b.w;
+    reinterpret_cast<uint4*>(words)[i] = a;
+  }
+}
+
+__global__ void k_set_new(const uint32_t* __restrict__ words, const uint32_t* __restrict__ sig, uint64_t n,
+                          uint64_t* __restrict__ flag) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool miss = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    miss |= !sgd::test_bit(words, sig[i]);
+  if (__any(miss) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+__global__ void k_count_missing(const uint32_t* __restrict__ words, const uint32_t* __restrict__ v, uint64_t n,
+                                unsigned long long* __restrict__ out) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    c += !sgd::test_bit(words, v[i]);
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
+// popcount of the bitmap, per 4096-word tile (for count and export)
+__global__ __launch_bounds__(kBlock) void k_set_tile_pop(const uint32_t* __restrict__ words,
+                                                         uint32_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t red[kBlock / 64];
+  const uint4* w4 = reinterpret_cast<const uint4*>(words) + (uint64_t)blockIdx.x * (kTile / 4);
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kTile / 4 / kBlock; j++) {
+    uint4 v = w4[j * kBlock + threadIdx.x];
+    c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// each thread owns 16 consecutive words of the tile; block-scan of their
+// popcounts gives each thread's first output slot.
+__global__ __launch_bounds__(kBlock) void k_set_export(const uint32_t* __restrict__ words,
+                                                       const uint64_t* __restrict__ tile_base,
+                                                       uint32_t* __restrict__ out, uint64_t cap) {
+  __shared__ uint32_t part[kBlock];
+  uint64_t w0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * 16;
+  uint64_t tb = tile_base[blockIdx.x];
+  if (tile_base[blockIdx.x + 1] == tb) return;  // empty tile (block-uniform)
+  const uint4* w4 = reinterpret_cast<const uint4*>(words + w0);
+  uint32_t w[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint4 v = w4[j];
+    w[4 * j] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+    c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+  }
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (int d = 1; d < kBlock; d <<= 1) {
+    uint32_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t pos = tb + part[threadIdx.x] - c;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    uint32_t x = w[j];
+    while (x) {
+      int b = __ffs(x) - 1;
+      x &= x - 1;
+      if (pos < cap) out[pos] = (uint32_t)((w0 + j) * 32 + b);
+      pos++;
+    }
+  }
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+// ---- C-ABI -------------------------------------------------------------------
+extern "C" {
+
+const char* sg_version(void) { return "syzsig 0.1 gfx950"; }
+const char* sg_last_error(void) { return g_err.c_str(); }
+
+int sg_ctx_create(int device, sg_ctx** out) {
+  if (!out) {
+    set_error("sg_ctx_create: out is NULL");
+    return SG_EINVAL;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    set_error("no HIP device available (libsyzsig has no CPU path)");
+    return SG_ENODEV;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("device %d out of range (%d devices)", device, ndev);
+    return SG_EINVAL;
+  }
+  hipDeviceProp_t prop;
+  SG_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("device %d is %s; libsyzsig is built for gfx950 (MI355X) only", device, prop.gcnArchName);
+    return SG_ENODEV;
+  }
+  sg_ctx* c = new sg_ctx();
+  c->device = device;
+  int rc = ensure_device(c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  c->stream = c->own_stream;
+  e = hipMalloc(&c->dscal, 256);
+  if (e != hipSuccess) {
+    hipStreamDestroy(c->own_stream);
+    delete c;
+    return hip_fail(e, "hipMalloc(dscal)");
+  }
+  *out = c;
+  return SG_OK;
+}
+
+void sg_ctx_destroy(sg_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (auto& r : ctx->timer.pending) {
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  for (auto ev : ctx->timer.pool) hipEventDestroy(ev);
+  if (ctx->ws) hipFree(ctx->ws);
+  if (ctx->pin) hipHostFree(ctx->pin);
+  if (ctx->owner) hipFree(ctx->owner);
+  if (ctx->dscal) hipFree(ctx->dscal);
+  if (ctx->gen_prob) hipFree(ctx->gen_prob);
+  if (ctx->gen_alias) hipFree(ctx->gen_alias);
+  if (ctx->gen_perm) hipFree(ctx->gen_perm);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+int sg_ctx_sync(sg_ctx* ctx) {
+  if (!ctx) return SG_EINVAL;
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream) {
+  if (!ctx) return SG_EINVAL;
+  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  return SG_OK;
+}
+
+void* sg_ctx_stream(sg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int sg_ctx_timing(sg_ctx* ctx, int enable) {
+  if (!ctx) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  timer_collect(ctx);
+  KernelTimer& t = ctx->timer;
+  for (auto& v : t.ms) v = 0;
+  for (auto& v : t.count) v = 0;
+  t.enabled = enable != 0;
+  return SG_OK;
+}
+
+int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* launches) {
+  if (!ctx || !name) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  timer_collect(ctx);
+  KernelTimer& t = ctx->timer;
+  auto it = t.ids.find(name);
+  if (ms) *ms = it == t.ids.end() ? 0 : t.ms[it->second];
+  if (launches) *launches = it == t.ids.end() ? 0 : t.count[it->second];
+  return SG_OK;
+}
+
+int sg_set_create(sg_ctx* ctx, sg_set** out) {
+  if (!ctx || !out) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  sg_set* s = new sg_set();
+  s->ctx = ctx;
+  hipError_t e = hipMalloc(&s->words, kSetBytes);
+  if (e != hipSuccess) {
+    delete s;
+    return hip_fail(e, "hipMalloc(set)");
+  }
+  e = hipMemsetAsync(s->words, 0, kSetBytes, ctx->stream);
+  if (e != hipSuccess) {
+    hipFree(s->words);
+    delete s;
+    return hip_fail(e, "hipMemset(set)");
+  }
+  *out = s;
+  return SG_OK;
+}
+
+void sg_set_destroy(sg_set* set) {
+  if (!set) return;
+  hipSetDevice(set->ctx->device);
+  hipStreamSynchronize(set->ctx->stream);
+  if (set->owned) hipFree(set->words);
+  delete set;
+}
+
+int sg_set_clear(sg_set* set) {
+  if (!set) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  SG_HIP(hipMemsetAsync(set->words, 0, kSetBytes, ctx->stream));
+  return SG_OK;
+}
+
+void* sg_set_device_words(sg_set* set) { return set ? set->words : nullptr; }
+
+int sg_set_wrap_dev(sg_ctx* ctx, void* d_words, sg_set** out) {
+  if (!ctx || !d_words || !out || ((uintptr_t)d_words & 15)) {
+    set_error("sg_set_wrap_dev: invalid argument (words must be 16-B aligned device memory)");
+    return SG_EINVAL;
+  }
+  sg_set* s = new sg_set();
+  s->ctx = ctx;
+  s->words = (uint32_t*)d_words;
+  s->owned = false;
+  *out = s;
+  return SG_OK;
+}
+
+int sg_set_copy(sg_set* dst, sg_set* src) {
+  if (!dst || !src || dst->ctx != src->ctx) return SG_EINVAL;
+  sg_ctx* ctx = dst->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  if (dst != src) SG_HIP(hipMemcpyAsync(dst->words, src->words, kSetBytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return SG_OK;
+}
+
+int sg_set_count_missing_dev(sg_set* set, const uint32_t* d_vals, uint64_t n, uint64_t* out) {
+  if (!set || !out || (n && !d_vals)) return SG_EINVAL;
+  *out = 0;
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  SG_HIP(hipMemsetAsync(ctx->dscal, 0, 8, ctx->stream));
+  hipLaunchKernelGGL(k_count_missing, dim3(2048), dim3(256), 0, ctx->stream, set->words, d_vals, n,
+                     (unsigned long long*)ctx->dscal);
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out, ctx->dscal, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_set_or_dev(sg_set* set, const uint32_t* d_words) {
+  if (!set || !d_words) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_set_or, dim3(4096), dim3(256), 0, ctx->stream, set->words, d_words);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+static int set_tile_bases(sg_set* set, uint64_t** bases_out, uint64_t* total) {
+  sg_ctx* ctx = set->ctx;
+  const uint64_t ntile = kSetWords / kTile;  // 32768
+  WsPlan p;
+  size_t o_cnt = p.add(ntile * 4);
+  size_t o_base = p.add((ntile + 1) * 8);
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(ntile));
+  if (rc) return rc;
+  uint32_t* cnt = (uint32_t*)ws_at(ctx, o_cnt);
+  uint64_t* base = (uint64_t*)ws_at(ctx, o_base);
+  hipLaunchKernelGGL(k_set_tile_pop, dim3((uint32_t)ntile), dim3(kBlock), 0, ctx->stream, set->words, cnt);
+  rc = scan_counts(ctx, cnt, base, ntile, p.total);
+  if (rc) return rc;
+  SG_HIP(hipMemcpyAsync(total, base + ntile, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  *bases_out = base;
+  return SG_OK;
+}
+
+int sg_set_count(sg_set* set, uint64_t* out) {
+  if (!set || !out) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  uint64_t* bases;
+  return set_tile_bases(set, &bases, out);
+}
+
+int sg_set_export(sg_set* set, uint32_t* out, size_t cap, size_t* n) {
+  if (!set || !n || (cap && !out)) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  uint64_t* bases;
+  uint64_t total = 0;
+  rc = set_tile_bases(set, &bases, &total);
+  if (rc) return rc;
+  *n = (size_t)total;
+  uint64_t m = total < cap ? total : cap;
+  if (m == 0) return SG_OK;
+  // output staged in the workspace after the scan area
+  size_t used = ((kSetWords / kTile) * 4 + 255) / 256 * 256 + (((kSetWords / kTile) + 1) * 8 + 255) / 256 * 256;
+  size_t o_out = used + scan_ws_bytes(kSetWords / kTile);
+  o_out = (o_out + 255) & ~size_t(255);
+  rc = ws_reserve(ctx, o_out + m * 4);
+  if (rc) return rc;
+  // ws may have been reallocated: recompute the tile bases if so
+  rc = set_tile_bases(set, &bases, &total);
+  if (rc) return rc;
+  uint32_t* dout = (uint32_t*)ws_at(ctx, o_out);
+  hipLaunchKernelGGL(k_set_export, dim3((uint32_t)(kSetWords / kTile)), dim3(kBlock), 0, ctx->stream, set->words,
+                     bases, dout, (uint64_t)m);
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out, dout, m * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_set_add(sg_set* set, const uint32_t* sig, size_t n) {
+  if (!set || (n && !sig)) return SG_EINVAL;
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  rc = ws_reserve(ctx, n * 4);
+  if (rc) return rc;
+  uint32_t* d = (uint32_t*)ctx->ws;
+  SG_HIP(hipMemcpyAsync(d, sig, n * 4, hipMemcpyHostToDevice, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "set_add");
+    hipLaunchKernelGGL(k_set_add, dim3(std::min<uint64_t>(div_up(n, 256), 8192)), dim3(256), 0, ctx->stream,
+                       set->words, d, (uint64_t)n);
+  }
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_set_new(sg_set* set, const uint32_t* sig, size_t n, int* out) {
+  if (!set || !out || (n && !sig)) return SG_EINVAL;
+  *out = 0;
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  rc = ws_reserve(ctx, n * 4);
+  if (rc) return rc;
+  uint32_t* d = (uint32_t*)ctx->ws;
+  SG_HIP(hipMemcpyAsync(d, sig, n * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemsetAsync(ctx->dscal, 0, 8, ctx->stream));
+  hipLaunchKernelGGL(k_set_new, dim3(std::min<uint64_t>(div_up(n, 256), 8192)), dim3(256), 0, ctx->stream,
+                     set->words, d, (uint64_t)n, ctx->dscal);
+  SG_HIP(hipGetLastError());
+  uint64_t flag = 0;
+  SG_HIP(hipMemcpyAsync(&flag, ctx->dscal, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  *out = flag ? 1 : 0;
+  return SG_OK;
+}
+
+}  // extern "C"

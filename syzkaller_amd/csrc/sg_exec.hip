@@ -1,0 +1,276 @@
+// sg_exec.hip -- executor edge signal (trace -> per-call signal) and the
+// synthetic Zipf trace generator.
+//
+// Reference: executor/executor.h:389-401 (the signal loop of
+// handle_completion), :497-505 hash(), :507-526 dedup(); the dedup table is
+// fresh per program because the executor forks a child per program
+// (executor/executor_linux.cc:174-194) and shared by that program's calls.
+//
+// The dedup decisions are inherently sequential within a program (each
+// insert can change later lookups), so one wave owns one program and its
+// 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 64
+// edges at a time in parallel (pc ^ hash(prev pc) needs only a neighbour
+// shuffle); the table walk of one edge is one 4-lane LDS probe plus two
+// ballots, decided in scalar registers; kept edges are written with one
+// coalesced compaction store per 64 PCs.
+#include "sg_internal.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace sg {
+
+constexpr uint32_t kDedupSize = 8192;  // executor.h:506
+
+__device__ __forceinline__ uint32_t exec_hash(uint32_t a) {  // executor.h:497-505
+  a = (a ^ 61) ^ (a >> 16);
+  a = a + (a << 3);
+  a = a ^ (a >> 4);
+  a = a * 0x27d4eb2du;
+  a = a ^ (a >> 15);
+  return a;
+}
+
+__global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__ pcs,
+                                                    const uint64_t* __restrict__ call_off,
+                                                    const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
+                                                    uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t table[kDedupSize];
+  const int lane = threadIdx.x;
+  const uint64_t p = blockIdx.x;
+  for (uint32_t i = lane; i < kDedupSize; i += 64) table[i] = 0;
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t c0 = prog_off[p], c1 = prog_off[p + 1];
+  for (uint64_t c = c0; c < c1; c++) {
+    const uint64_t b = call_off[c], e = call_off[c + 1];
+    uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
+    uint64_t outpos = b;
+    for (uint64_t j = b; j < e; j += 64) {
+      const uint64_t idx = j + lane;
+      const bool valid = idx < e;
+      const uint32_t pc = valid ? pcs[idx] : 0u;
+      const uint32_t h = exec_hash(pc);
+      uint32_t hprev = __shfl_up(h, 1);
+      if (lane == 0) hprev = carry;
+      const uint32_t sig = pc ^ hprev;  // executor.h:393-395
+      const int nvalid = (int)((e - j) < 64 ? (e - j) : 64);
+      carry = __shfl(h, nvalid - 1);
+      uint64_t keep = 0;
+      for (int i = 0; i < nvalid; i++) {
+        const uint32_t s = __builtin_amdgcn_readlane(sig, i);
+        // executor.h:509-525: probe (s+q) % 8192 for q = 0..3 in order; a
+        // slot equal to s means duplicate, an empty slot takes s, and when
+        // all four are taken slot s % 8192 is overwritten.
+        const uint32_t t = lane < 4 ? table[(s + (uint32_t)lane) & (kDedupSize - 1)] : 1u;
+        const uint64_t eqm = __ballot(lane < 4 && t == s);
+        const uint64_t zm = __ballot(lane < 4 && t == 0u);
+        const uint64_t any = (eqm | zm) & 0xFull;
+        if (any) {
+          const int q = __ffsll((unsigned long long)any) - 1;
+          if ((eqm >> q) & 1ull) continue;  // dedup() == true: not written
+          if (lane == 0) table[(s + (uint32_t)q) & (kDedupSize - 1)] = s;
+        } else {
+          if (lane == 0) table[s & (kDedupSize - 1)] = s;
+        }
+        keep |= 1ull << i;
+      }
+      if ((keep >> lane) & 1ull) tmp[outpos + __popcll(keep & lt)] = sig;
+      outpos += __popcll(keep);
+    }
+    if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
+  }
+}
+
+// dense CSR from the per-call capacity layout: one wave per call
+__global__ __launch_bounds__(256) void k_exec_compact(const uint32_t* __restrict__ tmp,
+                                                      const uint64_t* __restrict__ call_off,
+                                                      const uint64_t* __restrict__ sig_off, uint64_t ncalls,
+                                                      uint32_t* __restrict__ out) {
+  uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= ncalls) return;
+  const int lane = threadIdx.x & 63;
+  uint64_t src = call_off[c], dst = sig_off[c], n = sig_off[c + 1] - sig_off[c];
+  for (uint64_t i = lane; i < n; i += 64) out[dst + i] = tmp[src + i];
+}
+
+// ---- Zipf generator ----------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_gen_traces(uint64_t seed, uint32_t nranks, uint64_t g0, uint64_t n, const uint32_t* __restrict__ prob,
+                             const uint32_t* __restrict__ alias, const uint32_t* __restrict__ perm,
+                             uint32_t* __restrict__ out) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ull * (g0 + i + 1));
+    uint32_t bucket = (uint32_t)(((h >> 32) * (uint64_t)nranks) >> 32);
+    uint32_t frac = (uint32_t)h;
+    uint32_t rank = frac < prob[bucket] ? bucket : alias[bucket];
+    out[i] = 0x81000000u + 16u * perm[rank];
+  }
+}
+
+// Vose alias tables for Zipf(s) over ranks 1..N (rank r has weight r^-s) and a
+// seeded Fisher-Yates permutation rank -> pc slot.  Host-side, deterministic.
+static void build_zipf_tables(uint64_t seed, double s, uint32_t N, std::vector<uint32_t>& prob,
+                              std::vector<uint32_t>& alias, std::vector<uint32_t>& perm) {
+  std::vector<double> q(N);
+  double sum = 0;
+  for (uint32_t k = 0; k < N; k++) {
+    q[k] = std::pow((double)(k + 1), -s);
+    sum += q[k];
+  }
+  for (uint32_t k = 0; k < N; k++) q[k] = q[k] * N / sum;
+  prob.assign(N, 0);
+  alias.assign(N, 0);
+  std::vector<uint32_t> small, large;
+  for (uint32_t k = 0; k < N; k++) (q[k] < 1.0 ? small : large).push_back(k);
+  while (!small.empty() && !large.empty()) {
+    uint32_t l = small.back();
+    small.pop_back();
+    uint32_t g = large.back();
+    large.pop_back();
+    double t = q[l] * 4294967296.0;
+    prob[l] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    alias[l] = g;
+    q[g] = (q[g] + q[l]) - 1.0;
+    (q[g] < 1.0 ? small : large).push_back(g);
+  }
+  for (uint32_t k : large) {
+    prob[k] = 0xFFFFFFFFu;
+    alias[k] = k;
+  }
+  for (uint32_t k : small) {
+    prob[k] = 0xFFFFFFFFu;
+    alias[k] = k;
+  }
+  perm.resize(N);
+  for (uint32_t k = 0; k < N; k++) perm[k] = k;
+  uint64_t st = seed ^ 0x5EEDC0DEull;
+  for (uint32_t k = N - 1; k > 0; k--) {
+    st += 0x9E3779B97F4A7C15ull;
+    uint64_t r = mix64(st);
+    uint32_t j = (uint32_t)(((r >> 32) * (uint64_t)(k + 1)) >> 32);
+    uint32_t t = perm[k];
+    perm[k] = perm[j];
+    perm[j] = t;
+  }
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
+                       uint64_t nprog, uint64_t ncalls, uint64_t npcs, uint32_t* d_sig_vals, uint64_t* d_sig_off) {
+  if (!ctx || !d_call_off || !d_prog_off || !d_sig_off || (npcs && (!d_pcs || !d_sig_vals))) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  if (ncalls == 0) {
+    SG_HIP(hipMemsetAsync(d_sig_off, 0, 8, ctx->stream));
+    return SG_OK;
+  }
+  WsPlan p;
+  size_t o_tmp = p.add(npcs * 4), o_cnt = p.add(ncalls * 4);
+  size_t scan_off = p.total;
+  rc = ws_reserve(ctx, p.total + scan_ws_bytes(ncalls));
+  if (rc) return rc;
+  uint32_t* tmp = (uint32_t*)ws_at(ctx, o_tmp);
+  uint32_t* cnt = (uint32_t*)ws_at(ctx, o_cnt);
+  SG_HIP(hipMemsetAsync(cnt, 0, ncalls * 4, ctx->stream));
+  if (nprog) {
+    ScopedTimer tm(ctx, "exec_signal");
+    hipLaunchKernelGGL(k_exec_signal, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off, d_prog_off,
+                       tmp, cnt);
+  }
+  SG_HIP(hipGetLastError());
+  rc = scan_counts(ctx, cnt, d_sig_off, ncalls, scan_off);
+  if (rc) return rc;
+  {
+    ScopedTimer tm(ctx, "exec_compact");
+    hipLaunchKernelGGL(k_exec_compact, dim3(div_up(ncalls, 4)), dim3(256), 0, ctx->stream, tmp, d_call_off, d_sig_off,
+                       ncalls, d_sig_vals);
+  }
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, const uint64_t* prog_off,
+                   size_t nprog, uint32_t* sig_vals, uint64_t* sig_off) {
+  if (!ctx || !call_off || !prog_off || !sig_off) return SG_EINVAL;
+  uint64_t ncalls = prog_off[nprog];
+  uint64_t npcs = call_off[ncalls];
+  if (prog_off[0] != 0 || call_off[0] != 0 || (npcs && (!pcs || !sig_vals))) return SG_EINVAL;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+  }
+  char* st = nullptr;
+  size_t b0 = (npcs * 4 + 255) & ~size_t(255), b1 = ((ncalls + 1) * 8 + 255) & ~size_t(255),
+         b2 = ((nprog + 1) * 8 + 255) & ~size_t(255);
+  SG_HIP(hipMallocAsync((void**)&st, 2 * b0 + 2 * b1 + b2 + 256, ctx->stream));
+  uint32_t* dp = (uint32_t*)st;
+  uint32_t* dsv = (uint32_t*)(st + b0);
+  uint64_t* dco = (uint64_t*)(st + 2 * b0);
+  uint64_t* dso = (uint64_t*)(st + 2 * b0 + b1);
+  uint64_t* dpo = (uint64_t*)(st + 2 * b0 + 2 * b1);
+  if (npcs) SG_HIP(hipMemcpyAsync(dp, pcs, npcs * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dco, call_off, (ncalls + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dpo, prog_off, (nprog + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  int rc = sg_exec_signal_dev(ctx, dp, dco, dpo, nprog, ncalls, npcs, dsv, dso);
+  if (rc) {
+    hipFreeAsync(st, ctx->stream);
+    return rc;
+  }
+  SG_HIP(hipMemcpyAsync(sig_off, dso, (ncalls + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (sig_off[ncalls]) SG_HIP(hipMemcpyAsync(sig_vals, dsv, sig_off[ncalls] * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipFreeAsync(st, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_gen_zipf_traces_dev(sg_ctx* ctx, uint64_t seed, uint64_t trace_seed, double zipf_s, uint32_t nranks,
+                           uint64_t prog_base, uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs) {
+  if (!ctx || !d_pcs || nranks == 0 || nranks > (1u << 24) || !(zipf_s > 0)) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  if (!ctx->gen_prob || ctx->gen_seed != seed || ctx->gen_s != zipf_s || ctx->gen_nranks != nranks) {
+    std::vector<uint32_t> prob, alias, perm;
+    build_zipf_tables(seed, zipf_s, nranks, prob, alias, perm);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->gen_prob) {
+      hipFree(ctx->gen_prob);
+      hipFree(ctx->gen_alias);
+      hipFree(ctx->gen_perm);
+      ctx->gen_prob = ctx->gen_alias = ctx->gen_perm = nullptr;
+    }
+    SG_HIP(hipMalloc(&ctx->gen_prob, nranks * 4));
+    SG_HIP(hipMalloc(&ctx->gen_alias, nranks * 4));
+    SG_HIP(hipMalloc(&ctx->gen_perm, nranks * 4));
+    SG_HIP(hipMemcpy(ctx->gen_prob, prob.data(), nranks * 4, hipMemcpyHostToDevice));
+    SG_HIP(hipMemcpy(ctx->gen_alias, alias.data(), nranks * 4, hipMemcpyHostToDevice));
+    SG_HIP(hipMemcpy(ctx->gen_perm, perm.data(), nranks * 4, hipMemcpyHostToDevice));
+    ctx->gen_seed = seed;
+    ctx->gen_s = zipf_s;
+    ctx->gen_nranks = nranks;
+  }
+  uint64_t per_prog = (uint64_t)calls * pcs_per_call;
+  uint64_t n = nprog * per_prog;
+  if (n == 0) return SG_OK;
+  hipLaunchKernelGGL(k_gen_traces, dim3(std::min<uint64_t>(div_up(n, 256), 65536)), dim3(256), 0, ctx->stream, trace_seed,
+                     nranks, prog_base * per_prog, n, ctx->gen_prob, ctx->gen_alias, ctx->gen_perm, d_pcs);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+}  // extern "C"

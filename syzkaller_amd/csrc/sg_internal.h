@@ -1,0 +1,169 @@
+// sg_internal.h -- shared host/device plumbing of libsyzsig.so (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/syzsig.h"
+
+namespace sg {
+
+// 2^32-bit direct-indexed signal bitmap: 2^27 words = 512 MiB.
+constexpr uint64_t kSetWords = 1ull << 27;
+constexpr uint64_t kSetBytes = kSetWords * 4;
+// First-owner table: one u32 key per possible signal value = 16 GiB.
+constexpr uint64_t kOwnerEntries = 1ull << 32;
+constexpr uint32_t kOwnerInf = 0xFFFFFFFFu;
+
+// Element tiles of the streaming kernels: 256 threads, one uint4 (4 values)
+// per lane per step, 4 steps per wave -> 4096 values per workgroup tile;
+// a "chunk" is one wave-instruction's 256 values and carries a 4 x u64
+// ballot mask (bit l of word k <-> value 4l+k of the chunk).
+constexpr int kBlock = 256;
+constexpr int kChunk = 256;
+constexpr int kTile = 4096;
+constexpr int kChunksPerTile = kTile / kChunk;  // 16
+constexpr int kWin = 1024;                      // record-offset window kept in LDS per tile
+
+void set_error(const char* fmt, ...);
+
+struct KernelTimer {
+  bool enabled = false;
+  struct Rec {
+    int id;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, int> ids;
+  std::vector<std::string> names;
+  std::vector<double> ms;
+  std::vector<uint64_t> count;
+};
+
+}  // namespace sg
+
+struct sg_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // grow-only device workspace and pinned host staging
+  void* ws = nullptr;
+  size_t ws_cap = 0;
+  void* pin = nullptr;
+  size_t pin_cap = 0;
+  // first-owner table and its decreasing key floor
+  uint32_t* owner = nullptr;
+  uint64_t owner_floor = 0;
+  // small device scalars (counters / flags)
+  uint64_t* dscal = nullptr;
+  // cached Zipf generator tables (alias method + rank->pc permutation)
+  uint32_t* gen_prob = nullptr;
+  uint32_t* gen_alias = nullptr;
+  uint32_t* gen_perm = nullptr;
+  uint64_t gen_seed = 0;
+  double gen_s = 0;
+  uint32_t gen_nranks = 0;
+  sg::KernelTimer timer;
+  std::mutex mu;
+};
+
+struct sg_set {
+  sg_ctx* ctx = nullptr;
+  uint32_t* words = nullptr;
+  bool owned = true;
+};
+
+namespace sg {
+
+// ---- host helpers (sg_ctx.hip) ----
+int hip_fail(hipError_t e, const char* what);
+#define SG_HIP(call)                                     \
+  do {                                                   \
+    hipError_t e_ = (call);                              \
+    if (e_ != hipSuccess) return ::sg::hip_fail(e_, #call); \
+  } while (0)
+
+int ensure_device(sg_ctx* ctx);
+// Carve `n` bump-allocated regions out of the workspace (each 256-B aligned).
+struct WsPlan {
+  size_t off[16];
+  int n = 0;
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    size_t o = total;
+    off[n++] = o;
+    total += (bytes + 255) & ~size_t(255);
+    return o;
+  }
+};
+int ws_reserve(sg_ctx* ctx, size_t bytes);
+inline void* ws_at(sg_ctx* ctx, size_t off) { return (char*)ctx->ws + off; }
+int pin_reserve(sg_ctx* ctx, size_t bytes);
+// Reserve `nkeys` first-owner keys: returns key_lo such that keys
+// key_lo .. key_lo+nkeys-1 are below every key already stored in the table.
+int owner_keys(sg_ctx* ctx, uint64_t nkeys, uint32_t* key_lo);
+
+// Kernel timing around launches on ctx->stream.
+void timer_begin(sg_ctx* ctx, const char* name, int* slot);
+void timer_end(sg_ctx* ctx, int slot);
+struct ScopedTimer {
+  sg_ctx* c;
+  int slot = -1;
+  ScopedTimer(sg_ctx* ctx, const char* name) : c(ctx) { timer_begin(ctx, name, &slot); }
+  ~ScopedTimer() { timer_end(c, slot); }
+};
+
+inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Device exclusive scan of u32 counts into u64 offsets, out[n] = total
+// (sg_scan.hip).  Uses the workspace tail beyond `ws_used`.
+int scan_counts(sg_ctx* ctx, const uint32_t* d_in, uint64_t* d_out, uint64_t n, size_t ws_used);
+size_t scan_ws_bytes(uint64_t n);
+
+// Shared first-owner pipeline (sg_triage.hip).
+struct OwnerJob {
+  const uint32_t* vals;   // device
+  const uint64_t* off;    // device, nseg+1 (nullptr: every element is its own segment)
+  uint64_t nvals;
+  uint64_t nseg;
+  const uint32_t* filter; // set words consulted before claiming (nullptr: none)
+  const uint32_t* order_rank;  // device rank of each segment (nullptr: rank = segment index)
+};
+int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint64_t* d_cmask, uint64_t* d_dmask,
+                        uint32_t* d_tile_rec, uint8_t* d_seg_flag, uint32_t* set_a, uint32_t* set_b);
+
+}  // namespace sg
+
+// ---- device helpers -------------------------------------------------------
+namespace sgd {
+
+__device__ __forceinline__ bool test_bit(const uint32_t* words, uint32_t s) {
+  return (words[s >> 5] >> (s & 31)) & 1u;
+}
+__device__ __forceinline__ void set_bit(uint32_t* words, uint32_t s) {
+  atomicOr(&words[s >> 5], 1u << (s & 31));
+}
+
+// largest r in [lo, hi] with off[r] <= i (off non-decreasing), searched in
+// `off` (global or LDS pointer).
+template <typename P>
+__device__ __forceinline__ uint64_t seg_search(P off, uint64_t lo, uint64_t hi, uint64_t i) {
+  while (lo < hi) {
+    uint64_t mid = lo + (hi - lo + 1) / 2;
+    if (off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+}  // namespace sgd

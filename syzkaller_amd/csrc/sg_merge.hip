@@ -1,0 +1,585 @@
+// sg_merge.hip -- sorted-slice algebra of pkg/cover on the GPU.
+//
+// Reference: pkg/cover/cover.go:28-40 Canonicalize, :42-102 Difference /
+// SymmetricDifference / Union / Intersection via foreach, :106-117
+// HasDifference.
+//
+// foreach (cover.go:81-102) is a two-pointer walk that, for a value v seen a
+// times in cov0 and b times in cov1, emits max(a,b) (Union), min(a,b)
+// (Intersection), max(a-b,0) (Difference) or |a-b| (SymmetricDifference)
+// copies, and drops every 0xFFFFFFFF.  Here every element decides on its own:
+// element i of one list, the t-th copy of its value there (t = i - first
+// index of the value), is kept iff t < or >= the value's count in the other
+// list (binary searches), and lands at
+//   (kept elements of its own list before it) + (kept elements of the other
+//   list with a smaller value; ties: cov0's copies first)
+// so any pair size runs fully parallel with one ballot-mask compaction.
+//
+// Canonicalize = segmented sort (4096-value LDS bitonic tiles, then rank-merge
+// passes for longer segments) + unique in place.  `last` starts at sent
+// (cover.go:31), so a value is kept iff it differs from its predecessor, the
+// first one iff it is not 0xFFFFFFFF.  The tail beyond the canonical length
+// keeps the sorted values, exactly like Go's in-place loop.
+#include "sg_internal.h"
+
+#include <algorithm>
+#include <numeric>
+
+namespace sg {
+
+constexpr uint32_t kSent = 0xFFFFFFFFu;  // cover.go:17
+
+__device__ __forceinline__ uint64_t lower_bound(const uint32_t* a, uint64_t n, uint32_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint64_t upper_bound(const uint32_t* a, uint64_t n, uint32_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// number of mask bits at positions < p (masks in chunk-ballot layout)
+__device__ __forceinline__ uint64_t mask_prefix(const uint64_t* mask, const uint64_t* base, uint64_t nchunks,
+                                                uint64_t p) {
+  uint64_t c = p / kChunk;
+  if (c >= nchunks) return base[nchunks];
+  uint32_t q = (uint32_t)(p % kChunk);
+  uint64_t acc = base[c];
+  for (int k = 0; k < 4; k++) {
+    int lim = q > (uint32_t)k ? (int)((q - k + 3) / 4) : 0;
+    uint64_t lm = lim >= 64 ? ~0ull : ((1ull << lim) - 1);
+    acc += __popcll(mask[c * 4 + k] & lm);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ bool mask_bit(const uint64_t* mask, uint64_t u) {
+  uint64_t c = u / kChunk;
+  uint32_t q = (uint32_t)(u % kChunk);
+  return (mask[c * 4 + (q & 3)] >> (q >> 2)) & 1ull;
+}
+
+// element u of a chunk-ballot space: chunk c = u/256, lane = (u%256)/4, k = u%4
+struct Side {
+  const uint32_t* v;     // values
+  const uint64_t* beg;   // per pair
+  const uint64_t* len;
+  const uint64_t* off;   // exclusive scan of len (npair+1): virtual element space
+};
+
+struct MergeArgs {
+  int op;
+  Side a, b;
+  uint64_t npair;
+  uint64_t* mask[2];
+  uint32_t* cnt[2];
+  uint64_t* base[2];
+  uint64_t nchunks[2];
+  uint32_t* out;
+  const uint64_t* out_beg;
+  uint64_t* out_len;
+};
+
+template <int kSide>  // 0: cov0 (a), 1: cov1 (b)
+__device__ __forceinline__ bool merge_keep(const MergeArgs& m, uint64_t u, uint64_t& k, uint32_t& x) {
+  const Side& me = kSide == 0 ? m.a : m.b;
+  const Side& ot = kSide == 0 ? m.b : m.a;
+  k = sgd::seg_search(me.off, 0, m.npair - 1, u);
+  uint64_t i = u - me.off[k];
+  const uint32_t* mine = me.v + me.beg[k];
+  x = mine[i];
+  if (x == kSent) return false;  // cover.go:97
+  const uint32_t* other = ot.v + ot.beg[k];
+  uint64_t on = ot.len[k];
+  uint64_t t = i - lower_bound(mine, i, x);
+  uint64_t c = upper_bound(other, on, x) - lower_bound(other, on, x);
+  switch (m.op) {
+    case SG_OP_DIFFERENCE: return kSide == 0 && t >= c;
+    case SG_OP_INTERSECT: return kSide == 0 && t < c;
+    case SG_OP_UNION: return kSide == 0 ? true : t >= c;
+    default: return t >= c;  // SG_OP_SYMDIFF
+  }
+}
+
+template <int kSide>
+__global__ __launch_bounds__(kBlock) void k_merge_keep(MergeArgs m) {
+  const int lane = threadIdx.x & 63;
+  uint64_t c = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (c >= m.nchunks[kSide]) return;
+  const Side& me = kSide == 0 ? m.a : m.b;
+  uint64_t n = me.off[m.npair];
+  uint32_t bits = 0;
+  for (int q = 0; q < 4; q++) {
+    uint64_t u = c * kChunk + lane * 4 + q;
+    if (u >= n) continue;
+    uint64_t k;
+    uint32_t x;
+    if (merge_keep<kSide>(m, u, k, x)) bits |= 1u << q;
+  }
+  uint64_t b0 = __ballot(bits & 1u), b1 = __ballot(bits & 2u), b2 = __ballot(bits & 4u), b3 = __ballot(bits & 8u);
+  uint64_t mine = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+  if (lane < 4) m.mask[kSide][c * 4 + lane] = mine;
+  if (lane == 0) m.cnt[kSide][c] = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+}
+
+template <int kSide>
+__global__ void k_merge_scatter(MergeArgs m) {
+  const Side& me = kSide == 0 ? m.a : m.b;
+  const Side& ot = kSide == 0 ? m.b : m.a;
+  uint64_t n = me.off[m.npair];
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += stride) {
+    if (!mask_bit(m.mask[kSide], u)) continue;
+    uint64_t k = sgd::seg_search(me.off, 0, m.npair - 1, u);
+    uint64_t i = u - me.off[k];
+    uint32_t x = me.v[me.beg[k] + i];
+    uint64_t pos = mask_prefix(m.mask[kSide], m.base[kSide], m.nchunks[kSide], u) -
+                   mask_prefix(m.mask[kSide], m.base[kSide], m.nchunks[kSide], me.off[k]);
+    const uint32_t* other = ot.v + ot.beg[k];
+    uint64_t j = kSide == 0 ? lower_bound(other, ot.len[k], x) : upper_bound(other, ot.len[k], x);
+    if (m.nchunks[1 - kSide])
+      pos += mask_prefix(m.mask[1 - kSide], m.base[1 - kSide], m.nchunks[1 - kSide], ot.off[k] + j) -
+             mask_prefix(m.mask[1 - kSide], m.base[1 - kSide], m.nchunks[1 - kSide], ot.off[k]);
+    m.out[m.out_beg[k] + pos] = x;
+  }
+}
+
+__global__ void k_merge_len(MergeArgs m) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m.npair) return;
+  uint64_t L = 0;
+  for (int s = 0; s < 2; s++) {
+    if (!m.nchunks[s]) continue;
+    const Side& me = s == 0 ? m.a : m.b;
+    L += mask_prefix(m.mask[s], m.base[s], m.nchunks[s], me.off[k + 1]) -
+         mask_prefix(m.mask[s], m.base[s], m.nchunks[s], me.off[k]);
+  }
+  m.out_len[k] = L;
+}
+
+// HasDifference: some element of a (t-th copy) with t >= count in b.
+__global__ void k_has_difference(const uint32_t* __restrict__ a, uint64_t na, const uint32_t* __restrict__ b,
+                                 uint64_t nb, uint64_t* flag) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool hit = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
+    uint32_t x = a[i];
+    uint64_t t = i - lower_bound(a, i, x);
+    uint64_t c = upper_bound(b, nb, x) - lower_bound(b, nb, x);
+    hit |= t >= c;
+  }
+  if (__any(hit) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+// ---- segmented sort ----------------------------------------------------------
+struct SortChunk {
+  uint64_t start;  // global element index
+  uint32_t len;    // <= 4096
+};
+
+__global__ __launch_bounds__(kBlock) void k_sort_chunks(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                        const SortChunk* __restrict__ chunks) {
+  __shared__ uint32_t s[kTile];
+  SortChunk ch = chunks[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < kTile; i += kBlock) s[i] = i < ch.len ? in[ch.start + i] : kSent;
+  __syncthreads();
+  // bitonic sort of 4096 values, 8 compare-exchanges per thread per stage
+  for (uint32_t k = 2; k <= kTile; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = threadIdx.x; t < kTile / 2; t += kBlock) {
+        uint32_t i = 2 * t - (t & (j - 1));  // index with bit j clear
+        uint32_t l = i + j;
+        bool up = (i & k) == 0;
+        uint32_t x = s[i], y = s[l];
+        if ((x > y) == up) {
+          s[i] = y;
+          s[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < ch.len; i += kBlock) out[ch.start + i] = s[i];
+}
+
+struct BigSeg {
+  uint64_t start;  // global element index of the segment
+  uint64_t len;
+};
+
+// one rank-merge pass of width w over the big segments [0, nbig) (sorted by
+// length descending, so the active ones form a prefix); `vs` = exclusive scan
+// of their lengths (virtual element space).
+__global__ void k_merge_pass(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                             const BigSeg* __restrict__ segs, const uint64_t* __restrict__ vs, uint64_t nbig,
+                             uint64_t w) {
+  uint64_t n = vs[nbig];
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += stride) {
+    uint64_t si = sgd::seg_search(vs, 0, nbig - 1, u);
+    BigSeg sg = segs[si];
+    uint64_t i = u - vs[si];
+    const uint32_t* src = in + sg.start;
+    uint64_t r = i / w, pair0 = (r & ~1ull) * w;
+    uint32_t x = src[i];
+    uint64_t pos;
+    if ((r & 1) == 0) {
+      uint64_t rs = pair0 + w;
+      uint64_t rl = rs < sg.len ? std::min<uint64_t>(w, sg.len - rs) : 0;
+      pos = pair0 + (i - pair0) + lower_bound(src + rs, rl, x);
+    } else {
+      uint64_t ls = pair0;
+      pos = pair0 + (i - (pair0 + w)) + upper_bound(src + ls, w, x);
+    }
+    out[sg.start + pos] = x;
+  }
+}
+
+struct CanonArgs {
+  const uint32_t* buf[2];
+  const uint64_t* off;
+  uint64_t nseg;
+  uint64_t n;
+  const uint8_t* parity;  // per segment: which buffer holds its sorted values
+  uint64_t* mask;
+  uint32_t* cnt;
+  uint64_t* base;
+  uint64_t nchunks;
+  uint32_t* out;
+  uint64_t* out_len;
+};
+
+__global__ __launch_bounds__(kBlock) void k_unique_keep(CanonArgs a) {
+  const int lane = threadIdx.x & 63;
+  uint64_t c = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (c >= a.nchunks) return;
+  uint32_t bits = 0;
+  for (int q = 0; q < 4; q++) {
+    uint64_t u = c * kChunk + lane * 4 + q;
+    if (u >= a.n) continue;
+    uint64_t k = sgd::seg_search(a.off, 0, a.nseg - 1, u);
+    const uint32_t* b = a.buf[a.parity[k]];
+    uint32_t x = b[u];
+    uint32_t last = u == a.off[k] ? kSent : b[u - 1];  // cover.go:31-37
+    if (x != last) bits |= 1u << q;
+  }
+  uint64_t b0 = __ballot(bits & 1u), b1 = __ballot(bits & 2u), b2 = __ballot(bits & 4u), b3 = __ballot(bits & 8u);
+  uint64_t mine = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+  if (lane < 4) a.mask[c * 4 + lane] = mine;
+  if (lane == 0) a.cnt[c] = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+}
+
+__global__ void k_unique_len(CanonArgs a) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.nseg) return;
+  a.out_len[k] = mask_prefix(a.mask, a.base, a.nchunks, a.off[k + 1]) -
+                 mask_prefix(a.mask, a.base, a.nchunks, a.off[k]);
+}
+
+// out = sorted values with the first out_len[k] positions of each segment
+// replaced by the kept (unique) ones.
+__global__ void k_unique_write(CanonArgs a) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < a.n; u += stride) {
+    uint64_t k = sgd::seg_search(a.off, 0, a.nseg - 1, u);
+    const uint32_t* b = a.buf[a.parity[k]];
+    uint32_t x = b[u];
+    uint64_t s = a.off[k];
+    if (u - s >= a.out_len[k]) a.out[u] = x;  // stale tail: the sorted value
+    if (mask_bit(a.mask, u)) {
+      uint64_t pos = mask_prefix(a.mask, a.base, a.nchunks, u) - mask_prefix(a.mask, a.base, a.nchunks, s);
+      a.out[s + pos] = x;
+    }
+  }
+}
+
+// ---- host orchestration ----------------------------------------------------------
+static int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg, uint64_t* out_len) {
+  // off: host offsets (nseg+1); d_vals: device values (sorted+uniqued in place)
+  uint64_t n = off[nseg];
+  std::vector<SortChunk> chunks;
+  std::vector<BigSeg> big;
+  std::vector<uint8_t> parity(nseg, 0);
+  for (uint64_t k = 0; k < nseg; k++) {
+    uint64_t L = off[k + 1] - off[k];
+    for (uint64_t q = 0; q < L; q += kTile) chunks.push_back({off[k] + q, (uint32_t)std::min<uint64_t>(kTile, L - q)});
+    if (L > (uint64_t)kTile) {
+      big.push_back({off[k], L});
+      int passes = 0;
+      for (uint64_t w = kTile; w < L; w <<= 1) passes++;
+      parity[k] = passes & 1;
+    }
+  }
+  std::sort(big.begin(), big.end(), [](const BigSeg& x, const BigSeg& y) { return x.len > y.len; });
+  std::vector<uint64_t> vs(big.size() + 1, 0);
+  for (size_t i = 0; i < big.size(); i++) vs[i + 1] = vs[i] + big[i].len;
+  uint64_t ntiles = (n + kTile - 1) / kTile, nchunks = ntiles * kChunksPerTile;
+  WsPlan p;
+  size_t o_b0 = p.add(n * 4), o_b1 = p.add(n * 4), o_ch = p.add(chunks.size() * sizeof(SortChunk)),
+         o_big = p.add(big.size() * sizeof(BigSeg)), o_vs = p.add(vs.size() * 8), o_off = p.add((nseg + 1) * 8),
+         o_par = p.add(nseg), o_mask = p.add(nchunks * 32), o_cnt = p.add(nchunks * 4),
+         o_base = p.add((nchunks + 1) * 8), o_len = p.add(nseg * 8);
+  size_t scan_off = p.total;
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nchunks));
+  if (rc) return rc;
+  uint32_t* b0 = (uint32_t*)ws_at(ctx, o_b0);
+  uint32_t* b1 = (uint32_t*)ws_at(ctx, o_b1);
+  SortChunk* dch = (SortChunk*)ws_at(ctx, o_ch);
+  BigSeg* dbig = (BigSeg*)ws_at(ctx, o_big);
+  uint64_t* dvs = (uint64_t*)ws_at(ctx, o_vs);
+  uint64_t* doff = (uint64_t*)ws_at(ctx, o_off);
+  uint8_t* dpar = (uint8_t*)ws_at(ctx, o_par);
+  uint64_t* dlen = (uint64_t*)ws_at(ctx, o_len);
+  if (!chunks.empty())
+    SG_HIP(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(SortChunk), hipMemcpyHostToDevice, ctx->stream));
+  if (!big.empty()) {
+    SG_HIP(hipMemcpyAsync(dbig, big.data(), big.size() * sizeof(BigSeg), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipMemcpyAsync(dvs, vs.data(), vs.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  }
+  SG_HIP(hipMemcpyAsync(doff, off, (nseg + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dpar, parity.data(), nseg, hipMemcpyHostToDevice, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "canon_sort");
+    if (!chunks.empty())
+      hipLaunchKernelGGL(k_sort_chunks, dim3((uint32_t)chunks.size()), dim3(kBlock), 0, ctx->stream, d_vals, b0,
+                         dch);
+    // rank-merge passes: active segments (len > w) are a prefix of `big`
+    uint32_t* bufs[2] = {b0, b1};
+    int pass = 0;
+    for (uint64_t w = kTile;; w <<= 1, pass++) {
+      uint64_t nact = 0;
+      while (nact < big.size() && big[nact].len > w) nact++;
+      if (nact == 0) break;
+      uint64_t nel = vs[nact];
+      hipLaunchKernelGGL(k_merge_pass, dim3((uint32_t)std::min<uint64_t>(div_up(nel, 256), 16384)), dim3(256), 0,
+                         ctx->stream, bufs[pass & 1], bufs[(pass + 1) & 1], dbig, dvs, nact, w);
+    }
+  }
+  CanonArgs a{};
+  a.buf[0] = b0;
+  a.buf[1] = b1;
+  a.off = doff;
+  a.nseg = nseg;
+  a.n = n;
+  a.parity = dpar;
+  a.mask = (uint64_t*)ws_at(ctx, o_mask);
+  a.cnt = (uint32_t*)ws_at(ctx, o_cnt);
+  a.base = (uint64_t*)ws_at(ctx, o_base);
+  a.nchunks = nchunks;
+  a.out = d_vals;
+  a.out_len = dlen;
+  hipLaunchKernelGGL(k_unique_keep, dim3(div_up(nchunks, kBlock / 64)), dim3(kBlock), 0, ctx->stream, a);
+  rc = scan_counts(ctx, a.cnt, a.base, nchunks, scan_off);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_unique_len, dim3(div_up(nseg, 256)), dim3(256), 0, ctx->stream, a);
+  hipLaunchKernelGGL(k_unique_write, dim3((uint32_t)std::min<uint64_t>(div_up(n, 256), 16384)), dim3(256), 0,
+                     ctx->stream, a);
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out_len, dlen, nseg * 8, hipMemcpyDeviceToHost, ctx->stream));
+  return SG_OK;
+}
+
+static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+                     const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+                     const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
+                     uint64_t* out_len) {
+  std::vector<uint64_t> aoff(npair + 1, 0), boff(npair + 1, 0);
+  for (size_t k = 0; k < npair; k++) {
+    if (a_beg[k] + a_len[k] > a_total || b_beg[k] + b_len[k] > b_total ||
+        out_beg[k] + a_len[k] + b_len[k] > out_total) {
+      set_error("sg_merge_batch: pair %zu out of bounds", k);
+      return SG_EINVAL;
+    }
+    aoff[k + 1] = aoff[k] + a_len[k];
+    boff[k + 1] = boff[k] + b_len[k];
+  }
+  bool bside = op == SG_OP_UNION || op == SG_OP_SYMDIFF;
+  uint64_t na = aoff[npair], nb = bside ? boff[npair] : 0;
+  uint64_t nca = ((na + kTile - 1) / kTile) * kChunksPerTile, ncb = ((nb + kTile - 1) / kTile) * kChunksPerTile;
+  WsPlan p;
+  size_t o_a = p.add(a_total * 4), o_b = p.add(b_total * 4), o_out = p.add(out_total * 4);
+  size_t o_meta = p.add((npair * 2 + (npair + 1)) * 8 * 2 + npair * 8 * 2);
+  size_t o_m0 = p.add(nca * 32), o_m1 = p.add(ncb * 32), o_c0 = p.add(nca * 4), o_c1 = p.add(ncb * 4),
+         o_s0 = p.add((nca + 1) * 8), o_s1 = p.add((ncb + 1) * 8);
+  size_t scan_off = p.total;
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(std::max(nca, ncb)));
+  if (rc) return rc;
+  uint32_t* da = (uint32_t*)ws_at(ctx, o_a);
+  uint32_t* db = (uint32_t*)ws_at(ctx, o_b);
+  uint32_t* dout = (uint32_t*)ws_at(ctx, o_out);
+  uint64_t* meta = (uint64_t*)ws_at(ctx, o_meta);
+  // meta layout: a_beg a_len aoff b_beg b_len boff out_beg out_len
+  uint64_t *m_abeg = meta, *m_alen = m_abeg + npair, *m_aoff = m_alen + npair, *m_bbeg = m_aoff + npair + 1,
+           *m_blen = m_bbeg + npair, *m_boff = m_blen + npair, *m_obeg = m_boff + npair + 1,
+           *m_olen = m_obeg + npair;
+  if (a_total) SG_HIP(hipMemcpyAsync(da, a, a_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (b_total) SG_HIP(hipMemcpyAsync(db, b, b_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_abeg, a_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_alen, a_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_aoff, aoff.data(), (npair + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_bbeg, b_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_blen, b_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_boff, boff.data(), (npair + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(m_obeg, out_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  MergeArgs m{};
+  m.op = op;
+  m.a = {da, m_abeg, m_alen, m_aoff};
+  m.b = {db, m_bbeg, m_blen, m_boff};
+  m.npair = npair;
+  m.mask[0] = (uint64_t*)ws_at(ctx, o_m0);
+  m.mask[1] = (uint64_t*)ws_at(ctx, o_m1);
+  m.cnt[0] = (uint32_t*)ws_at(ctx, o_c0);
+  m.cnt[1] = (uint32_t*)ws_at(ctx, o_c1);
+  m.base[0] = (uint64_t*)ws_at(ctx, o_s0);
+  m.base[1] = (uint64_t*)ws_at(ctx, o_s1);
+  m.nchunks[0] = nca;
+  m.nchunks[1] = ncb;
+  m.out = dout;
+  m.out_beg = m_obeg;
+  m.out_len = m_olen;
+  {
+    ScopedTimer tm(ctx, "merge_keep");
+    if (nca) hipLaunchKernelGGL(k_merge_keep<0>, dim3(div_up(nca, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
+    if (ncb) hipLaunchKernelGGL(k_merge_keep<1>, dim3(div_up(ncb, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
+  }
+  if (nca) {
+    rc = scan_counts(ctx, m.cnt[0], m.base[0], nca, scan_off);
+    if (rc) return rc;
+  }
+  if (ncb) {
+    rc = scan_counts(ctx, m.cnt[1], m.base[1], ncb, scan_off);
+    if (rc) return rc;
+  }
+  {
+    ScopedTimer tm(ctx, "merge_scatter");
+    if (na)
+      hipLaunchKernelGGL(k_merge_scatter<0>, dim3((uint32_t)std::min<uint64_t>(div_up(na, 256), 16384)), dim3(256), 0,
+                         ctx->stream, m);
+    if (nb)
+      hipLaunchKernelGGL(k_merge_scatter<1>, dim3((uint32_t)std::min<uint64_t>(div_up(nb, 256), 16384)), dim3(256), 0,
+                         ctx->stream, m);
+  }
+  hipLaunchKernelGGL(k_merge_len, dim3(div_up(npair, 256)), dim3(256), 0, ctx->stream, m);
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out_len, m_olen, npair * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  // copy back only each pair's result range
+  for (size_t k = 0; k < npair; k++)
+    if (out_len[k])
+      SG_HIP(hipMemcpyAsync(out + out_beg[k], dout + out_beg[k], out_len[k] * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_canonicalize_batch(sg_ctx* ctx, uint32_t* vals, const uint64_t* off, size_t nseg, uint64_t* out_len) {
+  if (!ctx || !off || (nseg && !out_len)) return SG_EINVAL;
+  if (nseg == 0) return SG_OK;
+  if (off[0] != 0) return SG_EINVAL;
+  for (size_t k = 0; k < nseg; k++)
+    if (off[k + 1] < off[k]) return SG_EINVAL;
+  uint64_t n = off[nseg];
+  if (n && !vals) return SG_EINVAL;
+  if (n == 0) {
+    for (size_t k = 0; k < nseg; k++) out_len[k] = 0;
+    return SG_OK;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  uint32_t* dv = nullptr;
+  SG_HIP(hipMallocAsync((void**)&dv, n * 4, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dv, vals, n * 4, hipMemcpyHostToDevice, ctx->stream));
+  rc = canonicalize_dev(ctx, dv, off, nseg, out_len);
+  if (rc) {
+    hipFreeAsync(dv, ctx->stream);
+    return rc;
+  }
+  SG_HIP(hipMemcpyAsync(vals, dv, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipFreeAsync(dv, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_canonicalize(sg_ctx* ctx, uint32_t* v, size_t n, size_t* nout) {
+  if (!ctx || !nout || (n && !v)) return SG_EINVAL;
+  uint64_t off[2] = {0, n}, len = 0;
+  int rc = sg_canonicalize_batch(ctx, v, off, 1, &len);
+  *nout = (size_t)len;
+  return rc;
+}
+
+int sg_merge_batch(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+                   const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+                   const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
+                   uint64_t* out_len) {
+  if (!ctx || op < 0 || op > 3 || (npair && (!a_beg || !a_len || !b_beg || !b_len || !out_beg || !out_len)) ||
+      (a_total && !a) || (b_total && !b) || (out_total && !out)) {
+    set_error("sg_merge_batch: invalid argument");
+    return SG_EINVAL;
+  }
+  if (npair == 0) return SG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  return merge_run(ctx, op, a, a_total, a_beg, a_len, b, b_total, b_beg, b_len, npair, out, out_total, out_beg,
+                   out_len);
+}
+
+int sg_merge(sg_ctx* ctx, int op, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+             size_t* nout) {
+  if (!nout) return SG_EINVAL;
+  uint64_t ab = 0, al = na, bb = 0, bl = nb, ob = 0, ol = 0;
+  *nout = 0;
+  if (na + nb == 0) return ctx ? SG_OK : SG_EINVAL;
+  int rc = sg_merge_batch(ctx, op, a, na, &ab, &al, b, nb, &bb, &bl, 1, out, na + nb, &ob, &ol);
+  *nout = (size_t)ol;
+  return rc;
+}
+
+int sg_has_difference(sg_ctx* ctx, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, int* out) {
+  if (!ctx || !out || (na && !a) || (nb && !b)) return SG_EINVAL;
+  *out = 0;
+  if (na == 0) return SG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  WsPlan p;
+  size_t o_a = p.add(na * 4), o_b = p.add(nb * 4);
+  rc = ws_reserve(ctx, p.total);
+  if (rc) return rc;
+  uint32_t* da = (uint32_t*)ws_at(ctx, o_a);
+  uint32_t* db = (uint32_t*)ws_at(ctx, o_b);
+  SG_HIP(hipMemcpyAsync(da, a, na * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (nb) SG_HIP(hipMemcpyAsync(db, b, nb * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemsetAsync(ctx->dscal, 0, 8, ctx->stream));
+  hipLaunchKernelGGL(k_has_difference, dim3((uint32_t)std::min<uint64_t>(div_up(na, 256), 4096)), dim3(256), 0,
+                     ctx->stream, da, (uint64_t)na, db, (uint64_t)nb, ctx->dscal);
+  SG_HIP(hipGetLastError());
+  uint64_t f = 0;
+  SG_HIP(hipMemcpyAsync(&f, ctx->dscal, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  *out = f ? 1 : 0;
+  return SG_OK;
+}
+
+}  // extern "C"

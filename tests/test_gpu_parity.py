@@ -1,0 +1,358 @@
+"""Parity of the MI355X product (libsyzsig.so, through its C-ABI) with the
+oracle and the reference's own known answers.  Bit-exact everywhere: this path
+is integer / index work only."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from tests import refmodel as R
+
+pytestmark = pytest.mark.gpu
+
+SENT = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def C(ctx):
+    from syzkaller_amd import cover
+
+    return cover
+
+
+def zipf_batch(rng, nprog, calls, pcs, s=1.1, nranks=1 << 16, ragged=False):
+    """Synthetic Zipf traces -> per-call signal through the executor restatement."""
+    lens = (rng.integers(0, 2 * pcs, size=nprog * calls) if ragged else np.full(nprog * calls, pcs)).astype(np.uint64)
+    call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ranks = np.minimum(rng.zipf(s, size=int(call_off[-1])), nranks) - 1
+    trace = (0x81000000 + 16 * ranks).astype(np.uint32)
+    prog_off = (np.arange(nprog + 1) * calls).astype(np.uint64)
+    return O.exec_signal(trace, call_off, prog_off)
+
+
+# ---- pkg/cover KATs through the product (cover_test.go) -------------------------
+OPS = {"TestDifference": "Difference", "TestSymmetricDifference": "SymmetricDifference", "TestUnion": "Union",
+       "TestIntersection": "Intersection"}
+
+
+def _cases(t):
+    cases = [(c["v0"], c["v1"], c["r"]) for c in t["cases"]]
+    if t["symmetric"]:
+        cases += [(b, a, r) for a, b, r in cases]
+    cases.append(([], [], []))
+    return cases
+
+
+@pytest.mark.parametrize("name", sorted(OPS))
+def test_kat_ops(C, kats, name):
+    f = getattr(C, OPS[name])
+    for v0, v1, r in _cases(kats[name]):
+        res = f(np.array(v0, np.uint32), np.array(v1, np.uint32))
+        assert list(res) == r
+        assert list(res) == sorted(res)
+
+
+def test_kat_canonicalize(C, kats):
+    for v0, _, r in _cases(kats["TestCanonicalize"]):
+        assert list(C.Canonicalize(np.array(v0, np.uint32))) == r
+
+
+def test_kat_minimize(C, kats):
+    for case in kats["TestMinimize"]["cases"]:
+        assert C.Minimize([np.array(c, np.uint32) for c in case["inp"]]) == case["out"]
+
+
+# ---- random parity with the oracle ---------------------------------------------
+def test_ops_random_vs_oracle(C):
+    rng = np.random.default_rng(100)
+    for it in range(300):
+        n0, n1 = (int(x) for x in rng.integers(0, 40, size=2))
+        hi = [4, 64, 1 << 32][it % 3]
+        a = np.sort(rng.integers(0, hi, size=n0, dtype=np.uint64)).astype(np.uint32)
+        b = np.sort(rng.integers(0, hi, size=n1, dtype=np.uint64)).astype(np.uint32)
+        if it % 5 == 0:
+            a = np.sort(np.concatenate([a, np.full(int(rng.integers(1, 3)), SENT, np.uint32)]))
+        if it % 7 == 0:
+            b = np.sort(np.concatenate([b, np.full(1, SENT, np.uint32)]))
+        for op, f in enumerate([C.Difference, C.SymmetricDifference, C.Union, C.Intersection]):
+            assert np.array_equal(f(a, b), O.foreach(op, a, b)), (op, a, b)
+        assert C.HasDifference(a, b) == O.has_difference(a, b)
+
+
+def test_ops_large_multiset(C):
+    rng = np.random.default_rng(101)
+    for n0, n1, hi in [(100000, 3000, 5000), (4096, 1 << 20, 1 << 22), (70000, 70000, 1 << 30)]:
+        a = np.sort(rng.integers(0, hi, size=n0)).astype(np.uint32)
+        b = np.sort(rng.integers(0, hi, size=n1)).astype(np.uint32)
+        for op, f in enumerate([C.Difference, C.SymmetricDifference, C.Union, C.Intersection]):
+            assert np.array_equal(f(a, b), O.foreach(op, a, b)), (op, n0, n1)
+        assert C.HasDifference(a, b) == O.has_difference(a, b)
+        assert C.HasDifference(b, a) == O.has_difference(b, a)
+
+
+def test_has_difference_property(C):
+    # cover_test.go:210-221
+    rng = np.random.default_rng(102)
+    for _ in range(200):
+        a = C.Canonicalize(rng.integers(0, 100, size=rng.integers(0, 20)).astype(np.uint32))
+        b = C.Canonicalize(rng.integers(0, 100, size=rng.integers(0, 20)).astype(np.uint32))
+        assert C.HasDifference(a, b) == (C.Difference(a, b).size != 0)
+
+
+def test_merge_batch_shared_corpus(C):
+    # C1 shape in miniature: many traces vs one corpus signal, Union and Difference
+    rng = np.random.default_rng(103)
+    corpus = np.unique(rng.integers(0, 1 << 24, size=200000)).astype(np.uint32)
+    traces = [np.sort(rng.integers(0, 1 << 24, size=int(rng.integers(0, 3000)))).astype(np.uint32) for _ in range(64)]
+    a = np.concatenate(traces)
+    a_len = np.array([t.size for t in traces], np.uint64)
+    a_beg = np.concatenate([[0], np.cumsum(a_len)[:-1]]).astype(np.uint64)
+    b_beg = np.zeros(64, np.uint64)
+    b_len = np.full(64, corpus.size, np.uint64)
+    for op in range(4):
+        res = C.merge_batch(op, a, a_beg, a_len, corpus, b_beg, b_len)
+        for k, t in enumerate(traces):
+            assert np.array_equal(res[k], O.foreach(op, t, corpus)), (op, k)
+
+
+def test_canonicalize_random_vs_oracle(C):
+    rng = np.random.default_rng(104)
+    for n in [0, 1, 2, 63, 64, 100, 4095, 4096, 4097, 8193, 20000, 70000, 300000]:
+        for hi in [3, 1000, 1 << 32]:
+            v = rng.integers(0, hi, size=n, dtype=np.uint64).astype(np.uint32)
+            if n and hi == 3:
+                v[rng.integers(0, n)] = SENT
+            exp, m = O.canonicalize(v)
+            got = v.copy()
+            res = C.Canonicalize(got)
+            assert res.size == m and np.array_equal(res, exp[:m]), (n, hi)
+            assert np.array_equal(got, exp), (n, hi)  # whole slice, stale tail included
+
+
+def test_canonicalize_batch_ragged(C):
+    rng = np.random.default_rng(105)
+    lens = [0, 5, 4096, 1, 0, 9000, 33, 70000, 4097, 2, 16384]
+    segs = [rng.integers(0, [10, 1 << 32][k % 2], size=L, dtype=np.uint64).astype(np.uint32) for k, L in enumerate(lens)]
+    segs[3][:] = SENT
+    vals = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    got = vals.copy()
+    out_len = C.canonicalize_batch(got, off)
+    for k in range(len(lens)):
+        exp, m = O.canonicalize(segs[k])
+        assert out_len[k] == m
+        assert np.array_equal(got[off[k]:off[k + 1]], exp)
+
+
+def test_minimize_vs_oracle(C):
+    rng = np.random.default_rng(106)
+    for n, hi in [(1, 5), (7, 20), (50, 100), (2000, 5000), (20000, 1 << 16)]:
+        covs = [C.Canonicalize(rng.integers(0, hi, size=int(rng.integers(0, 60))).astype(np.uint32)) for _ in range(n)]
+        vals, off = C.to_csr(covs)
+        assert np.array_equal(C.minimize_csr(vals, off), O.minimize(vals, off)), n
+        order = rng.permutation(n).astype(np.uint32)
+        assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order)), n
+        # non-canonical covers with duplicates and sentinels are processed the same way
+        raw = [rng.integers(0, 8, size=int(rng.integers(0, 6))).astype(np.uint32) for _ in range(n)]
+        rv, ro = C.to_csr(raw)
+        rv[rv == 7] = SENT
+        assert np.array_equal(C.minimize_csr(rv, ro, order), O.minimize(rv, ro, order)), n
+
+
+# ---- signal sets (map replacements) --------------------------------------------
+def test_signal_set_ops(C):
+    rng = np.random.default_rng(107)
+    s = C.SignalSet()
+    o = O.OSet()
+    for it in range(20):
+        add = rng.integers(0, 1 << 32, size=int(rng.integers(0, 5000)), dtype=np.uint64).astype(np.uint32)
+        if it % 3 == 0:
+            add = np.concatenate([add, np.array([0, SENT, 1, 0], np.uint32)])
+        C.SignalAdd(s, add)
+        o.add(add)
+        probe = np.concatenate([add[: add.size // 2], rng.integers(0, 1 << 32, size=300, dtype=np.uint64).astype(np.uint32)])
+        assert C.SignalNew(s, probe) == O.signal_new(o, probe)
+        assert C.SignalNew(s, add) is False
+        assert np.array_equal(C.SignalDiff(s, probe), O.signal_diff(o, probe))
+    assert len(s) == len(o)
+    assert np.array_equal(s.export(), o.export())
+    s.clear()
+    assert len(s) == 0 and s.export().size == 0
+
+
+# ---- the hot path: batched new-signal triage (fuzzer.go:645-693) ----------------
+def _check_triage(C, sets, osets, vals, off):
+    ms, ns = sets
+    om, on = osets
+    flags, dv, do = C.triage_batch(ms, ns, vals, off)
+    ef, ev, eo = O.triage_batch(om, on, vals, off)
+    assert np.array_equal(flags, ef)
+    assert np.array_equal(do, eo)
+    assert np.array_equal(dv, ev)
+    return flags
+
+
+def test_triage_small_vs_python(C):
+    rng = np.random.default_rng(108)
+    ms, ns = C.SignalSet(), C.SignalSet()
+    for it in range(60):
+        ms.clear()
+        ns.clear()
+        nrec = int(rng.integers(0, 40))
+        recs = [[int(x) for x in rng.integers(0, 80, size=rng.integers(0, 14))] for _ in range(nrec)]
+        if it % 4 == 0 and nrec:
+            recs[0] += [0, SENT, SENT]
+        m0 = sorted(set(int(x) for x in rng.integers(0, 80, size=rng.integers(0, 50))))
+        C.SignalAdd(ms, np.array(m0, np.uint32))
+        vals = np.array([x for r in recs for x in r], dtype=np.uint32)
+        off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+        flags, dv, do = C.triage_batch(ms, ns, vals, off)
+        pm, pn = set(m0), set()
+        pf, pd = R.triage(pm, pn, recs)
+        assert list(flags) == pf
+        assert [list(dv[int(do[r]):int(do[r + 1])]) for r in range(nrec)] == pd
+        assert set(ms.export().tolist()) == pm and set(ns.export().tolist()) == pn
+
+
+def test_triage_zipf_sequence_vs_oracle(C):
+    """Several consecutive batches against the same sets (the fuzzer's steady
+    state): exercises the decreasing owner-key generations."""
+    rng = np.random.default_rng(109)
+    ms, ns = C.SignalSet(), C.SignalSet()
+    om, on = O.OSet(), O.OSet()
+    warm, _ = zipf_batch(rng, 64, 8, 256)
+    C.SignalAdd(ms, warm)
+    om.add(warm)
+    for b in range(6):
+        vals, off = zipf_batch(rng, 128, 8, 512, ragged=(b % 2 == 1))
+        flags = _check_triage(C, (ms, ns), (om, on), vals, off)
+        assert 0 < flags.sum() < flags.size
+    assert np.array_equal(ms.export(), om.export())
+    assert np.array_equal(ns.export(), on.export())
+
+
+def test_triage_edge_cases(C):
+    ms, ns = C.SignalSet(), C.SignalSet()
+    om, on = O.OSet(), O.OSet()
+    cases = [
+        (np.array([], np.uint32), np.array([0], np.uint64)),                  # no records
+        (np.array([], np.uint32), np.array([0, 0, 0], np.uint64)),            # only empty records
+        (np.array([0, SENT, 0, SENT], np.uint32), np.array([0, 2, 2, 4], np.uint64)),
+        (np.array([7] * 5000, np.uint32), np.array([0, 2500, 5000], np.uint64)),  # dups within a record
+        (np.arange(10000, dtype=np.uint32), np.array([0, 1, 1, 1, 4096, 4097, 8191, 10000], np.uint64)),
+        (np.arange(10000, dtype=np.uint32), np.array([0, 10000], np.uint64)),  # everything already known
+    ]
+    for vals, off in cases:
+        _check_triage(C, (ms, ns), (om, on), vals, off)
+    # many empty records around tile boundaries (record window > LDS window)
+    rng = np.random.default_rng(110)
+    lens = np.where(rng.random(20000) < 0.9, 0, rng.integers(1, 30, size=20000)).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    vals = rng.integers(0, 1 << 20, size=int(off[-1])).astype(np.uint32)
+    _check_triage(C, (ms, ns), (om, on), vals, off)
+    # records longer than a tile, unaligned lengths
+    lens = rng.integers(4000, 70000, size=12).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    vals = rng.integers(0, 1 << 21, size=int(off[-1])).astype(np.uint32)
+    _check_triage(C, (ms, ns), (om, on), vals, off)
+    assert np.array_equal(ms.export(), om.export())
+
+
+def test_triage_flags_only_matches(C):
+    rng = np.random.default_rng(111)
+    ms, om = C.SignalSet(), O.OSet()
+    vals, off = zipf_batch(rng, 64, 4, 300)
+    flags, dv, do = C.triage_batch(ms, None, vals, off, want_diff=False)
+    assert dv is None and do is None
+    assert np.array_equal(flags, O.triage_flags_only(om, None, vals, off))
+
+
+# ---- manager / fuzzer merges ------------------------------------------------------
+def test_add_inputs_vs_oracle(C):
+    rng = np.random.default_rng(112)
+    cs, ms = C.SignalSet(), C.SignalSet()
+    oc, om = O.OSet(), O.OSet()
+    m0 = rng.integers(0, 5000, size=3000).astype(np.uint32)
+    C.SignalAdd(ms, m0)
+    om.add(m0)
+    for _ in range(3):
+        inputs = [rng.integers(0, 8000, size=int(rng.integers(0, 200))).astype(np.uint32) for _ in range(100)]
+        vals, off = C.to_csr(inputs)
+        C.add_inputs(cs, ms, vals, off)
+        O.add_inputs(oc, om, vals, off)
+        assert np.array_equal(cs.export(), oc.export())
+        assert np.array_equal(ms.export(), om.export())
+
+
+def test_accept_batch_vs_oracle(C):
+    rng = np.random.default_rng(113)
+    cs, cc = C.SignalSet(), C.SignalSet()
+    oc, ov = O.OSet(), O.OSet()
+    for _ in range(3):
+        sig = [C.Canonicalize(rng.integers(0, 3000, size=int(rng.integers(0, 100))).astype(np.uint32))
+               for _ in range(300)]
+        cov = [C.Canonicalize(rng.integers(0, 1 << 30, size=int(rng.integers(0, 50))).astype(np.uint32))
+               for _ in range(300)]
+        sv, so = C.to_csr(sig)
+        cv, co = C.to_csr(cov)
+        acc = C.accept_batch(cs, cc, sv, so, cv, co)
+        eacc = O.accept_batch(oc, ov, sv, so, cv, co)
+        assert np.array_equal(acc, eacc)
+        assert np.array_equal(cs.export(), oc.export())
+        assert np.array_equal(cc.export(), ov.export())
+
+
+def test_merge_poll_vs_oracle(C):
+    rng = np.random.default_rng(114)
+    mm, om = C.SignalSet(), O.OSet()
+    for _ in range(4):
+        polls = [np.unique(rng.integers(0, 20000, size=int(rng.integers(0, 2000)))).astype(np.uint32)
+                 for _ in range(20)]
+        polls = [rng.permutation(p) for p in polls]  # map iteration order
+        polls.append(np.array([5, 5, 6, 5], np.uint32))  # duplicates: first occurrence only
+        av, ao = C.to_csr(polls)
+        nv, no = C.merge_poll(mm, av, ao)
+        ev, eo = O.merge_poll(om, av, ao)
+        assert np.array_equal(no, eo) and np.array_equal(nv, ev)
+    assert np.array_equal(mm.export(), om.export())
+
+
+# ---- executor edge signal (executor.h:389-401, :497-526) --------------------------
+def test_exec_signal_vs_reference_golden(C, exec_golden):
+    g = exec_golden
+    sig, off = C.exec_signal(g["pcs"], g["call_off"], g["prog_off"])
+    assert np.array_equal(off, g["sig_off"])
+    assert np.array_equal(sig, g["sig"])
+
+
+def test_exec_signal_random_vs_oracle(C):
+    rng = np.random.default_rng(115)
+    for nprog, calls, pcs in [(1, 1, 1), (3, 5, 10), (40, 16, 1024), (4, 2, 30000)]:
+        lens = rng.integers(0, 2 * pcs, size=nprog * calls).astype(np.uint64)
+        call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        trace = (0x81000000 + 16 * (np.minimum(rng.zipf(1.1, size=int(call_off[-1])), 1 << 18) - 1)).astype(np.uint32)
+        prog_off = (np.arange(nprog + 1) * calls).astype(np.uint64)
+        a = C.exec_signal(trace, call_off, prog_off)
+        b = O.exec_signal(trace, call_off, prog_off)
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
+
+
+# ---- cover report (syz-manager/cover.go:257-307) ------------------------------------
+def _symtab(rng, nsym, base=0xffffffff81000000):
+    starts = base + 16 * np.sort(rng.choice(nsym * 8, size=nsym, replace=False)).astype(np.uint64)
+    sizes = 16 * rng.integers(1, 8, size=nsym).astype(np.uint64)
+    nxt = np.append(starts[1:], starts[-1] + sizes[-1])
+    ends = np.minimum(starts + sizes, nxt)
+    sites = np.unique(np.concatenate([s + 5 + 16 * np.arange(int((e - s) // 16) + 1, dtype=np.uint64)
+                                      for s, e in zip(starts, ends)]))
+    return starts, ends, sites
+
+
+def test_cover_uncovered_vs_oracle(C):
+    rng = np.random.default_rng(116)
+    for nsym, nq in [(1, 1), (10, 50), (500, 4000), (5000, 100000)]:
+        starts, ends, sites = _symtab(rng, nsym)
+        q = rng.choice(sites, size=nq) + 5 - 0xffffffff00000000
+        q = np.concatenate([q, rng.integers(0, 1 << 32, size=nq // 10, dtype=np.uint64)]).astype(np.uint32)
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        exp = O.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        assert np.array_equal(got, exp), nsym
