@@ -55,9 +55,12 @@ int sg_ctx_create(int device, sg_ctx** out);
 void sg_ctx_destroy(sg_ctx* ctx);
 /* Wait for all work queued on the context's stream. */
 int sg_ctx_sync(sg_ctx* ctx);
-/* Use an external HIP stream (e.g. torch's current stream); NULL restores the
- * context's own stream. */
+/* Queue all further work on `hip_stream` (e.g. torch's current stream; NULL is
+ * the legacy default stream).  The context's own stream is a blocking stream,
+ * i.e. ordered with the legacy default stream. */
 int sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream);
+/* Go back to the context's own stream. */
+int sg_ctx_reset_stream(sg_ctx* ctx);
 void* sg_ctx_stream(sg_ctx* ctx);
 /* Per-kernel device timing with HIP events on the context's stream.
  * enable != 0 starts recording (and resets the tallies). */

@@ -36,6 +36,7 @@ SIGNATURES = {
     "sg_ctx_destroy": (None, [c_void_p]),
     "sg_ctx_sync": (c_int, [c_void_p]),
     "sg_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "sg_ctx_reset_stream": (c_int, [c_void_p]),
     "sg_ctx_stream": (c_void_p, [c_void_p]),
     "sg_ctx_timing": (c_int, [c_void_p, c_int]),
     "sg_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), P64]),

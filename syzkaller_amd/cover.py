@@ -66,7 +66,11 @@ class Context:
         call("sg_ctx_sync", self.h)
 
     def set_stream(self, hip_stream):
-        call("sg_ctx_set_stream", self.h, c_void_p(hip_stream) if hip_stream else None)
+        """Queue on `hip_stream` (an int handle; 0 = the legacy default stream)."""
+        call("sg_ctx_set_stream", self.h, c_void_p(hip_stream))
+
+    def reset_stream(self):
+        call("sg_ctx_reset_stream", self.h)
 
     def timing(self, enable):
         call("sg_ctx_timing", self.h, 1 if enable else 0)

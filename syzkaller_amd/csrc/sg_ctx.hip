@@ -393,7 +393,7 @@ int sg_ctx_create(int device, sg_ctx** out) {
     delete c;
     return rc;
   }
-  e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  e = hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault);  // blocking: ordered with the null stream
   if (e != hipSuccess) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
@@ -437,7 +437,13 @@ int sg_ctx_sync(sg_ctx* ctx) {
 
 int sg_ctx_set_stream(sg_ctx* ctx, void* hip_stream) {
   if (!ctx) return SG_EINVAL;
-  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  ctx->stream = (hipStream_t)hip_stream;  // NULL: the device's legacy default stream
+  return SG_OK;
+}
+
+int sg_ctx_reset_stream(sg_ctx* ctx) {
+  if (!ctx) return SG_EINVAL;
+  ctx->stream = ctx->own_stream;
   return SG_OK;
 }
 
