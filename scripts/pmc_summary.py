@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (separate FETCH_SIZE and WRITE_SIZE runs of
+the same bench command) into profiles/pmc_traffic.json.
+
+Per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half of the bytes of a wide coalesced streaming read, so the
+read side is doubled ("fetch_bytes_x2"); the raw value is kept too.  Only the
+full-size launches of each kernel are summarised (the largest grid)."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+KERNELS = {"triage_claim": "k_claim<true>", "triage_resolve": "k_resolve<true>", "part_hist": "k_part_hist",
+           "part_scatter": "k_part_scatter", "bucket_triage": "k_bucket_triage", "count_missing": "k_count_missing",
+           "emit_scatter": "k_scatter("}
+
+
+def load(path, counter):
+    out = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        for key, pat in KERNELS.items():
+            if pat in r["Kernel_Name"]:
+                out[key].append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0,
+                                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    return out
+
+
+def main(fetch_csv, write_csv, out_json, tag):
+    f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+    res = {"tag": tag, "source": [fetch_csv, write_csv],
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the same command; "
+                     "KiB -> bytes; read side doubled per the gfx950 FETCH_SIZE note (exact for wide streaming reads, "
+                     "uncalibrated for the random 4-B probes)", "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        fl = f.get(k, [])
+        wl = w.get(k, [])
+        if not fl or not wl:
+            continue
+        g = max(x[0] for x in fl)
+        fb = [x[1] for x in fl if x[0] >= 0.9 * g]
+        gw = max(x[0] for x in wl)
+        wb = [x[1] for x in wl if x[0] >= 0.9 * gw]
+        fetch = sum(fb) / len(fb)
+        write = sum(wb) / len(wb)
+        res["kernels"][k] = {"launches": len(fb), "fetch_bytes_raw": fetch, "fetch_bytes_x2": 2 * fetch,
+                             "write_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write}
+    json.dump(res, open(out_json, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])

@@ -390,6 +390,9 @@ static int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, 
                      ctx->stream, a);
   SG_HIP(hipGetLastError());
   SG_HIP(hipMemcpyAsync(out_len, dlen, nseg * 8, hipMemcpyDeviceToHost, ctx->stream));
+  // the chunk / segment descriptors above are host locals: the queued copies
+  // may still read them, so drain before they go out of scope
+  SG_HIP(hipStreamSynchronize(ctx->stream));
   return SG_OK;
 }
 
