@@ -69,21 +69,16 @@ class Poll:
     OR, and an all-gather (RCCL has no bitwise-OR reduction)."""
 
     def __init__(self, world, newbuf):
+        from syzkaller_amd.dist import OrExchange
+
         self.world = world
         self.newbuf = newbuf
-        if world > 1:
-            self.recv = torch.empty_like(newbuf)
-            self.full = torch.empty_like(newbuf)
+        self.ex = OrExchange(newbuf) if world > 1 else None
 
     def __call__(self, maxsig):
-        if self.world > 1:
-            dist.all_to_all_single(self.recv, self.newbuf)
-            shards = self.recv.view(self.world, -1)
-            acc = shards[0].clone()
-            for i in range(1, self.world):
-                acc.bitwise_or_(shards[i])
-            dist.all_gather_into_tensor(self.full, acc)
-            call("sg_set_or_dev", maxsig.h, self.full.data_ptr())
+        if self.ex is not None:
+            merged = self.ex(self.newbuf)
+            call("sg_set_or_dev", maxsig.h, merged.data_ptr())
         self.newbuf.zero_()
 
 
