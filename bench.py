@@ -83,8 +83,30 @@ class Poll:
 
 
 def triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off):
+    """fuzzer.go:645-693 over one batch.  With diff buffers the claim/resolve
+    path also emits the ordered diff lists; without, the partitioned path
+    computes the same flags and set updates (the diff is a transient of the
+    reference loop, fuzzer.go:669-674)."""
     call("sg_triage_batch_dev", ctx.h, maxsig.h, newsig.h, b.vals.data_ptr(), b.off.data_ptr(), b.nvals, b.nrec,
-         rec_new.data_ptr(), diff_vals.data_ptr(), diff_off.data_ptr())
+         rec_new.data_ptr(), diff_vals.data_ptr() if diff_vals is not None else None,
+         diff_off.data_ptr() if diff_off is not None else None)
+
+
+KERNELS = ["part1_hist", "part1_scatter", "part2_hist", "part2_scatter", "bucket_bounds", "bucket_triage",
+           "tile_rec", "triage_claim", "triage_resolve", "scan", "emit"]
+
+
+def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords, nt):
+    """Algorithmic bytes per launch of each kernel."""
+    return {
+        "part1_hist": 4 * n_in + 256 * nt * 4,
+        "part1_scatter": 4 * n_in + 8 * n_in + 256 * nt * 8,
+        "part2_hist": 8 * n_in + 512 * nt * 4,
+        "part2_scatter": 8 * n_in + 8 * n_in + 512 * nt * 8,
+        "bucket_triage": 8 * n_in + 4 * (1 << 27) + 12 * n_newwords + n_rec,
+        "triage_claim": 4 * n_in + 4 * n_in + 8 * n_cand + n_in / 8,
+        "triage_resolve": n_in / 8 + 4 * n_cand + 4 * n_cand + 16 * n_diff + n_rec + n_in / 8 + n_in / 64,
+    }
 
 
 def set_count(s):
@@ -161,6 +183,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-account", action="store_true", help="skip the byte-accounting replay")
+    ap.add_argument("--diff", action="store_true", help="also emit the ordered diff lists (claim/resolve path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -224,8 +247,9 @@ def main():
 
     # warm-up steps (untimed)
     gpu_flags0 = None
+    dv_t, do_t = (diff_vals, diff_off) if args.diff else (None, None)
     for k in range(args.warmup):
-        triage_step(ctx, maxsig, newsig, batches[k], rec_new, diff_vals, diff_off)
+        triage_step(ctx, maxsig, newsig, batches[k], rec_new, dv_t, do_t)
         if k == 0:
             gpu_flags0 = rec_new[: batches[0].nrec].cpu().numpy()
         poll(maxsig)
@@ -246,14 +270,14 @@ def main():
     ctx.timing(True)
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
-        triage_step(ctx, maxsig, newsig, batches[k], rec_new, diff_vals, diff_off)
+        triage_step(ctx, maxsig, newsig, batches[k], rec_new, dv_t, do_t)
         poll(maxsig)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernels = {}
-    for name in ["tile_rec", "triage_claim", "triage_resolve", "scan", "emit"]:
+    for name in KERNELS:
         ms, n = ctx.kernel_time(name)
         if n:
             kernels[name] = {"ms_total": ms, "launches": n}
@@ -274,42 +298,52 @@ def main():
         call("sg_set_copy", maxsig.h, backup.h)
         newbuf.zero_()
         torch.cuda.synchronize()
-        n_in = n_cand = n_diff = n_rec = 0
+        n_in = n_cand = n_diff = n_rec = n_new = n_queued = 0
         for k in range(args.warmup, args.warmup + args.steps):
             b = batches[k]
             c = ctypes_u64()
             call("sg_set_count_missing_dev", maxsig.h, b.vals.data_ptr(), b.nvals, ctypes_byref(c))
+            m_before = len(maxsig)
+            # the diff path here, so the diff element count is known too
             triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off)
             torch.cuda.synchronize()
             n_diff += int(diff_off[b.nrec].item())
+            n_queued += int(rec_new[: b.nrec].sum().item())
+            n_new += len(maxsig) - m_before
             n_in += b.nvals
             n_cand += c.value
             n_rec += b.nrec
             poll(maxsig)
         torch.cuda.synchronize()
-        acct = {"n_in": n_in, "n_cand": n_cand, "n_diff": n_diff, "n_rec": n_rec}
+        acct = {"n_in": n_in, "n_cand": n_cand, "n_diff": n_diff, "n_rec": n_rec, "n_new_signal": n_new,
+                "n_queued": n_queued}
 
     result = None
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
         roof = None
+        pipeline = None
         if acct and kernels:
             L = args.steps
-            n_in, n_cand, n_diff, n_rec = (acct[x] / L for x in ("n_in", "n_cand", "n_diff", "n_rec"))
-            # algorithmic bytes per launch
-            bytes_claim = 4 * n_in + 4 * n_in + 8 * n_cand + n_in / 8
-            bytes_resolve = n_in / 8 + 4 * n_cand + 4 * n_cand + 16 * n_diff + n_rec + n_in / 8 + n_in / 64
-            per = {"triage_claim": bytes_claim, "triage_resolve": bytes_resolve}
+            n_in, n_cand, n_diff, n_rec, n_new = (acct[x] / L for x in ("n_in", "n_cand", "n_diff", "n_rec",
+                                                                         "n_new_signal"))
+            nt = (n_in + 16383) // 16384
+            per = algo_bytes(n_in, n_cand, n_diff, n_rec, min(n_new, 1 << 27), nt)
             for kname, b in per.items():
                 if kname in kernels:
                     avg_s = kernels[kname]["ms_total"] / kernels[kname]["launches"] / 1e3
                     kernels[kname]["avg_ms"] = avg_s * 1e3
                     kernels[kname]["algo_bytes_per_launch"] = b
                     kernels[kname]["achieved_GBs"] = b / avg_s / 1e9
-            dom = max(per, key=lambda k: kernels.get(k, {}).get("ms_total", 0))
+            dom = max((k for k in per if k in kernels), key=lambda k: kernels[k]["ms_total"])
             ach = kernels[dom]["achieved_GBs"]
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom)}
+            # whole-step view with SURVEY.md §8(d)'s C2 formula (N_uniq taken as N_in)
+            b_step = 4 * n_in + 4 * n_in + 8 * n_cand + 4 * n_cand + 4 * n_diff + n_rec / 8
+            pipeline = {"algo_bytes_per_step": b_step, "achieved_GBs": b_step / (ms_step / 1e3) / 1e9,
+                        "frac": b_step / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS,
+                        "formula": "4N_in + 4N_uniq + 8N_cand + 4N_cand + 4N_out + N_rec/8 (N_uniq=N_in)"}
         cpu = None
         if world == 1 and not args.no_cpu and m0_values is not None:
             cpu = cpu_baseline(m0_values, batches[0], cfg, gpu_flags0, args.cpu_budget)
@@ -340,6 +374,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": kernels,
+            "pipeline_roofline": pipeline,
+            "path": "claim/resolve + ordered diff" if args.diff else "partitioned (flags + set updates)",
             "accounting": acct,
             "gen_s": round(t_gen, 2),
         }

@@ -1,0 +1,351 @@
+// sg_bucket.hip -- partitioned new-signal triage (the fast path of
+// sg_triage_batch when the caller does not ask for the ordered diff lists).
+//
+// Reference: syz-fuzzer/fuzzer.go:645-693.  Its observable results are which
+// call records get queued for triage (fuzzer.go:678-690) and the updated
+// maxSignal / newSignal (fuzzer.go:673-674); the diff slice (fuzzer.go:669)
+// is a transient that only feeds those SignalAdd calls.
+//
+// Same first-owner rule as sg_triage.hip (a record is new iff it is the
+// first, in sequential order, to contain some signal s not in maxSignal),
+// organised so that no access is random across HBM:
+//   1. stable LSD partition of (s, record) pairs by bits 15..22 of s,
+//   2. stable LSD partition by bits 23..31 -> pairs grouped by the 17-bit
+//      bucket s >> 15, and inside a bucket still in sequential order,
+//   3. one workgroup per bucket of 32768 signals: its slice of maxSignal
+//      (4 KiB) and a direct first-owner table (32768 x u32 = 128 KiB) live in
+//      LDS; owner = LDS atomicMin of the record index; the record is new iff
+//      it owns some signal; the slice's new bits are written back to
+//      maxSignal and OR-ed into newSignal by the bucket's only writer.
+// No global atomics, no 16 GiB owner table, every HBM stream coalesced.
+//
+// Partition pass = histogram kernel (per 16384-value tile, LDS counters) +
+// device exclusive scan over [digit][tile] + scatter kernel: each wave ranks
+// its 1024 values in order with a ballot multisplit (stable), the tile is
+// reordered by digit in LDS and written out in digit runs.
+#include "sg_internal.h"
+
+namespace sg {
+
+constexpr int kPT = 16384;                  // partition tile (values)
+constexpr int kPThreads = 1024;             // 16 waves
+constexpr int kPWaves = kPThreads / 64;
+constexpr int kPerWave = kPT / kPWaves;     // 1024 values per wave, in order
+constexpr int kBucketBits = 15;             // 32768 signals per bucket
+constexpr uint32_t kNumBuckets = 1u << (32 - kBucketBits);  // 131072
+constexpr int kD0Shift = 15, kD0Bits = 8;   // pass 1 digit: bits 15..22
+constexpr int kD1Shift = 23, kD1Bits = 9;   // pass 2 digit: bits 23..31
+
+struct PartArgs {
+  const uint32_t* vals;    // pass 1 input
+  const uint64_t* pairs;   // pass 2 input: (s << 32) | record
+  uint64_t n;
+  uint64_t ntiles;
+  const uint64_t* rec_off; // pass 1: record offsets (nrec+1)
+  uint64_t nrec;
+  const uint32_t* tile_rec;// pass 1: record of each tile's first value (ntiles+1)
+  uint32_t* hist;          // [digit][tile]
+  const uint64_t* goff;    // scanned hist: output start of (digit, tile)
+  uint64_t* out;           // pairs out
+};
+
+template <int kShift, int kBits>
+__device__ __forceinline__ uint32_t digit_of(uint32_t s) {
+  return (s >> kShift) & ((1u << kBits) - 1);
+}
+
+template <bool kPairs>
+__device__ __forceinline__ uint32_t value_at(const PartArgs& a, uint64_t e) {
+  return kPairs ? (uint32_t)(a.pairs[e] >> 32) : a.vals[e];
+}
+
+// lanes of this wave holding the same digit as this lane (valid lanes only)
+template <int kBits>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < kBits; b++) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(valid && bit);
+    m &= bit ? bb : ~bb;
+  }
+  return valid ? m : 0ull;
+}
+
+template <bool kPairs, int kShift, int kBits>
+__global__ __launch_bounds__(kPThreads) void k_part_hist(PartArgs a) {
+  constexpr int R = 1 << kBits;
+  __shared__ uint32_t cnt[R];
+  for (int i = threadIdx.x; i < R; i += kPThreads) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kPT;
+  for (int i = threadIdx.x; i < kPT; i += kPThreads) {
+    const uint64_t e = t0 + i;
+    if (e < a.n) atomicAdd(&cnt[digit_of<kShift, kBits>(value_at<kPairs>(a, e))], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[(uint64_t)d * a.ntiles + blockIdx.x] = cnt[d];
+}
+
+template <bool kPairs, int kShift, int kBits>
+__global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
+  constexpr int R = 1 << kBits;
+  __shared__ uint64_t stage[kPT];             // the tile, reordered by digit (128 KiB)
+  __shared__ uint16_t cur[kPWaves][R];        // per-wave digit cursors
+  __shared__ uint16_t dstart[R];              // tile-local start of each digit
+  __shared__ uint32_t tot[R];
+  __shared__ uint64_t gbase[R];               // global start of (digit, this tile)
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t tile = blockIdx.x, t0 = tile * kPT;
+  const uint64_t ebase = t0 + (uint64_t)w * kPerWave;
+  for (int d = lane; d < R; d += 64) cur[w][d] = 0;
+  for (int d = tid; d < R; d += kPThreads) gbase[d] = a.goff[(uint64_t)d * a.ntiles + tile];
+  // walk 1: per-wave digit counts, in order
+  for (int k = 0; k < kPerWave / 64; k++) {
+    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
+    const bool v = e < a.n;
+    const uint32_t d = digit_of<kShift, kBits>(v ? value_at<kPairs>(a, e) : 0u);
+    const uint64_t m = match_digit<kBits>(d, v);
+    if (v && !(m & lt)) cur[w][d] += (uint16_t)__popcll(m);
+  }
+  __syncthreads();
+  // exclusive prefix over waves per digit, then over digits
+  for (int d = tid; d < R; d += kPThreads) {
+    uint32_t acc = 0;
+    for (int q = 0; q < kPWaves; q++) {
+      const uint32_t c = cur[q][d];
+      cur[q][d] = (uint16_t)acc;
+      acc += c;
+    }
+    tot[d] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {  // one wave scans the R digit totals
+    uint32_t carry = 0;
+    for (int base = 0; base < R; base += 64) {
+      uint32_t x = tot[base + lane];
+      uint32_t incl = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      dstart[base + lane] = (uint16_t)(carry + incl - x);
+      carry += __shfl(incl, 63);
+    }
+  }
+  __syncthreads();
+  for (int d = lane; d < R; d += 64) cur[w][d] += dstart[d];
+  // record lookup bounds of this tile (pass 1)
+  uint64_t ra = 0, rb = 0;
+  if (!kPairs) {
+    ra = a.tile_rec[tile];
+    rb = a.tile_rec[tile + 1];
+  }
+  // walk 2: stable rank -> LDS position
+  for (int k = 0; k < kPerWave / 64; k++) {
+    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
+    const bool v = e < a.n;
+    uint64_t pair = 0;
+    if (v) {
+      if (kPairs) {
+        pair = a.pairs[e];
+      } else {
+        const uint32_t s = a.vals[e];
+        const uint32_t r = (uint32_t)sgd::seg_search(a.rec_off, ra, rb, e);
+        pair = ((uint64_t)s << 32) | r;
+      }
+    }
+    const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pair >> 32));
+    const uint64_t m = match_digit<kBits>(d, v);
+    if (v) {
+      const uint32_t base = cur[w][d];
+      stage[base + __popcll(m & lt)] = pair;
+      if (!(m & lt)) cur[w][d] = (uint16_t)(base + __popcll(m));
+    }
+  }
+  __syncthreads();
+  // write out in digit runs (consecutive threads -> consecutive addresses)
+  const uint32_t ntile = (uint32_t)(a.n - t0 < (uint64_t)kPT ? a.n - t0 : (uint64_t)kPT);
+  for (uint32_t p = tid; p < ntile; p += kPThreads) {
+    const uint64_t pair = stage[p];
+    const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pair >> 32));
+    a.out[gbase[d] + (p - dstart[d])] = pair;
+  }
+}
+
+__global__ void k_tile_rec_pt(const uint64_t* __restrict__ off, uint64_t nseg, uint64_t n, uint64_t ntiles,
+                              uint32_t* __restrict__ tile_rec) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  uint64_t e = t * kPT;
+  if (e >= n) e = n - 1;
+  tile_rec[t] = (uint32_t)sgd::seg_search(off, 0, nseg - 1, e);
+}
+
+// first pair index of every bucket (pairs grouped by s >> 15, ascending)
+__global__ void k_bucket_bounds(const uint64_t* __restrict__ pairs, uint64_t n, uint64_t* __restrict__ bounds) {
+  uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > kNumBuckets) return;
+  const uint64_t key = b << kBucketBits;  // first signal of bucket b (2^32 for b == kNumBuckets)
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if ((pairs[mid] >> 32) < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  bounds[b] = lo;
+}
+
+struct BucketArgs {
+  const uint64_t* pairs;
+  const uint64_t* bounds;
+  uint32_t* mwords;  // maxSignal
+  uint32_t* nwords;  // newSignal (nullable)
+  uint8_t* rec_new;
+};
+
+__global__ __launch_bounds__(kPThreads) void k_bucket_triage(BucketArgs a) {
+  constexpr uint32_t kSig = 1u << kBucketBits;  // 32768
+  constexpr uint32_t kWords = kSig / 32;       // 1024
+  __shared__ __attribute__((aligned(16))) uint32_t owner[kSig];  // 128 KiB
+  __shared__ uint32_t mslice[kWords];
+  const uint32_t b = blockIdx.x;
+  const uint64_t lo = a.bounds[b], hi = a.bounds[b + 1];
+  if (lo == hi) return;  // no signal of this batch falls in the bucket
+  const int tid = threadIdx.x;
+  uint32_t* mg = a.mwords + (uint64_t)b * kWords;
+  for (uint32_t i = tid; i < kWords; i += kPThreads) mslice[i] = mg[i];
+  uint4* o4 = reinterpret_cast<uint4*>(owner);
+  for (uint32_t i = tid; i < kSig / 4; i += kPThreads) o4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  __syncthreads();
+  // owner(s) = first record (minimum index) holding s, among s not in maxSignal
+  for (uint64_t i = lo + tid; i < hi; i += kPThreads) {
+    const uint64_t p = a.pairs[i];
+    const uint32_t sl = (uint32_t)(p >> 32) & (kSig - 1);
+    if (!((mslice[sl >> 5] >> (sl & 31)) & 1u)) atomicMin(&owner[sl], (uint32_t)p);
+  }
+  __syncthreads();
+  // a record is queued iff it owns some signal (fuzzer.go:666, :678-690)
+  for (uint64_t i = lo + tid; i < hi; i += kPThreads) {
+    const uint64_t p = a.pairs[i];
+    const uint32_t sl = (uint32_t)(p >> 32) & (kSig - 1);
+    const uint32_t r = (uint32_t)p;
+    if (owner[sl] == r) a.rec_new[r] = 1;  // owner set => s was not in maxSignal
+  }
+  // new bits of the slice: maxSignal |= new, newSignal |= new (fuzzer.go:673-674)
+  const int w = tid >> 6, lane = tid & 63;
+  for (uint32_t base = (uint32_t)w * 64; base < kSig; base += kPThreads) {
+    const uint64_t nb = __ballot(owner[base + lane] != ~0u);
+    if (lane == 0 && nb) {
+      const uint32_t wi = base >> 5;
+      const uint32_t lo32 = (uint32_t)nb, hi32 = (uint32_t)(nb >> 32);
+      if (lo32) {
+        mg[wi] = mslice[wi] | lo32;
+        if (a.nwords) a.nwords[(uint64_t)b * kWords + wi] |= lo32;
+      }
+      if (hi32) {
+        mg[wi + 1] = mslice[wi + 1] | hi32;
+        if (a.nwords) a.nwords[(uint64_t)b * kWords + wi + 1] |= hi32;
+      }
+    }
+  }
+}
+
+size_t bucket_ws_bytes(uint64_t n) {
+  const uint64_t nt = (n + kPT - 1) / kPT;
+  WsPlan p;
+  p.add(n * 8);
+  p.add(n * 8);
+  p.add((uint64_t)(1 << kD0Bits) * nt * 4);
+  p.add(((uint64_t)(1 << kD0Bits) * nt + 1) * 8);
+  p.add((uint64_t)(1 << kD1Bits) * nt * 4);
+  p.add(((uint64_t)(1 << kD1Bits) * nt + 1) * 8);
+  p.add((nt + 1) * 4);
+  p.add(((uint64_t)kNumBuckets + 1) * 8);
+  return p.total + scan_ws_bytes((uint64_t)(1 << kD1Bits) * nt);
+}
+
+// Flags-only triage of a device-resident batch (ctx lock held, ws reserved).
+int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
+  if (nrec >= 0xFFFFFFFFull) {
+    set_error("bucket triage: record index must fit 32 bits");
+    return SG_EINVAL;
+  }
+  if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
+  if (n == 0) return SG_OK;
+  const uint64_t nt = (n + kPT - 1) / kPT;
+  WsPlan p;
+  const size_t oA = p.add(n * 8), oB = p.add(n * 8);
+  const size_t oH1 = p.add((uint64_t)(1 << kD0Bits) * nt * 4), oO1 = p.add(((uint64_t)(1 << kD0Bits) * nt + 1) * 8);
+  const size_t oH2 = p.add((uint64_t)(1 << kD1Bits) * nt * 4), oO2 = p.add(((uint64_t)(1 << kD1Bits) * nt + 1) * 8);
+  const size_t oTR = p.add((nt + 1) * 4), oBB = p.add(((uint64_t)kNumBuckets + 1) * 8);
+  const size_t scan_off = p.total;
+  int rc = ws_reserve(ctx, bucket_ws_bytes(n));
+  if (rc) return rc;
+  uint64_t* A = (uint64_t*)ws_at(ctx, oA);
+  uint64_t* B = (uint64_t*)ws_at(ctx, oB);
+  PartArgs pa{};
+  pa.n = n;
+  pa.ntiles = nt;
+  pa.rec_off = d_off;
+  pa.nrec = nrec;
+  pa.tile_rec = (uint32_t*)ws_at(ctx, oTR);
+  hipLaunchKernelGGL(k_tile_rec_pt, dim3(div_up(nt + 1, 256)), dim3(256), 0, ctx->stream, d_off, nrec, n, nt,
+                     (uint32_t*)pa.tile_rec);
+  {
+    ScopedTimer tm(ctx, "part1_hist");
+    pa.vals = d_vals;
+    pa.hist = (uint32_t*)ws_at(ctx, oH1);
+    hipLaunchKernelGGL((k_part_hist<false, kD0Shift, kD0Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream,
+                       pa);
+  }
+  rc = scan_counts(ctx, pa.hist, (uint64_t*)ws_at(ctx, oO1), (uint64_t)(1 << kD0Bits) * nt, scan_off);
+  if (rc) return rc;
+  {
+    ScopedTimer tm(ctx, "part1_scatter");
+    pa.goff = (uint64_t*)ws_at(ctx, oO1);
+    pa.out = A;
+    hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                       ctx->stream, pa);
+  }
+  {
+    ScopedTimer tm(ctx, "part2_hist");
+    pa.vals = nullptr;
+    pa.pairs = A;
+    pa.hist = (uint32_t*)ws_at(ctx, oH2);
+    hipLaunchKernelGGL((k_part_hist<true, kD1Shift, kD1Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream,
+                       pa);
+  }
+  rc = scan_counts(ctx, pa.hist, (uint64_t*)ws_at(ctx, oO2), (uint64_t)(1 << kD1Bits) * nt, scan_off);
+  if (rc) return rc;
+  {
+    ScopedTimer tm(ctx, "part2_scatter");
+    pa.goff = (uint64_t*)ws_at(ctx, oO2);
+    pa.out = B;
+    hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                       ctx->stream, pa);
+  }
+  BucketArgs ba{};
+  ba.pairs = B;
+  ba.bounds = (uint64_t*)ws_at(ctx, oBB);
+  ba.mwords = mwords;
+  ba.nwords = nwords;
+  ba.rec_new = d_rec_new;
+  {
+    ScopedTimer tm(ctx, "bucket_bounds");
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(div_up((uint64_t)kNumBuckets + 1, 256)), dim3(256), 0, ctx->stream, B,
+                       n, (uint64_t*)ba.bounds);
+  }
+  {
+    ScopedTimer tm(ctx, "bucket_triage");
+    hipLaunchKernelGGL(k_bucket_triage, dim3(kNumBuckets), dim3(kPThreads), 0, ctx->stream, ba);
+  }
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+}  // namespace sg

@@ -140,6 +140,10 @@ struct OwnerJob {
 int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint64_t* d_cmask, uint64_t* d_dmask,
                         uint32_t* d_tile_rec, uint8_t* d_seg_flag, uint32_t* set_a, uint32_t* set_b);
 
+// Partitioned flags-only triage (sg_bucket.hip); ctx lock held.
+int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new);
+
 }  // namespace sg
 
 // ---- device helpers -------------------------------------------------------

@@ -428,6 +428,9 @@ int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint3
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = check_alloc(ctx);
   if (rc) return rc;
+  if (!d_diff_vals && !d_diff_off)  // flags + set updates only: partitioned path
+    return bucket_triage(ctx, maxsig->words, newsig ? newsig->words : nullptr, d_vals, d_rec_off, nvals, nrec,
+                         d_rec_new);
   WsPlan p;
   size_t o[5];
   size_t scan_b = scratch_plan(p, nvals, o);

@@ -180,10 +180,38 @@ def test_signal_set_ops(C):
 
 
 # ---- the hot path: batched new-signal triage (fuzzer.go:645-693) ----------------
-def _check_triage(C, sets, osets, vals, off):
-    ms, ns = sets
+class TwoPaths:
+    """The same sets kept twice: one pair driven through the diff-emitting
+    claim/resolve path, one through the flags-only partitioned path."""
+
+    def __init__(self, C):
+        self.C = C
+        self.d = (C.SignalSet(), C.SignalSet())
+        self.f = (C.SignalSet(), C.SignalSet())
+
+    def add(self, vals):
+        self.C.SignalAdd(self.d[0], vals)
+        self.C.SignalAdd(self.f[0], vals)
+
+    def clear(self):
+        for s in self.d + self.f:
+            s.clear()
+
+    def triage(self, vals, off):
+        flags, dv, do = self.C.triage_batch(self.d[0], self.d[1], vals, off)
+        fflags, _, _ = self.C.triage_batch(self.f[0], self.f[1], vals, off, want_diff=False)
+        assert np.array_equal(flags, fflags), "partitioned path disagrees with the claim/resolve path"
+        return flags, dv, do
+
+    def exports(self):
+        m, n = self.d[0].export(), self.d[1].export()
+        assert np.array_equal(m, self.f[0].export()) and np.array_equal(n, self.f[1].export())
+        return m, n
+
+
+def _check_triage(P, osets, vals, off):
     om, on = osets
-    flags, dv, do = C.triage_batch(ms, ns, vals, off)
+    flags, dv, do = P.triage(vals, off)
     ef, ev, eo = O.triage_batch(om, on, vals, off)
     assert np.array_equal(flags, ef)
     assert np.array_equal(do, eo)
@@ -193,45 +221,50 @@ def _check_triage(C, sets, osets, vals, off):
 
 def test_triage_small_vs_python(C):
     rng = np.random.default_rng(108)
-    ms, ns = C.SignalSet(), C.SignalSet()
+    P = TwoPaths(C)
     for it in range(60):
-        ms.clear()
-        ns.clear()
+        P.clear()
         nrec = int(rng.integers(0, 40))
         recs = [[int(x) for x in rng.integers(0, 80, size=rng.integers(0, 14))] for _ in range(nrec)]
         if it % 4 == 0 and nrec:
             recs[0] += [0, SENT, SENT]
+        if it % 3 == 0:  # spread over many partition buckets
+            recs = [[(x * 0x9E3779B1) & 0xFFFFFFFF for x in r] for r in recs]
         m0 = sorted(set(int(x) for x in rng.integers(0, 80, size=rng.integers(0, 50))))
-        C.SignalAdd(ms, np.array(m0, np.uint32))
+        if it % 3 == 0:
+            m0 = sorted(set((x * 0x9E3779B1) & 0xFFFFFFFF for x in m0))
+        P.add(np.array(m0, np.uint32))
         vals = np.array([x for r in recs for x in r], dtype=np.uint32)
         off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
-        flags, dv, do = C.triage_batch(ms, ns, vals, off)
+        flags, dv, do = P.triage(vals, off)
         pm, pn = set(m0), set()
         pf, pd = R.triage(pm, pn, recs)
         assert list(flags) == pf
         assert [list(dv[int(do[r]):int(do[r + 1])]) for r in range(nrec)] == pd
-        assert set(ms.export().tolist()) == pm and set(ns.export().tolist()) == pn
+        m, n = P.exports()
+        assert set(m.tolist()) == pm and set(n.tolist()) == pn
 
 
 def test_triage_zipf_sequence_vs_oracle(C):
     """Several consecutive batches against the same sets (the fuzzer's steady
     state): exercises the decreasing owner-key generations."""
     rng = np.random.default_rng(109)
-    ms, ns = C.SignalSet(), C.SignalSet()
+    P = TwoPaths(C)
     om, on = O.OSet(), O.OSet()
     warm, _ = zipf_batch(rng, 64, 8, 256)
-    C.SignalAdd(ms, warm)
+    P.add(warm)
     om.add(warm)
     for b in range(6):
         vals, off = zipf_batch(rng, 128, 8, 512, ragged=(b % 2 == 1))
-        flags = _check_triage(C, (ms, ns), (om, on), vals, off)
+        flags = _check_triage(P, (om, on), vals, off)
         assert flags.sum() > 0
-    assert np.array_equal(ms.export(), om.export())
-    assert np.array_equal(ns.export(), on.export())
+    m, n = P.exports()
+    assert np.array_equal(m, om.export())
+    assert np.array_equal(n, on.export())
 
 
 def test_triage_edge_cases(C):
-    ms, ns = C.SignalSet(), C.SignalSet()
+    P = TwoPaths(C)
     om, on = O.OSet(), O.OSet()
     cases = [
         (np.array([], np.uint32), np.array([0], np.uint64)),                  # no records
@@ -242,19 +275,25 @@ def test_triage_edge_cases(C):
         (np.arange(10000, dtype=np.uint32), np.array([0, 10000], np.uint64)),  # everything already known
     ]
     for vals, off in cases:
-        _check_triage(C, (ms, ns), (om, on), vals, off)
+        _check_triage(P, (om, on), vals, off)
     # many empty records around tile boundaries (record window > LDS window)
     rng = np.random.default_rng(110)
     lens = np.where(rng.random(20000) < 0.9, 0, rng.integers(1, 30, size=20000)).astype(np.uint64)
     off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     vals = rng.integers(0, 1 << 20, size=int(off[-1])).astype(np.uint32)
-    _check_triage(C, (ms, ns), (om, on), vals, off)
-    # records longer than a tile, unaligned lengths
+    _check_triage(P, (om, on), vals, off)
+    # records longer than a tile, unaligned lengths, one of them reaching every partition bucket
     lens = rng.integers(4000, 70000, size=12).astype(np.uint64)
     off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     vals = rng.integers(0, 1 << 21, size=int(off[-1])).astype(np.uint32)
-    _check_triage(C, (ms, ns), (om, on), vals, off)
-    assert np.array_equal(ms.export(), om.export())
+    vals[: int(lens[0])] = rng.integers(0, 1 << 32, size=int(lens[0]), dtype=np.uint64).astype(np.uint32)
+    _check_triage(P, (om, on), vals, off)
+    # a skewed batch: every value in one 32768-signal bucket, heavily repeated
+    vals = (0xABC00000 + rng.integers(0, 32768, size=300000)).astype(np.uint32)
+    off = np.concatenate([[0], np.sort(rng.integers(0, vals.size, size=999)), [vals.size]]).astype(np.uint64)
+    _check_triage(P, (om, on), vals, off)
+    m, n = P.exports()
+    assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
 
 
 def test_triage_flags_only_matches(C):
@@ -264,6 +303,7 @@ def test_triage_flags_only_matches(C):
     flags, dv, do = C.triage_batch(ms, None, vals, off, want_diff=False)
     assert dv is None and do is None
     assert np.array_equal(flags, O.triage_flags_only(om, None, vals, off))
+    assert np.array_equal(ms.export(), om.export())
 
 
 # ---- manager / fuzzer merges ------------------------------------------------------
