@@ -136,17 +136,18 @@ __global__ __launch_bounds__(kBlock) void k_claim(PipeArgs a) {
       win_setup(a, tile, win, w);
       __syncthreads();
     }
-    uint32_t bits = cand;
-    while (bits) {
-      int b = __ffs(bits) - 1;
-      bits &= bits - 1;
-      int j = b >> 2, k = b & 3;
-      uint64_t e = chunk_of(tile, j, wave) * kChunk + lane * 4 + k;
-      uint64_t r = kSeg ? win_lookup(a, win, w, e) : e;
-      uint32_t rk = a.rank ? a.rank[r] : (uint32_t)r;
-      uint32_t key = a.key_lo + rk;
-      uint32_t* p = a.owner + x[j][k];
-      if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > key) atomicMin(p, key);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {  // static indices keep x[][] in registers
+        if (!((cand >> (4 * j + k)) & 1u)) continue;
+        uint64_t e = chunk_of(tile, j, wave) * kChunk + lane * 4 + k;
+        uint64_t r = kSeg ? win_lookup(a, win, w, e) : e;
+        uint32_t rk = a.rank ? a.rank[r] : (uint32_t)r;
+        uint32_t key = a.key_lo + rk;
+        uint32_t* p = a.owner + x[j][k];
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > key) atomicMin(p, key);
+      }
     }
   }
 #pragma unroll
