@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""bench_rows.py -- secondary measurements of the other SURVEY.md §8 rows on one
+MI355X (bench.py is the driver's headline; this one is for the §8 table).
+
+One JSON line per row, each with the row's device time (HIP-event kernel
+timers of libsyzsig on its stream), the end-to-end time of the host entry
+point (PCIe staging included), and the oracle on a bounded sample:
+
+  c1  pkg/cover Union/Difference (cover.go:42-102): 1000 canonical traces x 4096
+      PCs vs a canonical 1M-PC corpus signal (BASELINE.json configs[0]).
+  c4  cover.Minimize / minimizeCorpus (cover.go:120-146, manager.go:769-784):
+      500k corpus programs, lognormal lengths (median 1k, clipped [1, 16k]).
+  c5  cover report (syz-manager/cover.go:257-307): 100M PCs vs 5M sorted call
+      sites and 50k symbols.
+  a0  executor edge signal (executor.h:389-401, :497-526): 8192 programs x 16
+      calls x 1024 PCs.
+Usage: python bench_rows.py [c1 c4 c5 a0]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from syzkaller_amd import cover as C  # noqa: E402
+
+HBM = 8000.0
+
+
+def zipf_vals(rng, n, s=1.1, nranks=1 << 20):
+    r = np.minimum(rng.zipf(s, size=n), nranks) - 1
+    return (0x81000000 + 16 * r).astype(np.uint32)
+
+
+def ktime(ctx, names):
+    out = {}
+    for n in names:
+        ms, k = ctx.kernel_time(n)
+        if k:
+            out[n] = ms
+    return out
+
+
+def row_c1(ctx, rng):
+    from oracle import pyoracle as O
+
+    corpus = (0x81000000 + 16 * np.sort(rng.choice(1 << 22, size=1_000_000, replace=False))).astype(np.uint32)
+    traces = [np.unique(zipf_vals(rng, 6000, s=0.9, nranks=1 << 22))[:4096] for _ in range(1000)]
+    a = np.concatenate(traces)
+    a_len = np.array([t.size for t in traces], np.uint64)
+    a_beg = np.concatenate([[0], np.cumsum(a_len)[:-1]]).astype(np.uint64)
+    b_beg = np.zeros(1000, np.uint64)
+    b_len = np.full(1000, corpus.size, np.uint64)
+    res = {}
+    for op, name in [(2, "Union"), (0, "Difference")]:
+        C.merge_batch(op, a, a_beg, a_len, corpus, b_beg[:1], b_len[:1], ctx=ctx)  # warm
+        ctx.timing(True)
+        t0 = time.perf_counter()
+        out = C.merge_batch(op, a, a_beg, a_len, corpus, b_beg, b_len, ctx=ctx)
+        wall = time.perf_counter() - t0
+        kt = ktime(ctx, ["merge_keep", "merge_scatter", "scan"])
+        ctx.timing(False)
+        dev_ms = sum(kt.values())
+        n_in = int(a.size + 1000 * corpus.size)
+        n_out = sum(o.size for o in out)
+        algo = 4 * (n_in + n_out)
+        # oracle on a sample of 20 pairs
+        t1 = time.perf_counter()
+        for k in range(20):
+            assert np.array_equal(out[k], O.foreach(op, traces[k], corpus))
+        cpu_s = (time.perf_counter() - t1) / 20 * 1000
+        res[name] = {"pairs": 1000, "elements_in": n_in, "elements_out": n_out, "device_ms": dev_ms,
+                     "kernels_ms": kt, "wall_ms_host_api": wall * 1e3,
+                     "device_GBs_algo": algo / (dev_ms / 1e3) / 1e9, "frac_hbm": algo / (dev_ms / 1e3) / 1e9 / HBM,
+                     "cpu_oracle_ms_est_1000_pairs": cpu_s * 1e3, "parity_sample_20": True}
+    return {"row": "c1 pkg/cover merge ops", **res}
+
+
+def row_c4(ctx, rng):
+    from oracle import pyoracle as O
+
+    n = 500_000
+    lens = np.clip(np.exp(rng.normal(np.log(1000), 1.0, size=n)), 1, 16384).astype(np.int64)
+    vals = zipf_vals(rng, int(lens.sum()), s=1.1, nranks=1 << 22)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    order = C.minimize_order(off)
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    sel = C.minimize_csr(vals, off, order, ctx=ctx)
+    wall = time.perf_counter() - t0
+    kt = ktime(ctx, ["tile_rec", "triage_claim", "triage_resolve", "scan", "emit"])
+    ctx.timing(False)
+    dev_ms = sum(kt.values())
+    N = int(vals.size)
+    algo = 4 * N + 8 * N + 4 * N + n / 8
+    t1 = time.perf_counter()
+    ref = O.minimize(vals, off, order)
+    cpu = time.perf_counter() - t1
+    return {"row": "c4 cover.Minimize", "inputs": n, "elements": N, "selected": int(sel.size),
+            "parity_full": bool(np.array_equal(sel, ref)), "device_ms": dev_ms, "kernels_ms": kt,
+            "wall_ms_host_api": wall * 1e3, "device_GBs_algo": algo / (dev_ms / 1e3) / 1e9,
+            "frac_hbm": algo / (dev_ms / 1e3) / 1e9 / HBM, "cpu_oracle_s": cpu, "cpu_cores": 1}
+
+
+def row_c5(ctx, rng):
+    from oracle import pyoracle as O
+
+    nsym, nsites, nq = 50_000, 5_000_000, 100_000_000
+    base = 0xffffffff81000000
+    sizes = 16 * (1 + rng.integers(0, 2 * nsites // nsym, size=nsym)).astype(np.uint64)
+    starts = base + np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    ends = starts + sizes
+    per = (sizes // 16).astype(np.int64)
+    sites = np.concatenate([s + 5 + 16 * np.arange(k, dtype=np.uint64) for s, k in zip(starts, per)])[:nsites]
+    q = (rng.choice(sites[: nsites // 2], size=nq) + 5 - (np.uint64(0xffffffff) << np.uint64(32))).astype(np.uint32)
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites, ctx=ctx)
+    wall = time.perf_counter() - t0
+    kt = ktime(ctx, ["report_query"])
+    ctx.timing(False)
+    sample = 2_000_000
+    t1 = time.perf_counter()
+    ref = O.cover_uncovered(q[:sample], 0xffffffff, starts, ends, sites)
+    cpu = time.perf_counter() - t1
+    got_s = C.cover_uncovered(q[:sample], 0xffffffff, starts, ends, sites, ctx=ctx)
+    algo = 16 * nq
+    return {"row": "c5 cover report", "queries": nq, "sites": int(sites.size), "symbols": nsym,
+            "uncovered": int(got.size), "device_ms_query_kernel": kt.get("report_query"),
+            "wall_ms_host_api": wall * 1e3,
+            "query_GBs_algo": algo / (kt["report_query"] / 1e3) / 1e9 if kt.get("report_query") else None,
+            "parity_2M_prefix": bool(np.array_equal(got_s, ref)), "cpu_oracle_s_2M": cpu, "cpu_cores": 1}
+
+
+def row_a0(ctx, rng):
+    import torch
+
+    from syzkaller_amd._lib import call
+
+    nprog, calls, pcs = 8192, 16, 1024
+    npcs, ncalls = nprog * calls * pcs, nprog * calls
+    tr = torch.empty(npcs, dtype=torch.int32, device="cuda")
+    out = torch.empty(npcs, dtype=torch.int32, device="cuda")
+    co = torch.arange(0, npcs + 1, pcs, dtype=torch.int64, device="cuda")
+    po = torch.arange(0, ncalls + 1, calls, dtype=torch.int64, device="cuda")
+    so = torch.empty(ncalls + 1, dtype=torch.int64, device="cuda")
+    call("sg_gen_zipf_traces_dev", ctx.h, 0x5A17C0DE, 7, 1.1, 1 << 20, 0, nprog, calls, pcs, tr.data_ptr())
+    ctx.timing(True)
+    call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), co.data_ptr(), po.data_ptr(), nprog, ncalls, npcs,
+         out.data_ptr(), so.data_ptr())
+    kt = ktime(ctx, ["exec_signal", "exec_compact", "scan"])
+    ctx.timing(False)
+    return {"row": "a0 executor edge signal", "pcs": npcs, "signal_out": int(so[-1].item()), "kernels_ms": kt,
+            "pcs_per_s": npcs / (sum(kt.values()) / 1e3)}
+
+
+def main():
+    import torch
+
+    torch.cuda.set_device(0)
+    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0"]
+    ctx = C.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(2026)
+    for r in rows:
+        res = globals()["row_" + r](ctx, rng)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

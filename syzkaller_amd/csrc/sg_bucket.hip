@@ -20,7 +20,7 @@
 //      redone by a second kernel with a direct 32768-entry LDS table.
 // No global atomics, no 16 GiB owner table, every HBM stream coalesced.
 //
-// Partition pass = histogram kernel (per 16384-value tile, LDS counters) +
+// Partition pass = histogram kernel (per 8192-value tile, LDS counters) +
 // device exclusive scan over [digit][tile] + scatter kernel: each wave holds
 // its 1024 values in registers, ranks them in order with a ballot multisplit
 // (stable), the tile is reordered by digit in LDS and written out in digit
@@ -29,8 +29,8 @@
 
 namespace sg {
 
-constexpr int kPT = 16384;                  // partition tile (values)
-constexpr int kPThreads = 1024;             // 16 waves
+constexpr int kPT = 8192;                   // partition tile (values): LDS fits two tiles per CU
+constexpr int kPThreads = 512;              // 8 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;     // 1024 values per wave, in order
 constexpr int kSteps = kPerWave / 64;       // 16 values per lane
@@ -40,7 +40,7 @@ constexpr uint32_t kBucketWords = kBucketSig / 32;  // 1024
 constexpr uint32_t kNumBuckets = 1u << (32 - kBucketBits);  // 131072
 constexpr int kD0Shift = 15, kD0Bits = 8;   // pass 1 digit: bits 15..22
 constexpr int kD1Shift = 23, kD1Bits = 9;   // pass 2 digit: bits 23..31
-constexpr int kRecWin = 1024;               // record offsets kept in LDS per tile
+constexpr int kRecWin = 512;                // record offsets kept in LDS per tile
 constexpr int kBTThreads = 512;             // bucket kernel
 constexpr int kHashBits = 11;
 constexpr int kHash = 1 << kHashBits;       // candidate hash slots per bucket
@@ -131,7 +131,7 @@ template <bool kPairs, int kShift, int kBits>
 __global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
   constexpr int R = 1 << kBits;
   constexpr int W = kPairs ? 1 : kRecWin;
-  __shared__ uint64_t stage[kPT];             // the tile, reordered by digit (128 KiB)
+  __shared__ uint64_t stage[kPT];             // the tile, reordered by digit (64 KiB)
   __shared__ uint16_t cur[kPWaves][R];        // per-wave digit cursors
   __shared__ uint16_t dstart[R];              // tile-local start of each digit
   __shared__ uint32_t tot[R];

@@ -65,6 +65,21 @@ int pin_reserve(sg_ctx* ctx, size_t bytes) {
   return SG_OK;
 }
 
+int dstage_reserve(sg_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->dstage_cap) return SG_OK;
+  size_t cap = ctx->dstage_cap ? ctx->dstage_cap : (16u << 20);
+  while (cap < bytes) cap *= 2;
+  if (ctx->dstage) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    SG_HIP(hipFree(ctx->dstage));
+    ctx->dstage = nullptr;
+    ctx->dstage_cap = 0;
+  }
+  SG_HIP(hipMalloc(&ctx->dstage, cap));
+  ctx->dstage_cap = cap;
+  return SG_OK;
+}
+
 int owner_keys(sg_ctx* ctx, uint64_t nkeys, uint32_t* key_lo) {
   if (nkeys >= kOwnerInf) {
     set_error("batch of %llu keys exceeds the 32-bit first-owner key space", (unsigned long long)nkeys);
@@ -420,6 +435,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   for (auto ev : ctx->timer.pool) hipEventDestroy(ev);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->pin) hipHostFree(ctx->pin);
+  if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);
   if (ctx->dscal) hipFree(ctx->dscal);
   if (ctx->gen_prob) hipFree(ctx->gen_prob);

@@ -208,15 +208,17 @@ int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, c
   uint64_t ncalls = prog_off[nprog];
   uint64_t npcs = call_off[ncalls];
   if (prog_off[0] != 0 || call_off[0] != 0 || (npcs && (!pcs || !sig_vals))) return SG_EINVAL;
+  char* st = nullptr;
+  size_t b0 = (npcs * 4 + 255) & ~size_t(255), b1 = ((ncalls + 1) * 8 + 255) & ~size_t(255),
+         b2 = ((nprog + 1) * 8 + 255) & ~size_t(255);
   {
     std::lock_guard<std::mutex> g(ctx->mu);
     int rc = ensure_device(ctx);
     if (rc) return rc;
+    rc = dstage_reserve(ctx, 2 * b0 + 2 * b1 + b2 + 256);
+    if (rc) return rc;
+    st = (char*)ctx->dstage;
   }
-  char* st = nullptr;
-  size_t b0 = (npcs * 4 + 255) & ~size_t(255), b1 = ((ncalls + 1) * 8 + 255) & ~size_t(255),
-         b2 = ((nprog + 1) * 8 + 255) & ~size_t(255);
-  SG_HIP(hipMallocAsync((void**)&st, 2 * b0 + 2 * b1 + b2 + 256, ctx->stream));
   uint32_t* dp = (uint32_t*)st;
   uint32_t* dsv = (uint32_t*)(st + b0);
   uint64_t* dco = (uint64_t*)(st + 2 * b0);
@@ -226,14 +228,10 @@ int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, c
   SG_HIP(hipMemcpyAsync(dco, call_off, (ncalls + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(dpo, prog_off, (nprog + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   int rc = sg_exec_signal_dev(ctx, dp, dco, dpo, nprog, ncalls, npcs, dsv, dso);
-  if (rc) {
-    hipFreeAsync(st, ctx->stream);
-    return rc;
-  }
+  if (rc) return rc;
   SG_HIP(hipMemcpyAsync(sig_off, dso, (ncalls + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   if (sig_off[ncalls]) SG_HIP(hipMemcpyAsync(sig_vals, dsv, sig_off[ncalls] * 4, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipFreeAsync(st, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   return SG_OK;
 }

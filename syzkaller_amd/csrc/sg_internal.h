@@ -59,6 +59,9 @@ struct sg_ctx {
   size_t ws_cap = 0;
   void* pin = nullptr;
   size_t pin_cap = 0;
+  // grow-only device staging for the host entry points' inputs / outputs
+  void* dstage = nullptr;
+  size_t dstage_cap = 0;
   // first-owner table and its decreasing key floor
   uint32_t* owner = nullptr;
   uint64_t owner_floor = 0;
@@ -107,6 +110,7 @@ struct WsPlan {
 int ws_reserve(sg_ctx* ctx, size_t bytes);
 inline void* ws_at(sg_ctx* ctx, size_t off) { return (char*)ctx->ws + off; }
 int pin_reserve(sg_ctx* ctx, size_t bytes);
+int dstage_reserve(sg_ctx* ctx, size_t bytes);
 // Reserve `nkeys` first-owner keys: returns key_lo such that keys
 // key_lo .. key_lo+nkeys-1 are below every key already stored in the table.
 int owner_keys(sg_ctx* ctx, uint64_t nkeys, uint32_t* key_lo);

@@ -509,16 +509,13 @@ int sg_canonicalize_batch(sg_ctx* ctx, uint32_t* vals, const uint64_t* off, size
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
-  uint32_t* dv = nullptr;
-  SG_HIP(hipMallocAsync((void**)&dv, n * 4, ctx->stream));
+  rc = dstage_reserve(ctx, n * 4);
+  if (rc) return rc;
+  uint32_t* dv = (uint32_t*)ctx->dstage;
   SG_HIP(hipMemcpyAsync(dv, vals, n * 4, hipMemcpyHostToDevice, ctx->stream));
   rc = canonicalize_dev(ctx, dv, off, nseg, out_len);
-  if (rc) {
-    hipFreeAsync(dv, ctx->stream);
-    return rc;
-  }
+  if (rc) return rc;
   SG_HIP(hipMemcpyAsync(vals, dv, n * 4, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipFreeAsync(dv, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   return SG_OK;
 }

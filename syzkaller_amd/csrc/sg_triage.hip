@@ -491,17 +491,20 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
   uint8_t* dflag;
   uint32_t* ddv;
   uint64_t* ddo;
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    int rc = check_alloc(ctx);
-    if (rc) return rc;
-  }
-  // separate allocation for the staged batch so the workspace stays free
+  // staged batch lives in the context's device staging buffer (the workspace
+  // stays free for the pipeline)
   size_t b_vals = (nvals * 4 + 255) & ~size_t(255), b_off = ((nrec + 1) * 8 + 255) & ~size_t(255),
          b_flag = (nrec + 256) & ~size_t(255);
   size_t b_dv = want_diff ? b_vals : 0, b_do = want_diff ? b_off : 0;
   char* stage = nullptr;
-  SG_HIP(hipMallocAsync((void**)&stage, b_vals + b_off + b_flag + b_dv + b_do + 256, ctx->stream));
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int rc = check_alloc(ctx);
+    if (rc) return rc;
+    rc = dstage_reserve(ctx, b_vals + b_off + b_flag + b_dv + b_do + 256);
+    if (rc) return rc;
+    stage = (char*)ctx->dstage;
+  }
   dv = (uint32_t*)stage;
   doff = (uint64_t*)(stage + b_vals);
   dflag = (uint8_t*)(stage + b_vals + b_off);
@@ -510,17 +513,13 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
   if (nvals) SG_HIP(hipMemcpyAsync(dv, vals, nvals * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(doff, rec_off, (nrec + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   int rc = sg_triage_batch_dev(ctx, maxsig, newsig, dv, doff, nvals, nrec, dflag, ddv, ddo);
-  if (rc) {
-    hipFreeAsync(stage, ctx->stream);
-    return rc;
-  }
+  if (rc) return rc;
   if (nrec) SG_HIP(hipMemcpyAsync(rec_new, dflag, nrec, hipMemcpyDeviceToHost, ctx->stream));
   uint64_t total = 0;
   if (want_diff) SG_HIP(hipMemcpyAsync(&total, ddo + nrec, 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   if (diff_off) SG_HIP(hipMemcpyAsync(diff_off, ddo, (nrec + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   if (diff_vals && total) SG_HIP(hipMemcpyAsync(diff_vals, ddv, total * 4, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipFreeAsync(stage, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   if (n_diff) *n_diff = total;
   return SG_OK;
