@@ -82,7 +82,25 @@ class SyzSigError(RuntimeError):
         self.rc = rc
 
 
+def _preload_torch_hip_runtime():
+    """One HIP runtime per process: when PyTorch-ROCm is installed, bind
+    libsyzsig to the libamdhip64 that torch ships (torch loads it by the name
+    `libamdhip64.so`, we by the soname `libamdhip64.so.7`; loading ours first
+    would put two runtimes in the process).  Does not import torch."""
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+        if spec and spec.origin:
+            rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+            if os.path.exists(rt):
+                ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+    except OSError:
+        pass
+
+
 def _load():
+    _preload_torch_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C syzkaller_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")

@@ -27,6 +27,8 @@
 // runs.
 #include "sg_internal.h"
 
+#include <cstdlib>
+
 namespace sg {
 
 constexpr int kPT = 8192;                   // partition tile (values): LDS fits two tiles per CU
@@ -127,12 +129,13 @@ __global__ __launch_bounds__(kPThreads) void k_part_hist(PartArgs a) {
   for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[(uint64_t)d * a.ntiles + blockIdx.x] = cnt[d];
 }
 
-template <bool kPairs, int kShift, int kBits>
+template <bool kPairs, int kShift, int kBits, bool kDirect>
 __global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
   constexpr int R = 1 << kBits;
   constexpr int W = kPairs ? 1 : kRecWin;
-  __shared__ uint64_t stage[kPT];             // the tile, reordered by digit (64 KiB)
+  __shared__ uint64_t stage[kDirect ? 1 : kPT];  // the tile, reordered by digit (64 KiB)
   __shared__ uint16_t cur[kPWaves][R];        // per-wave digit cursors
+  __shared__ uint32_t cur32[kDirect ? kPWaves : 1][kDirect ? R : 1];
   __shared__ uint16_t dstart[R];              // tile-local start of each digit
   __shared__ uint32_t tot[R];
   __shared__ uint64_t gbase[R];               // global start of (digit, this tile)
@@ -196,7 +199,11 @@ __global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
     }
   }
   __syncthreads();
-  for (int d = lane; d < R; d += 64) cur[w][d] += dstart[d];
+  if (kDirect) {  // cursors become global positions of this wave's values
+    for (int d = lane; d < R; d += 64) cur32[w][d] = (uint32_t)cur[w][d];
+  } else {
+    for (int d = lane; d < R; d += 64) cur[w][d] += dstart[d];
+  }
   // record of this lane's first value; later values of the lane only move forward
   uint64_t r = 0;
   if (!kPairs) {
@@ -221,12 +228,19 @@ __global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
     const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pair >> 32));
     const uint64_t m = match_digit<kBits>(d, v);
     if (v) {
-      const uint32_t base = cur[w][d];
-      stage[base + __popcll(m & lt)] = pair;
-      if (!(m & lt)) cur[w][d] = (uint16_t)(base + __popcll(m));
+      if (kDirect) {
+        const uint32_t base = cur32[w][d];
+        a.out[gbase[d] + base + __popcll(m & lt)] = pair;
+        if (!(m & lt)) cur32[w][d] = base + __popcll(m);
+      } else {
+        const uint32_t base = cur[w][d];
+        stage[base + __popcll(m & lt)] = pair;
+        if (!(m & lt)) cur[w][d] = (uint16_t)(base + __popcll(m));
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (kDirect) return;
   __syncthreads();
   // write out in digit runs (consecutive threads -> consecutive addresses)
   const uint32_t ntile = (uint32_t)(a.n - t0 < (uint64_t)kPT ? a.n - t0 : (uint64_t)kPT);
@@ -399,6 +413,17 @@ __global__ __launch_bounds__(kPThreads) void k_bucket_triage_direct(BucketArgs a
   }
 }
 
+// Experiment switch: SG_PART_DIRECT=1 scatters straight from registers to HBM
+// (no LDS reorder; more blocks per CU, partial-line writes).
+static bool part_direct() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SG_PART_DIRECT");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 size_t bucket_ws_bytes(uint64_t n) {
   const uint64_t nt = (n + kPT - 1) / kPT;
   WsPlan p;
@@ -456,8 +481,12 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     ScopedTimer tm(ctx, "part1_scatter");
     pa.goff = (uint64_t*)ws_at(ctx, oO1);
     pa.out = A;
-    hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                       ctx->stream, pa);
+    if (part_direct())
+      hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits, true>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                         ctx->stream, pa);
+    else
+      hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits, false>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                         ctx->stream, pa);
   }
   {
     ScopedTimer tm(ctx, "part2_hist");
@@ -473,8 +502,12 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     ScopedTimer tm(ctx, "part2_scatter");
     pa.goff = (uint64_t*)ws_at(ctx, oO2);
     pa.out = B;
-    hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                       ctx->stream, pa);
+    if (part_direct())
+      hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits, true>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                         ctx->stream, pa);
+    else
+      hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits, false>), dim3((uint32_t)nt), dim3(kPThreads), 0,
+                         ctx->stream, pa);
   }
   BucketArgs ba{};
   ba.pairs = B;
