@@ -97,13 +97,16 @@ KERNELS = ["part1_hist", "part1_scatter", "part2_hist", "part2_scatter", "bucket
 
 
 def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords, nt):
-    """Algorithmic bytes per launch of each kernel."""
+    """Algorithmic bytes per launch of each kernel.  n_cand =
+    values not in maxSignal at batch start."""
+    g2 = nt + 512
+    mbits = 4 * (1 << 27)  # the maxSignal bitmap, read once slice by slice
     return {
-        "part1_hist": 4 * n_in + 256 * nt * 4,
-        "part1_scatter": 4 * n_in + 8 * n_in + 256 * nt * 8,
-        "part2_hist": 8 * n_in + 512 * nt * 4,
-        "part2_scatter": 8 * n_in + 8 * n_in + 512 * nt * 8,
-        "bucket_triage": 8 * n_in + 4 * (1 << 27) + 12 * n_newwords + n_rec,
+        "part1_hist": 4 * n_in + 512 * nt * 4,
+        "part1_scatter": 4 * n_in + 8 * n_in + 512 * nt * 8,
+        "part2_hist": 4 * n_in + 256 * g2 * 4,
+        "part2_scatter": 8 * n_in + 8 * n_in + 256 * g2 * 8,
+        "bucket_triage": 8 * n_in + mbits + 16 * n_newwords + n_rec,
         "triage_claim": 4 * n_in + 4 * n_in + 8 * n_cand + n_in / 8,
         "triage_resolve": n_in / 8 + 4 * n_cand + 4 * n_cand + 16 * n_diff + n_rec + n_in / 8 + n_in / 64,
     }
@@ -327,7 +330,7 @@ def main():
             L = args.steps
             n_in, n_cand, n_diff, n_rec, n_new = (acct[x] / L for x in ("n_in", "n_cand", "n_diff", "n_rec",
                                                                          "n_new_signal"))
-            nt = (n_in + 16383) // 16384
+            nt = (n_in + 8191) // 8192  # partition tiles (kPT)
             per = algo_bytes(n_in, n_cand, n_diff, n_rec, min(n_new, 1 << 27), nt)
             for kname, b in per.items():
                 if kname in kernels:

@@ -49,7 +49,7 @@ def row_c1(ctx, rng):
     from oracle import pyoracle as O
 
     corpus = (0x81000000 + 16 * np.sort(rng.choice(1 << 22, size=1_000_000, replace=False))).astype(np.uint32)
-    traces = [np.unique(zipf_vals(rng, 6000, s=0.9, nranks=1 << 22))[:4096] for _ in range(1000)]
+    traces = [np.unique(zipf_vals(rng, 6000, s=1.05, nranks=1 << 22))[:4096] for _ in range(1000)]
     a = np.concatenate(traces)
     a_len = np.array([t.size for t in traces], np.uint64)
     a_beg = np.concatenate([[0], np.cumsum(a_len)[:-1]]).astype(np.uint64)
@@ -57,7 +57,7 @@ def row_c1(ctx, rng):
     b_len = np.full(1000, corpus.size, np.uint64)
     res = {}
     for op, name in [(2, "Union"), (0, "Difference")]:
-        C.merge_batch(op, a, a_beg, a_len, corpus, b_beg[:1], b_len[:1], ctx=ctx)  # warm
+        C.merge_batch(op, a, a_beg[:1], a_len[:1], corpus, b_beg[:1], b_len[:1], ctx=ctx)  # warm
         ctx.timing(True)
         t0 = time.perf_counter()
         out = C.merge_batch(op, a, a_beg, a_len, corpus, b_beg, b_len, ctx=ctx)

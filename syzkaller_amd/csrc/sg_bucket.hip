@@ -9,25 +9,29 @@
 // Same first-owner rule as sg_triage.hip (a record is new iff it is the
 // first, in sequential order, to contain some signal s not in maxSignal),
 // organised so that no access is random across HBM:
-//   1. stable LSD partition of (s, record) pairs by bits 15..22 of s,
-//   2. stable LSD partition by bits 23..31 -> pairs grouped by the 17-bit
-//      bucket s >> 15 (32768 signals, a 4 KiB slice of the bitmap),
-//   3. one workgroup per bucket: the bucket's maxSignal slice, its new bits,
-//      and a small LDS hash map signal -> min(record) over the candidates
-//      (signals not in maxSignal) decide which records are new; the slice's
-//      new bits go back to maxSignal / newSignal from the bucket's only
-//      writer.  Buckets with more candidates than the LDS lists hold are
-//      redone by a second kernel with a direct 32768-entry LDS table.
+//   1. stable MSD partition of the batch by the coarse digit s >> 23: 512
+//      slices of 2^23 signals, each backed by 1 MiB of the maxSignal bitmap;
+//      out: (s, record) in two u32 arrays,
+//   2. per coarse slice, a stable partition by the fine digit (s >> 15) & 255
+//      that DROPS every s already in maxSignal.  The workgroups of one XCD
+//      walk consecutive tiles, so the slice they probe is the same 1 MiB and
+//      stays in that XCD's L2; only the candidates (signals not in
+//      maxSignal, ~12 % of a C2 batch, far fewer in a warm fuzzer) go on,
+//      as (s << 32 | record) pairs grouped by the 17-bit bucket s >> 15,
+//   3. one workgroup per bucket (32768 signals): an LDS hash map
+//      signal -> min(record) over its candidates decides the new records
+//      and the bucket's new bits go back to maxSignal / newSignal from its
+//      only writer.  Buckets with more distinct candidates than the map
+//      holds are redone by a second kernel with a direct 32768-entry table.
 // No global atomics, no 16 GiB owner table, every HBM stream coalesced.
 //
-// Partition pass = histogram kernel (per 8192-value tile, LDS counters) +
+// A partition pass = histogram kernel (per 8192-value tile, LDS counters) +
 // device exclusive scan over [digit][tile] + scatter kernel: each wave holds
 // its 1024 values in registers, ranks them in order with a ballot multisplit
 // (stable), the tile is reordered by digit in LDS and written out in digit
-// runs.
+// runs.  Both scatters map blocks to tiles XCD-contiguously (T1 swizzle), so
+// the partial lines at digit-run seams of neighbouring tiles merge in one L2.
 #include "sg_internal.h"
-
-#include <cstdlib>
 
 namespace sg {
 
@@ -40,255 +44,334 @@ constexpr int kBucketBits = 15;             // 32768 signals per bucket
 constexpr uint32_t kBucketSig = 1u << kBucketBits;
 constexpr uint32_t kBucketWords = kBucketSig / 32;  // 1024
 constexpr uint32_t kNumBuckets = 1u << (32 - kBucketBits);  // 131072
-constexpr int kD0Shift = 15, kD0Bits = 8;   // pass 1 digit: bits 15..22
-constexpr int kD1Shift = 23, kD1Bits = 9;   // pass 2 digit: bits 23..31
-constexpr int kRecWin = 512;                // record offsets kept in LDS per tile
+constexpr int kCShift = 23, kCBits = 9;     // pass 1 (coarse) digit: bits 23..31
+constexpr int kFShift = 15, kFBits = 8;     // pass 2 (fine) digit: bits 15..22
+constexpr uint32_t kNumCoarse = 1u << kCBits;
+constexpr int kRecWin = 1024;               // record offsets kept in LDS per tile (tile-relative u16)
 constexpr int kBTThreads = 512;             // bucket kernel
-constexpr int kHashBits = 11;
-constexpr int kHash = 1 << kHashBits;       // candidate hash slots per bucket
-constexpr int kCandCap = 2048;              // candidates kept per bucket
+constexpr int kBU = 16;                     // pairs per thread in flight (8192 per block)
+constexpr int kHash = 4096;                 // max candidate hash slots per bucket
 
-struct PartArgs {
-  const uint32_t* vals;    // pass 1 input
-  const uint64_t* pairs;   // pass 2 input: (s << 32) | record
-  uint64_t n;
-  uint64_t ntiles;
-  const uint64_t* rec_off; // pass 1: record offsets (nrec+1)
-  uint64_t nrec;
-  const uint32_t* tile_rec;// pass 1: record of each tile's first value (ntiles+1)
-  uint32_t* hist;          // [digit][tile]
-  const uint64_t* goff;    // scanned hist: output start of (digit, tile)
-  uint64_t* out;           // pairs out
-};
+// blocks sharing an XCD (bid % 8 under round-robin dispatch) get a contiguous
+// run of tiles; a bijection on [0, g) for any g (speed only, never correctness)
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t g) {
+  const uint32_t x = bid & 7, q = g >> 3, r = g & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
 
 template <int kShift, int kBits>
 __device__ __forceinline__ uint32_t digit_of(uint32_t s) {
   return (s >> kShift) & ((1u << kBits) - 1);
 }
 
-// lanes of this wave holding the same digit as this lane (valid lanes only)
+// Counting sort of one tile held in registers (kSteps values per lane) by
+// digit, through LDS: counts, one-wave exclusive scan, then every value takes
+// a slot with an LDS atomic.  The order within a digit is NOT the input order
+// -- nothing downstream needs it: first owners are minima over records.
+// On return cnt[] is free, dstart[d] is the digit's first slot in the tile
+// and pos[k] the slot of value k (valid lanes only).
 template <int kBits>
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
-  uint64_t m = __ballot(valid);
+__device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t vmask, uint32_t* cnt,
+                                          uint16_t* dstart, uint32_t (&pos)[kSteps]) {
+  constexpr int R = 1 << kBits;
+  const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
-  for (int b = 0; b < kBits; b++) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = __ballot(valid && bit);
-    m &= bit ? bb : ~bb;
+  for (int k = 0; k < kSteps; k++)
+    if ((vmask >> k) & 1u) atomicAdd(&cnt[dv[k]], 1u);
+  __syncthreads();
+  if (tid < 64) {  // one wave scans the R digit counts; cnt becomes the cursor
+    uint32_t carry = 0;
+    for (int base = 0; base < R; base += 64) {
+      const uint32_t x = cnt[base + lane];
+      uint32_t incl = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t ex = carry + incl - x;
+      dstart[base + lane] = (uint16_t)ex;
+      cnt[base + lane] = ex;
+      carry += __shfl(incl, 63);
+    }
   }
-  return valid ? m : 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSteps; k++)
+    if ((vmask >> k) & 1u) pos[k] = atomicAdd(&cnt[dv[k]], 1u);
 }
 
-template <bool kPairs, int kShift, int kBits>
-__global__ __launch_bounds__(kPThreads) void k_part_hist(PartArgs a) {
-  constexpr int R = 1 << kBits;
+// ---------------------------------------------------------------- pass 1 ---
+
+struct P1Args {
+  const uint32_t* vals;
+  uint64_t n;
+  uint64_t ntiles;
+  const uint64_t* rec_off;  // nrec + 1
+  const uint32_t* tile_rec; // record of each tile's first value (ntiles + 1)
+  uint32_t* hist;           // [coarse digit][tile]
+  const uint64_t* goff;     // scanned hist
+  uint32_t* s_out;          // partitioned signals
+  uint32_t* r_out;          // their records
+};
+
+__global__ __launch_bounds__(kPThreads) void k_p1_hist(P1Args a) {
+  constexpr int R = 1 << kCBits;
   __shared__ uint32_t cnt[R];
   for (int i = threadIdx.x; i < R; i += kPThreads) cnt[i] = 0;
   __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kPT;
-  if (kPairs) {  // 16-B loads: 2 pairs per lane per load, 8 loads per lane
-    const bool full = t0 + kPT <= a.n && (((uintptr_t)a.pairs & 15) == 0);
-    if (full) {
-      const uint4* p4 = reinterpret_cast<const uint4*>(a.pairs + t0);
-      uint4 q[kPT / 2 / kPThreads];
+  if (t0 + kPT <= a.n && (((uintptr_t)a.vals & 15) == 0)) {  // 16-B loads, 4 per lane
+    const uint4* v4 = reinterpret_cast<const uint4*>(a.vals + t0);
+    uint4 q[kPT / 4 / kPThreads];
 #pragma unroll
-      for (int j = 0; j < kPT / 2 / kPThreads; j++) q[j] = p4[j * kPThreads + threadIdx.x];
+    for (int j = 0; j < kPT / 4 / kPThreads; j++) q[j] = v4[j * kPThreads + threadIdx.x];
 #pragma unroll
-      for (int j = 0; j < kPT / 2 / kPThreads; j++) {
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].y)], 1u);
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].w)], 1u);
-      }
-    } else {
-      for (int i = threadIdx.x; i < kPT; i += kPThreads) {
-        const uint64_t e = t0 + i;
-        if (e < a.n) atomicAdd(&cnt[digit_of<kShift, kBits>((uint32_t)(a.pairs[e] >> 32))], 1u);
-      }
+    for (int j = 0; j < kPT / 4 / kPThreads; j++) {
+      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].x)], 1u);
+      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].y)], 1u);
+      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].z)], 1u);
+      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].w)], 1u);
     }
-  } else {  // 16-B loads: 4 values per lane per load, 4 loads per lane
-    const bool full = t0 + kPT <= a.n && (((uintptr_t)a.vals & 15) == 0);
-    if (full) {
-      const uint4* v4 = reinterpret_cast<const uint4*>(a.vals + t0);
-      uint4 q[kPT / 4 / kPThreads];
-#pragma unroll
-      for (int j = 0; j < kPT / 4 / kPThreads; j++) q[j] = v4[j * kPThreads + threadIdx.x];
-#pragma unroll
-      for (int j = 0; j < kPT / 4 / kPThreads; j++) {
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].x)], 1u);
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].y)], 1u);
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].z)], 1u);
-        atomicAdd(&cnt[digit_of<kShift, kBits>(q[j].w)], 1u);
-      }
-    } else {
-      for (int i = threadIdx.x; i < kPT; i += kPThreads) {
-        const uint64_t e = t0 + i;
-        if (e < a.n) atomicAdd(&cnt[digit_of<kShift, kBits>(a.vals[e])], 1u);
-      }
+  } else {
+    for (int i = threadIdx.x; i < kPT; i += kPThreads) {
+      const uint64_t e = t0 + i;
+      if (e < a.n) atomicAdd(&cnt[digit_of<kCShift, kCBits>(a.vals[e])], 1u);
     }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[(uint64_t)d * a.ntiles + blockIdx.x] = cnt[d];
 }
 
-template <bool kPairs, int kShift, int kBits, bool kDirect>
-__global__ __launch_bounds__(kPThreads) void k_part_scatter(PartArgs a) {
-  constexpr int R = 1 << kBits;
-  constexpr int W = kPairs ? 1 : kRecWin;
-  __shared__ uint64_t stage[kDirect ? 1 : kPT];  // the tile, reordered by digit (64 KiB)
-  __shared__ uint16_t cur[kPWaves][R];        // per-wave digit cursors
-  __shared__ uint32_t cur32[kDirect ? kPWaves : 1][kDirect ? R : 1];
-  __shared__ uint16_t dstart[R];              // tile-local start of each digit
-  __shared__ uint32_t tot[R];
-  __shared__ uint64_t gbase[R];               // global start of (digit, this tile)
-  __shared__ uint64_t win[W];                 // pass 1: record offsets of the tile
+__global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
+  constexpr int R = 1 << kCBits;
+  __shared__ uint64_t stage[kPT];        // the tile grouped by digit: (s << 32) | record (64 KiB)
+  __shared__ uint32_t cnt[R];
+  __shared__ uint16_t dstart[R];         // tile-local start of each digit
+  __shared__ uint64_t gbase[R];          // global start of (digit, this tile)
+  __shared__ uint16_t win[kRecWin];      // record offsets of the tile, clamped to [t0, t0 + kPT] - t0
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint64_t tile = blockIdx.x, t0 = tile * kPT;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x), t0 = tile * kPT;
   const uint64_t ebase = t0 + (uint64_t)w * kPerWave;
   // this wave's 1024 values in registers, every load in flight at once
-  uint64_t pv[kSteps];
+  uint32_t sv[kSteps];
+  uint32_t vmask = 0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint64_t e = ebase + (uint64_t)k * 64 + lane;
-    if (kPairs)
-      pv[k] = e < a.n ? a.pairs[e] : 0ull;
-    else
-      pv[k] = e < a.n ? ((uint64_t)a.vals[e] << 32) : 0ull;
+    sv[k] = e < a.n ? a.vals[e] : 0u;
+    vmask |= (e < a.n ? 1u : 0u) << k;
   }
-  uint64_t ra = 0, rb = 0, wn = 0;
-  if (!kPairs) {
-    ra = a.tile_rec[tile];
-    rb = a.tile_rec[tile + 1];
-    wn = rb - ra + 1;
-    if (wn <= (uint64_t)W)
-      for (uint64_t i = tid; i < wn; i += kPThreads) win[i] = a.rec_off[ra + i];
-  }
-  for (int d = lane; d < R; d += 64) cur[w][d] = 0;
-  for (int d = tid; d < R; d += kPThreads) gbase[d] = a.goff[(uint64_t)d * a.ntiles + tile];
-  // walk 1: per-wave digit counts (not unrolled: unrolling piles up 16 steps of ballots and spills)
-#pragma unroll 1
-  for (int k = 0; k < kSteps; k++) {
-    const bool v = ebase + (uint64_t)k * 64 + lane < a.n;
-    const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pv[k] >> 32));
-    const uint64_t m = match_digit<kBits>(d, v);
-    if (v && !(m & lt)) cur[w][d] += (uint16_t)__popcll(m);
-    __builtin_amdgcn_sched_barrier(0);  // keep the steps' ballots from piling up in SGPRs
-  }
-  __syncthreads();
-  // exclusive prefix over waves per digit, then over digits
+  const uint64_t ra = a.tile_rec[tile], rb = a.tile_rec[tile + 1], wn = rb - ra + 1;
+  const bool inwin = wn <= (uint64_t)kRecWin;
+  if (inwin)
+    for (uint64_t i = tid; i < wn; i += kPThreads) {
+      const uint64_t o = a.rec_off[ra + i];
+      win[i] = (uint16_t)(o <= t0 ? 0 : (o - t0 >= (uint64_t)kPT ? kPT : o - t0));
+    }
   for (int d = tid; d < R; d += kPThreads) {
-    uint32_t acc = 0;
-    for (int q = 0; q < kPWaves; q++) {
-      const uint32_t c = cur[q][d];
-      cur[q][d] = (uint16_t)acc;
-      acc += c;
-    }
-    tot[d] = acc;
+    gbase[d] = a.goff[(uint64_t)d * a.ntiles + tile];
+    cnt[d] = 0;
   }
   __syncthreads();
-  if (tid < 64) {  // one wave scans the R digit totals
-    uint32_t carry = 0;
-    for (int base = 0; base < R; base += 64) {
-      uint32_t x = tot[base + lane];
-      uint32_t incl = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      dstart[base + lane] = (uint16_t)(carry + incl - x);
-      carry += __shfl(incl, 63);
-    }
-  }
-  __syncthreads();
-  if (kDirect) {  // cursors become global positions of this wave's values
-    for (int d = lane; d < R; d += 64) cur32[w][d] = (uint32_t)cur[w][d];
-  } else {
-    for (int d = lane; d < R; d += 64) cur[w][d] += dstart[d];
-  }
-  // record of this lane's first value; later values of the lane only move forward
-  uint64_t r = 0;
-  if (!kPairs) {
+  // records: a lane's values are in order, so its record only moves forward
+  uint32_t rv[kSteps];
+  {
+    uint64_t r = 0;
     const uint64_t e0 = ebase + lane;
-    if (e0 < a.n)
-      r = wn <= (uint64_t)W ? ra + sgd::seg_search(win, 0, wn - 1, e0) : sgd::seg_search(a.rec_off, ra, rb, e0);
-  }
-  // walk 2: stable rank -> LDS position
-#pragma unroll 1
-  for (int k = 0; k < kSteps; k++) {
-    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
-    const bool v = e < a.n;
-    uint64_t pair = pv[k];
-    if (!kPairs && v) {
-      if (wn <= (uint64_t)W) {
-        while (r < rb && win[r + 1 - ra] <= e) r++;
-      } else {
-        r = sgd::seg_search(a.rec_off, r, rb, e);
+    if (e0 < a.n) r = inwin ? ra + sgd::seg_search(win, 0, wn - 1, e0 - t0) : sgd::seg_search(a.rec_off, ra, rb, e0);
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint64_t e = ebase + (uint64_t)k * 64 + lane;
+      if ((vmask >> k) & 1u) {
+        if (inwin) {
+          const uint32_t el = (uint32_t)(e - t0);
+          while (r < rb && win[r + 1 - ra] <= el) r++;
+        } else {
+          r = sgd::seg_search(a.rec_off, r, rb, e);
+        }
       }
-      pair |= (uint32_t)r;
+      rv[k] = (uint32_t)r;
     }
-    const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pair >> 32));
-    const uint64_t m = match_digit<kBits>(d, v);
-    if (v) {
-      if (kDirect) {
-        const uint32_t base = cur32[w][d];
-        a.out[gbase[d] + base + __popcll(m & lt)] = pair;
-        if (!(m & lt)) cur32[w][d] = base + __popcll(m);
-      } else {
-        const uint32_t base = cur[w][d];
-        stage[base + __popcll(m & lt)] = pair;
-        if (!(m & lt)) cur[w][d] = (uint16_t)(base + __popcll(m));
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
   }
-  if (kDirect) return;
+  uint32_t dv[kSteps], pos[kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) dv[k] = digit_of<kCShift, kCBits>(sv[k]);
+  tile_rank<kCBits>(dv, vmask, cnt, dstart, pos);
+#pragma unroll
+  for (int k = 0; k < kSteps; k++)
+    if ((vmask >> k) & 1u) stage[pos[k]] = ((uint64_t)sv[k] << 32) | rv[k];
   __syncthreads();
   // write out in digit runs (consecutive threads -> consecutive addresses)
   const uint32_t ntile = (uint32_t)(a.n - t0 < (uint64_t)kPT ? a.n - t0 : (uint64_t)kPT);
   for (uint32_t p = tid; p < ntile; p += kPThreads) {
     const uint64_t pair = stage[p];
-    const uint32_t d = digit_of<kShift, kBits>((uint32_t)(pair >> 32));
+    const uint32_t d = digit_of<kCShift, kCBits>((uint32_t)(pair >> 32));
+    const uint64_t o = gbase[d] + (p - dstart[d]);
+    a.s_out[o] = (uint32_t)(pair >> 32);
+    a.r_out[o] = (uint32_t)pair;
+  }
+}
+
+// Tiles of pass 2: coarse slice c covers [cs[c], cs[c+1]) of the pass-1
+// output and owns tiles [tb[c], tb[c+1]); tb[512] = number of tiles.
+__global__ __launch_bounds__(kNumCoarse) void k_p2_tiles(const uint64_t* __restrict__ goff1, uint64_t nt, uint64_t n,
+                                                         uint64_t* __restrict__ cs, uint32_t* __restrict__ tb) {
+  __shared__ uint32_t k[kNumCoarse];
+  const uint32_t c = threadIdx.x;
+  const uint64_t lo = goff1[(uint64_t)c * nt];
+  const uint64_t hi = c + 1 < kNumCoarse ? goff1[(uint64_t)(c + 1) * nt] : n;
+  cs[c] = lo;
+  if (c == 0) cs[kNumCoarse] = n;
+  k[c] = (uint32_t)((hi - lo + kPT - 1) / kPT);
+  __syncthreads();
+  if (c < 64) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < kNumCoarse; base += 64) {
+      const uint32_t x = k[base + c];
+      uint32_t incl = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)c >= o) incl += y;
+      }
+      tb[base + c] = carry + incl - x;
+      carry += __shfl(incl, 63);
+    }
+    if (c == 0) tb[kNumCoarse] = carry;
+  }
+}
+
+struct P2Args {
+  const uint32_t* s_in;
+  const uint32_t* r_in;
+  const uint64_t* cs;       // coarse slice starts (513)
+  const uint32_t* tb;       // coarse slice first tiles (513)
+  uint32_t* hist;           // [c][fine digit][tile of c], base 256 * tb[c]
+  const uint64_t* goff;     // scanned hist
+  uint64_t* out;            // pairs (s << 32) | record grouped by s >> 15
+};
+
+struct P2Tile {
+  uint32_t c, j, kc;
+  uint64_t e0, e1;
+  bool live;
+};
+
+__device__ __forceinline__ P2Tile p2_tile(const P2Args& a) {
+  P2Tile t;
+  const uint32_t t2 = xcd_tile(blockIdx.x, gridDim.x);
+  const uint32_t nt2 = a.tb[kNumCoarse];
+  t.live = t2 < nt2;
+  if (!t.live) {
+    t.c = t.kc = 0;
+    t.j = t2;
+    t.e0 = t.e1 = 0;
+    return t;
+  }
+  t.c = (uint32_t)sgd::seg_search(a.tb, 0, kNumCoarse - 1, t2);  // largest c with tb[c] <= t2
+  t.j = t2 - a.tb[t.c];
+  t.kc = a.tb[t.c + 1] - a.tb[t.c];
+  t.e0 = a.cs[t.c] + (uint64_t)t.j * kPT;
+  const uint64_t end = a.cs[t.c + 1];
+  t.e1 = t.e0 + kPT < end ? t.e0 + kPT : end;
+  return t;
+}
+
+__device__ __forceinline__ uint64_t p2_hist_index(const P2Args& a, const P2Tile& t, uint32_t d) {
+  return ((uint64_t)a.tb[t.c] << kFBits) + (uint64_t)d * t.kc + t.j;
+}
+
+__global__ __launch_bounds__(kPThreads) void k_p2_hist(P2Args a) {
+  constexpr int R = 1 << kFBits;
+  __shared__ uint32_t cnt[R];
+  const P2Tile t = p2_tile(a);
+  if (!t.live) {  // tail of the upper-bound grid: zero its own slots
+    for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[((uint64_t)t.j << kFBits) + d] = 0;
+    return;
+  }
+  for (int i = threadIdx.x; i < R; i += kPThreads) cnt[i] = 0;
+  uint32_t sv[kPT / kPThreads];
+#pragma unroll
+  for (int k = 0; k < kPT / kPThreads; k++) {
+    const uint64_t e = t.e0 + (uint64_t)k * kPThreads + threadIdx.x;
+    sv[k] = e < t.e1 ? a.s_in[e] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPT / kPThreads; k++)
+    if (t.e0 + (uint64_t)k * kPThreads + threadIdx.x < t.e1) atomicAdd(&cnt[digit_of<kFShift, kFBits>(sv[k])], 1u);
+  __syncthreads();
+  for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[p2_hist_index(a, t, d)] = cnt[d];
+}
+
+__global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
+  constexpr int R = 1 << kFBits;
+  __shared__ uint64_t stage[kPT];
+  __shared__ uint32_t cnt[R];
+  __shared__ uint16_t dstart[R];
+  __shared__ uint64_t gbase[R];
+  const P2Tile t = p2_tile(a);
+  if (!t.live) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint64_t ebase = t.e0 + (uint64_t)w * kPerWave;
+  uint32_t sv[kSteps], rv[kSteps];
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
+    const bool v = e < t.e1;
+    sv[k] = v ? a.s_in[e] : 0u;
+    rv[k] = v ? a.r_in[e] : 0u;
+    vmask |= (v ? 1u : 0u) << k;
+  }
+  for (int d = tid; d < R; d += kPThreads) {
+    gbase[d] = a.goff[p2_hist_index(a, t, d)];
+    cnt[d] = 0;
+  }
+  __syncthreads();
+  uint32_t dv[kSteps], pos[kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) dv[k] = digit_of<kFShift, kFBits>(sv[k]);
+  tile_rank<kFBits>(dv, vmask, cnt, dstart, pos);
+#pragma unroll
+  for (int k = 0; k < kSteps; k++)
+    if ((vmask >> k) & 1u) stage[pos[k]] = ((uint64_t)sv[k] << 32) | rv[k];
+  __syncthreads();
+  const uint32_t ntile = (uint32_t)(t.e1 - t.e0);
+  for (uint32_t p = tid; p < ntile; p += kPThreads) {
+    const uint64_t pair = stage[p];
+    const uint32_t d = digit_of<kFShift, kFBits>((uint32_t)(pair >> 32));
     a.out[gbase[d] + (p - dstart[d])] = pair;
   }
 }
 
-__global__ void k_tile_rec_pt(const uint64_t* __restrict__ off, uint64_t nseg, uint64_t n, uint64_t ntiles,
-                              uint32_t* __restrict__ tile_rec) {
-  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > ntiles) return;
-  uint64_t e = t * kPT;
-  if (e >= n) e = n - 1;
-  tile_rec[t] = (uint32_t)sgd::seg_search(off, 0, nseg - 1, e);
-}
-
-// first pair index of every bucket (pairs grouped by s >> 15, ascending)
-__global__ void k_bucket_bounds(const uint64_t* __restrict__ pairs, uint64_t n, uint64_t* __restrict__ bounds) {
-  uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// First pair of every bucket b = (c << 8) | d, read off the pass-2 scan:
+// (c, d)'s first tile slot; empty slices point at the next slice's start.
+__global__ void k_bucket_bounds(const uint64_t* __restrict__ goff2, const uint32_t* __restrict__ tb,
+                                uint64_t nslots, uint64_t* __restrict__ bounds) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b > kNumBuckets) return;
-  const uint64_t key = b << kBucketBits;  // first signal of bucket b (2^32 for b == kNumBuckets)
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if ((pairs[mid] >> 32) < key)
-      lo = mid + 1;
-    else
-      hi = mid;
+  if (b == kNumBuckets) {
+    bounds[b] = goff2[nslots];
+    return;
   }
-  bounds[b] = lo;
+  const uint32_t c = (uint32_t)(b >> kFBits), d = (uint32_t)(b & ((1u << kFBits) - 1));
+  bounds[b] = goff2[((uint64_t)tb[c] << kFBits) + (uint64_t)d * (tb[c + 1] - tb[c])];
 }
 
 struct BucketArgs {
-  const uint64_t* pairs;
+  const uint64_t* pairs;  // (s << 32) | record, grouped by bucket s >> 15
   const uint64_t* bounds;
-  uint32_t* mwords;     // maxSignal
-  uint32_t* nwords;     // newSignal (nullable)
+  uint32_t* mwords;       // maxSignal
+  uint32_t* nwords;       // newSignal (nullable)
   uint8_t* rec_new;
-  uint32_t* spill;      // buckets left for the direct-table kernel
+  uint32_t* spill;        // buckets left for the direct-table kernel
   uint32_t* nspill;
 };
 
-__device__ __forceinline__ uint32_t slot_of(uint32_t sl) { return (sl * 2654435761u) >> (32 - kHashBits); }
+__device__ __forceinline__ uint32_t slot_of(uint32_t sl, int hbits) { return (sl * 2654435761u) >> (32 - hbits); }
 
-// Write the bucket's new bits: maxSignal = slice | new, newSignal |= new.
+// The bucket's new bits: maxSignal = slice | new, newSignal |= new (this
+// block is the only writer of the bucket's 1024 words).
 __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
                                                const uint32_t* nbits, int tid, int nthreads) {
   uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
@@ -302,82 +385,95 @@ __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, 
   }
 }
 
+__device__ __forceinline__ bool hash_insert(uint32_t* hkey, uint32_t* hval, uint32_t hsize, int hbits,
+                                            uint32_t* nbits, uint32_t sl, uint32_t rec) {
+  uint32_t h = slot_of(sl, hbits);
+  for (uint32_t probes = 0; probes < hsize; probes++) {
+    const uint32_t k = atomicCAS(&hkey[h], ~0u, sl);
+    if (k == ~0u) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+    if (k == ~0u || k == sl) {
+      atomicMin(&hval[h], rec);
+      return true;
+    }
+    h = (h + 1) & (hsize - 1);
+  }
+  return false;  // map full
+}
+
 __global__ __launch_bounds__(kBTThreads) void k_bucket_triage(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  __shared__ uint32_t hkey[kHash];
-  __shared__ uint32_t hval[kHash];
-  __shared__ uint64_t cand[kCandCap];   // (signal & 32767) << 32 | record
-  __shared__ uint32_t ncand, overflow;
+  __shared__ __attribute__((aligned(16))) uint32_t hkey[kHash];
+  __shared__ __attribute__((aligned(16))) uint32_t hval[kHash];
+  __shared__ uint32_t ncand;
   const uint32_t b = blockIdx.x;
   const uint64_t lo = a.bounds[b], hi = a.bounds[b + 1];
   if (lo == hi) return;  // no signal of this batch falls in the bucket
   const int tid = threadIdx.x;
+  constexpr uint64_t kChunkPairs = (uint64_t)kBTThreads * kBU;
+  // the first chunk of pairs (all of a typical bucket) in flight at once
+  uint64_t p[kBU];
+#pragma unroll
+  for (int u = 0; u < kBU; u++) {
+    const uint64_t i = lo + (uint64_t)u * kBTThreads + tid;
+    p[u] = i < hi ? a.pairs[i] : ~0ull;
+  }
   const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
   for (uint32_t i = tid; i < kBucketWords; i += kBTThreads) {
     mslice[i] = mg[i];
     nbits[i] = 0;
   }
-  for (uint32_t i = tid; i < kHash; i += kBTThreads) {
+  if (tid == 0) ncand = 0;
+  __syncthreads();
+  // candidates = signals not in maxSignal (fuzzer.go:666)
+  uint32_t cm = 0;
+#pragma unroll
+  for (int u = 0; u < kBU; u++) {
+    const uint32_t sl = (uint32_t)(p[u] >> 32) & (kBucketSig - 1);
+    if (p[u] != ~0ull && !((mslice[sl >> 5] >> (sl & 31)) & 1u)) cm |= 1u << u;
+  }
+  if (cm) atomicAdd(&ncand, (uint32_t)__popc(cm));
+  __syncthreads();
+  // map size: >= 2x the candidates (all could be distinct), capped
+  const uint64_t nc = hi - lo > kChunkPairs ? ~0ull : ncand;
+  int hbits = 6;
+  while ((1 << hbits) < kHash && (1ull << hbits) < 2 * nc) hbits++;
+  const uint32_t hsize = 1u << hbits;
+  for (uint32_t i = tid; i < hsize; i += kBTThreads) {
     hkey[i] = ~0u;
     hval[i] = ~0u;
   }
-  if (tid == 0) {
-    ncand = 0;
-    overflow = 0;
-  }
   __syncthreads();
-  // candidates: signals not in maxSignal; owner = min record per signal
-  constexpr int kU = 8;
-  for (uint64_t base = lo; base < hi; base += (uint64_t)kBTThreads * kU) {
-    uint64_t p[kU];
+  // owner = min record per candidate signal
+  bool ok = true;
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
+  for (int u = 0; u < kBU; u++)
+    if ((cm >> u) & 1u) ok &= hash_insert(hkey, hval, hsize, hbits, nbits, (uint32_t)(p[u] >> 32) & (kBucketSig - 1),
+                                          (uint32_t)p[u]);
+  for (uint64_t base = lo + kChunkPairs; base < hi; base += kChunkPairs) {  // big buckets
+#pragma unroll
+    for (int u = 0; u < kBU; u++) {
       const uint64_t i = base + (uint64_t)u * kBTThreads + tid;
       p[u] = i < hi ? a.pairs[i] : ~0ull;
     }
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-      if (p[u] == ~0ull) continue;
+    for (int u = 0; u < kBU; u++) {
       const uint32_t sl = (uint32_t)(p[u] >> 32) & (kBucketSig - 1);
-      const uint32_t rec = (uint32_t)p[u];
-      if ((mslice[sl >> 5] >> (sl & 31)) & 1u) continue;
-      atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
-      const uint32_t c = atomicAdd(&ncand, 1u);
-      if (c < (uint32_t)kCandCap) cand[c] = ((uint64_t)sl << 32) | rec;
-      uint32_t h = slot_of(sl);
-      int probes = 0;
-      for (;;) {
-        const uint32_t k = atomicCAS(&hkey[h], ~0u, sl);
-        if (k == ~0u || k == sl) {
-          atomicMin(&hval[h], rec);
-          break;
-        }
-        h = (h + 1) & (kHash - 1);
-        if (++probes == kHash) {
-          overflow = 1;
-          break;
-        }
-      }
+      if (p[u] != ~0ull && !((mslice[sl >> 5] >> (sl & 31)) & 1u))
+        ok &= hash_insert(hkey, hval, hsize, hbits, nbits, sl, (uint32_t)p[u]);
     }
   }
-  __syncthreads();
-  if (overflow || ncand > (uint32_t)kCandCap) {  // redo with the direct table (no global writes yet)
+  if (__syncthreads_or(!ok)) {  // redo with the direct table (no global writes yet)
     if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
     return;
   }
-  // a record is queued iff it owns some signal (fuzzer.go:666, :678-690)
-  for (uint32_t i = tid; i < ncand; i += kBTThreads) {
-    const uint64_t c = cand[i];
-    const uint32_t sl = (uint32_t)(c >> 32), rec = (uint32_t)c;
-    uint32_t h = slot_of(sl);
-    while (hkey[h] != sl) h = (h + 1) & (kHash - 1);
-    if (hval[h] == rec) a.rec_new[rec] = 1;
-  }
+  // a record is queued iff it owns some signal (fuzzer.go:678-690)
+  for (uint32_t i = tid; i < hsize; i += kBTThreads)
+    if (hkey[i] != ~0u) a.rec_new[hval[i]] = 1;
   flush_new_bits(a, b, mslice, nbits, tid, kBTThreads);
 }
 
-// Buckets with too many candidates: direct first-owner table in LDS.
+// Buckets with too many distinct candidates: direct first-owner table in LDS.
 __global__ __launch_bounds__(kPThreads) void k_bucket_triage_direct(BucketArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t owner[kBucketSig];  // 128 KiB
   __shared__ uint32_t mslice[kBucketWords];
@@ -403,41 +499,51 @@ __global__ __launch_bounds__(kPThreads) void k_bucket_triage_direct(BucketArgs a
       atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
     }
     __syncthreads();
-    for (uint64_t i = lo + tid; i < hi; i += kPThreads) {
-      const uint64_t p = a.pairs[i];
-      const uint32_t sl = (uint32_t)(p >> 32) & (kBucketSig - 1);
-      if (owner[sl] == (uint32_t)p) a.rec_new[(uint32_t)p] = 1;  // owner set => candidate
-    }
+    for (uint32_t i = tid; i < kBucketSig; i += kPThreads)
+      if (owner[i] != ~0u) a.rec_new[owner[i]] = 1;
     flush_new_bits(a, b, mslice, nbits, tid, kPThreads);
     __syncthreads();
   }
 }
 
-// Experiment switch: SG_PART_DIRECT=1 scatters straight from registers to HBM
-// (no LDS reorder; more blocks per CU, partial-line writes).
-static bool part_direct() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SG_PART_DIRECT");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
+__global__ void k_tile_rec_pt(const uint64_t* __restrict__ off, uint64_t nseg, uint64_t n, uint64_t ntiles,
+                              uint32_t* __restrict__ tile_rec) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  uint64_t e = t * kPT;
+  if (e >= n) e = n - 1;
+  tile_rec[t] = (uint32_t)sgd::seg_search(off, 0, nseg - 1, e);
 }
 
-size_t bucket_ws_bytes(uint64_t n) {
-  const uint64_t nt = (n + kPT - 1) / kPT;
+struct BucketPlan {
+  uint64_t nt, g2, nslots;
   WsPlan p;
-  p.add(n * 8);
-  p.add(n * 8);
-  p.add((uint64_t)(1 << kD0Bits) * nt * 4);
-  p.add(((uint64_t)(1 << kD0Bits) * nt + 1) * 8);
-  p.add((uint64_t)(1 << kD1Bits) * nt * 4);
-  p.add(((uint64_t)(1 << kD1Bits) * nt + 1) * 8);
-  p.add((nt + 1) * 4);
-  p.add(((uint64_t)kNumBuckets + 1) * 8);
-  p.add(((uint64_t)kNumBuckets + 1) * 4);
-  return p.total + scan_ws_bytes((uint64_t)(1 << kD1Bits) * nt);
-}
+  size_t oS, oR, oB, oH1, oO1, oTR, oCS, oTB, oH2, oO2, oBB, oSP, scan_off;
+  explicit BucketPlan(uint64_t n) {
+    nt = (n + kPT - 1) / kPT;
+    g2 = nt + kNumCoarse;  // upper bound on pass-2 tiles
+    nslots = g2 << kFBits;
+    oS = p.add(n * 4);
+    oR = p.add(n * 4);
+    oB = p.add(n * 8);
+    oH1 = p.add((uint64_t)kNumCoarse * nt * 4);
+    oO1 = p.add(((uint64_t)kNumCoarse * nt + 1) * 8);
+    oTR = p.add((nt + 1) * 4);
+    oCS = p.add((kNumCoarse + 1) * 8);
+    oTB = p.add((kNumCoarse + 1) * 4);
+    oH2 = p.add(nslots * 4);
+    oO2 = p.add((nslots + 1) * 8);
+    oBB = p.add(((uint64_t)kNumBuckets + 1) * 8);
+    oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
+    scan_off = p.total;
+  }
+  size_t bytes() const {
+    const uint64_t m = (uint64_t)kNumCoarse * nt > nslots ? (uint64_t)kNumCoarse * nt : nslots;
+    return p.total + scan_ws_bytes(m);
+  }
+};
+
+size_t bucket_ws_bytes(uint64_t n) { return BucketPlan(n).bytes(); }
 
 // Flags-only triage of a device-resident batch (ctx lock held).
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
@@ -448,80 +554,69 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
   if (n == 0) return SG_OK;
-  const uint64_t nt = (n + kPT - 1) / kPT;
-  WsPlan p;
-  const size_t oA = p.add(n * 8), oB = p.add(n * 8);
-  const size_t oH1 = p.add((uint64_t)(1 << kD0Bits) * nt * 4), oO1 = p.add(((uint64_t)(1 << kD0Bits) * nt + 1) * 8);
-  const size_t oH2 = p.add((uint64_t)(1 << kD1Bits) * nt * 4), oO2 = p.add(((uint64_t)(1 << kD1Bits) * nt + 1) * 8);
-  const size_t oTR = p.add((nt + 1) * 4), oBB = p.add(((uint64_t)kNumBuckets + 1) * 8);
-  const size_t oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
-  const size_t scan_off = p.total;
-  int rc = ws_reserve(ctx, bucket_ws_bytes(n));
+  if ((n + kPT - 1) / kPT + kNumCoarse >= 0xFFFFFFFFull) {
+    set_error("bucket triage: batch too large");
+    return SG_EINVAL;
+  }
+  const BucketPlan bp(n);
+  int rc = ws_reserve(ctx, bp.bytes());
   if (rc) return rc;
-  uint64_t* A = (uint64_t*)ws_at(ctx, oA);
-  uint64_t* B = (uint64_t*)ws_at(ctx, oB);
-  PartArgs pa{};
-  pa.n = n;
-  pa.ntiles = nt;
-  pa.rec_off = d_off;
-  pa.nrec = nrec;
-  pa.tile_rec = (uint32_t*)ws_at(ctx, oTR);
+  const uint64_t nt = bp.nt;
+  P1Args a1{};
+  a1.vals = d_vals;
+  a1.n = n;
+  a1.ntiles = nt;
+  a1.rec_off = d_off;
+  a1.tile_rec = (uint32_t*)ws_at(ctx, bp.oTR);
+  a1.hist = (uint32_t*)ws_at(ctx, bp.oH1);
+  a1.goff = (uint64_t*)ws_at(ctx, bp.oO1);
+  a1.s_out = (uint32_t*)ws_at(ctx, bp.oS);
+  a1.r_out = (uint32_t*)ws_at(ctx, bp.oR);
   hipLaunchKernelGGL(k_tile_rec_pt, dim3(div_up(nt + 1, 256)), dim3(256), 0, ctx->stream, d_off, nrec, n, nt,
-                     (uint32_t*)pa.tile_rec);
+                     (uint32_t*)a1.tile_rec);
   {
     ScopedTimer tm(ctx, "part1_hist");
-    pa.vals = d_vals;
-    pa.hist = (uint32_t*)ws_at(ctx, oH1);
-    hipLaunchKernelGGL((k_part_hist<false, kD0Shift, kD0Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream,
-                       pa);
+    hipLaunchKernelGGL(k_p1_hist, dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream, a1);
   }
-  rc = scan_counts(ctx, pa.hist, (uint64_t*)ws_at(ctx, oO1), (uint64_t)(1 << kD0Bits) * nt, scan_off);
+  rc = scan_counts(ctx, a1.hist, (uint64_t*)a1.goff, (uint64_t)kNumCoarse * nt, bp.scan_off);
   if (rc) return rc;
   {
     ScopedTimer tm(ctx, "part1_scatter");
-    pa.goff = (uint64_t*)ws_at(ctx, oO1);
-    pa.out = A;
-    if (part_direct())
-      hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits, true>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                         ctx->stream, pa);
-    else
-      hipLaunchKernelGGL((k_part_scatter<false, kD0Shift, kD0Bits, false>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                         ctx->stream, pa);
+    hipLaunchKernelGGL(k_p1_scatter, dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream, a1);
   }
+  P2Args a2{};
+  a2.s_in = a1.s_out;
+  a2.r_in = a1.r_out;
+  a2.cs = (uint64_t*)ws_at(ctx, bp.oCS);
+  a2.tb = (uint32_t*)ws_at(ctx, bp.oTB);
+  a2.hist = (uint32_t*)ws_at(ctx, bp.oH2);
+  a2.goff = (uint64_t*)ws_at(ctx, bp.oO2);
+  a2.out = (uint64_t*)ws_at(ctx, bp.oB);
+  hipLaunchKernelGGL(k_p2_tiles, dim3(1), dim3(kNumCoarse), 0, ctx->stream, a1.goff, nt, n, (uint64_t*)a2.cs,
+                     (uint32_t*)a2.tb);
   {
     ScopedTimer tm(ctx, "part2_hist");
-    pa.vals = nullptr;
-    pa.pairs = A;
-    pa.hist = (uint32_t*)ws_at(ctx, oH2);
-    hipLaunchKernelGGL((k_part_hist<true, kD1Shift, kD1Bits>), dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream,
-                       pa);
+    hipLaunchKernelGGL(k_p2_hist, dim3((uint32_t)bp.g2), dim3(kPThreads), 0, ctx->stream, a2);
   }
-  rc = scan_counts(ctx, pa.hist, (uint64_t*)ws_at(ctx, oO2), (uint64_t)(1 << kD1Bits) * nt, scan_off);
+  rc = scan_counts(ctx, a2.hist, (uint64_t*)a2.goff, bp.nslots, bp.scan_off);
   if (rc) return rc;
   {
     ScopedTimer tm(ctx, "part2_scatter");
-    pa.goff = (uint64_t*)ws_at(ctx, oO2);
-    pa.out = B;
-    if (part_direct())
-      hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits, true>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                         ctx->stream, pa);
-    else
-      hipLaunchKernelGGL((k_part_scatter<true, kD1Shift, kD1Bits, false>), dim3((uint32_t)nt), dim3(kPThreads), 0,
-                         ctx->stream, pa);
+    hipLaunchKernelGGL(k_p2_scatter, dim3((uint32_t)bp.g2), dim3(kPThreads), 0, ctx->stream, a2);
   }
   BucketArgs ba{};
-  ba.pairs = B;
-  ba.bounds = (uint64_t*)ws_at(ctx, oBB);
+  ba.pairs = a2.out;
+  ba.bounds = (uint64_t*)ws_at(ctx, bp.oBB);
   ba.mwords = mwords;
   ba.nwords = nwords;
   ba.rec_new = d_rec_new;
-  ba.nspill = (uint32_t*)ws_at(ctx, oSP);
+  ba.nspill = (uint32_t*)ws_at(ctx, bp.oSP);
   ba.spill = ba.nspill + 1;
   SG_HIP(hipMemsetAsync(ba.nspill, 0, 4, ctx->stream));
   {
     ScopedTimer tm(ctx, "bucket_bounds");
-    hipLaunchKernelGGL(k_bucket_bounds, dim3(div_up((uint64_t)kNumBuckets + 1, 256)), dim3(256), 0, ctx->stream, B,
-                       n, (uint64_t*)ba.bounds);
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(div_up((uint64_t)kNumBuckets + 1, 256)), dim3(256), 0, ctx->stream,
+                       a2.goff, a2.tb, bp.nslots, (uint64_t*)ba.bounds);
   }
   {
     ScopedTimer tm(ctx, "bucket_triage");

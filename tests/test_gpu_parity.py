@@ -292,6 +292,14 @@ def test_triage_edge_cases(C):
     vals = (0xABC00000 + rng.integers(0, 32768, size=300000)).astype(np.uint32)
     off = np.concatenate([[0], np.sort(rng.integers(0, vals.size, size=999)), [vals.size]]).astype(np.uint64)
     _check_triage(P, (om, on), vals, off)
+    # one coarse slice (s >> 23) spanning many partition tiles beside hundreds of
+    # tiny ones, and a bucket whose distinct candidates nearly fill the LDS map
+    big = (0x12000000 + rng.integers(0, 1 << 23, size=50000)).astype(np.uint32)
+    tiny = ((rng.integers(0, 512, size=700) << 23) | rng.integers(0, 1 << 23, size=700)).astype(np.uint32)
+    dense = (0x77700000 + rng.permutation(32768)[:3000]).astype(np.uint32)
+    vals = np.concatenate([tiny[:300], big, dense, tiny[300:], dense[::-1], big[:999]])
+    off = np.concatenate([[0], np.sort(rng.integers(0, vals.size, size=300)), [vals.size]]).astype(np.uint64)
+    _check_triage(P, (om, on), vals, off)
     m, n = P.exports()
     assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
 
