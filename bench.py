@@ -92,21 +92,32 @@ def triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off):
          diff_off.data_ptr() if diff_off is not None else None)
 
 
-KERNELS = ["part1_hist", "part1_scatter", "part2_hist", "part2_scatter", "bucket_bounds", "bucket_triage",
-           "tile_rec", "triage_claim", "triage_resolve", "scan", "emit"]
+KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan",
+           "triage_claim", "triage_resolve", "emit"]
 
 
-def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords, nt):
+def part_geometry(n_in, n_rec):
+    """Tile / chunk counts of the partitioned path (sg_bucket.hip BucketPlan):
+    pass-1 tiles, and pass-2 chunks (about one per non-empty group of 240
+    tiles x 256 slices for spread-out signal)."""
+    na = -(-int(n_in) // 8192)
+    t = na + (int(n_rec) - 1) // 256
+    kt = -(-t // 240)
+    return t, 256 * kt
+
+
+def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords):
     """Algorithmic bytes per launch of each kernel.  n_cand =
-    values not in maxSignal at batch start."""
-    g2 = nt + 512
+    values not in maxSignal at batch start.  Partition passes move 4 B per
+    entry each way plus their [digit][tile] offset tables."""
+    t, g2 = part_geometry(n_in, n_rec)
     mbits = 4 * (1 << 27)  # the maxSignal bitmap, read once slice by slice
     return {
-        "part1_hist": 4 * n_in + 512 * nt * 4,
-        "part1_scatter": 4 * n_in + 8 * n_in + 512 * nt * 8,
-        "part2_hist": 4 * n_in + 256 * g2 * 4,
-        "part2_scatter": 8 * n_in + 8 * n_in + 256 * g2 * 8,
-        "bucket_triage": 8 * n_in + mbits + 16 * n_newwords + n_rec,
+        "p1_hist": 4 * n_in + 256 * t * 4,
+        "p1_scatter": 4 * n_in + 4 * n_in + 256 * t * 4,
+        "p2_hist": 4 * n_in + 256 * g2 * 4,
+        "p2_scatter": 4 * n_in + 4 * n_in + 256 * g2 * 4,
+        "bucket_triage": 4 * n_in + mbits + 8 * n_cand + 16 * n_newwords + n_rec,
         "triage_claim": 4 * n_in + 4 * n_in + 8 * n_cand + n_in / 8,
         "triage_resolve": n_in / 8 + 4 * n_cand + 4 * n_cand + 16 * n_diff + n_rec + n_in / 8 + n_in / 64,
     }
@@ -330,8 +341,7 @@ def main():
             L = args.steps
             n_in, n_cand, n_diff, n_rec, n_new = (acct[x] / L for x in ("n_in", "n_cand", "n_diff", "n_rec",
                                                                          "n_new_signal"))
-            nt = (n_in + 8191) // 8192  # partition tiles (kPT)
-            per = algo_bytes(n_in, n_cand, n_diff, n_rec, min(n_new, 1 << 27), nt)
+            per = algo_bytes(n_in, n_cand, n_diff, n_rec, min(n_new, 1 << 27))
             for kname, b in per.items():
                 if kname in kernels:
                     avg_s = kernels[kname]["ms_total"] / kernels[kname]["launches"] / 1e3

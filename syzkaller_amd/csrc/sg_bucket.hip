@@ -6,84 +6,261 @@
 // maxSignal / newSignal (fuzzer.go:673-674); the diff slice (fuzzer.go:669)
 // is a transient that only feeds those SignalAdd calls.
 //
-// Same first-owner rule as sg_triage.hip (a record is new iff it is the
-// first, in sequential order, to contain some signal s not in maxSignal),
-// organised so that no access is random across HBM:
-//   1. stable MSD partition of the batch by the coarse digit s >> 23: 512
-//      slices of 2^23 signals, each backed by 1 MiB of the maxSignal bitmap;
-//      out: (s, record) in two u32 arrays,
-//   2. per coarse slice, a stable partition by the fine digit (s >> 15) & 255
-//      that DROPS every s already in maxSignal.  The workgroups of one XCD
-//      walk consecutive tiles, so the slice they probe is the same 1 MiB and
-//      stays in that XCD's L2; only the candidates (signals not in
-//      maxSignal, ~12 % of a C2 batch, far fewer in a warm fuzzer) go on,
-//      as (s << 32 | record) pairs grouped by the 17-bit bucket s >> 15,
-//   3. one workgroup per bucket (32768 signals): an LDS hash map
-//      signal -> min(record) over its candidates decides the new records
-//      and the bucket's new bits go back to maxSignal / newSignal from its
-//      only writer.  Buckets with more distinct candidates than the map
-//      holds are redone by a second kernel with a direct 32768-entry table.
-// No global atomics, no 16 GiB owner table, every HBM stream coalesced.
+// Same first-owner rule as sg_triage.hip: a record is new iff it is the
+// first, in sequential order, to contain some signal s not in maxSignal.
+// Owners are minima over record indices, so the order of entries inside a
+// partition never matters; what has to travel with each entry is its record.
+// Every stream here is 4 bytes per signal entry:
 //
-// A partition pass = histogram kernel (per 8192-value tile, LDS counters) +
-// device exclusive scan over [digit][tile] + scatter kernel: each wave holds
-// its 1024 values in registers, ranks them in order with a ballot multisplit
-// (stable), the tile is reordered by digit in LDS and written out in digit
-// runs.  Both scatters map blocks to tiles XCD-contiguously (T1 swizzle), so
-// the partial lines at digit-run seams of neighbouring tiles merge in one L2.
+//   tiles   the batch is cut into pass-1 tiles of <= kPT entries that span
+//           <= kRecCap records (cuts at every kPT-th entry and at every
+//           kRecCap-th record offset), so an entry's record is
+//           trec[tile] + an 8-bit in-tile index;
+//   pass 1  partition by the top byte of s (256 slices of 2^24 signals):
+//           entry = s << 8 | rec_in_tile, runs laid out [slice][tile];
+//   pass 2  per slice, groups of kGroupTiles consecutive pass-1 tiles, cut
+//           into chunks of <= kPT entries; partition by bits 16..23
+//           of s: entry = (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile,
+//           runs laid out [byte][chunk];
+//   bucket  one workgroup per 2^16-signal bucket (d, f): its 8 KiB maxSignal
+//           slice in LDS is the new-signal test; candidates (s not in
+//           maxSignal) recover their record through the chunk -> group ->
+//           tile tables and go into an LDS hash map s -> min(record).  The
+//           bucket's new bits go back to maxSignal / newSignal from their
+//           only writer.  Buckets whose distinct candidates overflow the map
+//           are redone by a direct-table kernel.
+// Each partition pass = a byte histogram per tile (LDS counters) + a device
+// exclusive scan + a scatter (tile in registers, LDS counting-rank, staged
+// by digit, written in digit runs).  No global atomics on the data path, no
+// random HBM access, no 16 GiB owner table.
 #include "sg_internal.h"
 
 namespace sg {
 
-constexpr int kPT = 8192;                   // partition tile (values): LDS fits two tiles per CU
-constexpr int kPThreads = 512;              // 8 waves
+constexpr int kPT = 8192;                    // entries per partition tile / chunk
+constexpr int kPThreads = 512;               // 8 waves
 constexpr int kPWaves = kPThreads / 64;
-constexpr int kPerWave = kPT / kPWaves;     // 1024 values per wave, in order
-constexpr int kSteps = kPerWave / 64;       // 16 values per lane
-constexpr int kBucketBits = 15;             // 32768 signals per bucket
-constexpr uint32_t kBucketSig = 1u << kBucketBits;
-constexpr uint32_t kBucketWords = kBucketSig / 32;  // 1024
-constexpr uint32_t kNumBuckets = 1u << (32 - kBucketBits);  // 131072
-constexpr int kCShift = 23, kCBits = 9;     // pass 1 (coarse) digit: bits 23..31
-constexpr int kFShift = 15, kFBits = 8;     // pass 2 (fine) digit: bits 15..22
-constexpr uint32_t kNumCoarse = 1u << kCBits;
-constexpr int kRecWin = 1024;               // record offsets kept in LDS per tile (tile-relative u16)
-constexpr int kBTThreads = 512;             // bucket kernel
-constexpr int kBU = 16;                     // pairs per thread in flight (8192 per block)
-constexpr int kHash = 4096;                 // max candidate hash slots per bucket
+constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
+constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
+constexpr uint32_t kRecCap = 256;            // records per pass-1 tile (8-bit index)
+// pass-1 tiles per pass-2 group (8-bit index).  A full tile puts ~kPT/256
+// entries into each slice, so a group is ~kGroupTiles * 32 entries: 240 keeps
+// it just under one kPT chunk for uniformly spread signal.
+constexpr uint32_t kGroupTiles = 240;
+constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
+constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
+constexpr int kBThreads = 512;
+constexpr int kBU = 16;                      // entries per thread per round in the bucket kernel
+constexpr uint32_t kHash = 4096;             // candidate map slots per bucket
+constexpr uint32_t kRunWin = 1024;           // chunk run starts kept in LDS per bucket
+constexpr uint32_t kQueue = 2048;            // candidates queued per round (dense processing)
+constexpr uint32_t kMaxProbe = 64;           // linear-probe cap before a bucket spills
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-// blocks sharing an XCD (bid % 8 under round-robin dispatch) get a contiguous
-// run of tiles; a bijection on [0, g) for any g (speed only, never correctness)
+// Blocks sharing an XCD (bid % 8 under round-robin dispatch) get a contiguous
+// run of tiles, so partial lines at the seams of neighbouring tiles' digit
+// runs merge in one L2.  A bijection on [0, g) for any g (speed only).
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t g) {
   const uint32_t x = bid & 7, q = g >> 3, r = g & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-template <int kShift, int kBits>
-__device__ __forceinline__ uint32_t digit_of(uint32_t s) {
-  return (s >> kShift) & ((1u << kBits) - 1);
+// ------------------------------------------------------------- tile cuts ---
+// Pass-1 tiles: sorted merge of A = {i * kPT : i < nA} and B = {rec_off[(j +
+// 1) * kRecCap] : j < nB} (both non-decreasing; ties put A first).
+// start[rank] = cut position (start[nA + nB] = n), aux[rank] = record holding
+// the entry at the cut.  Coinciding cuts give empty tiles.
+struct Cuts {
+  uint64_t nA, step, nB, n;
+  const uint64_t* rec_off;
+  uint64_t nrec;
+  uint32_t* start;
+  uint32_t* aux;
+  __device__ __forceinline__ uint64_t B(uint64_t j) const { return rec_off[(j + 1) * kRecCap]; }
+  // #{j : B[j] < x}
+  __device__ __forceinline__ uint64_t countB(uint64_t x) const {
+    uint64_t lo = 0, hi = nB;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (B(mid) < x)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  }
+};
+
+__global__ void k_cuts(Cuts c) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = c.nA + c.nB;
+  if (i > total) return;
+  if (i == total) {
+    c.start[total] = (uint32_t)c.n;
+    return;
+  }
+  uint64_t x, rank;
+  if (i < c.nA) {
+    x = i * c.step;
+    rank = i + c.countB(x);
+  } else {
+    const uint64_t j = i - c.nA;
+    x = c.B(j);
+    const uint64_t a = x / c.step + 1;
+    rank = j + (a < c.nA ? a : c.nA);
+  }
+  c.start[rank] = (uint32_t)x;
+  // record holding entry x (largest r with rec_off[r] <= x)
+  const uint64_t xe = x < c.n ? x : (c.n ? c.n - 1 : 0);
+  c.aux[rank] = (uint32_t)sgd::seg_search(c.rec_off, 0, c.nrec - 1, xe);
 }
 
-// Counting sort of one tile held in registers (kSteps values per lane) by
-// digit, through LDS: counts, one-wave exclusive scan, then every value takes
-// a slot with an LDS atomic.  The order within a digit is NOT the input order
-// -- nothing downstream needs it: first owners are minima over records.
-// On return cnt[] is free, dstart[d] is the digit's first slot in the tile
-// and pos[k] the slot of value k (valid lanes only).
-template <int kBits>
+// Pass-2 groups: group j = (slice j / kt, tiles [(j % kt) * kGroupTiles, +kGroupTiles))
+// covers [gstart(j), gstart(j + 1)) of the pass-1 output; it is cut into
+// ceil(size / kPT) chunks (none when empty).
+__device__ __forceinline__ uint32_t group_start(const uint32_t* goff1, uint64_t T, uint64_t kt, uint64_t ng,
+                                                uint32_t n, uint64_t j) {
+  return j < ng ? goff1[(j / kt) * T + (j % kt) * kGroupTiles] : n;
+}
+
+__global__ void k_group_chunks(const uint32_t* __restrict__ goff1, uint64_t T, uint64_t kt, uint64_t ng, uint32_t n,
+                               uint32_t* __restrict__ nch) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ng) return;
+  const uint32_t sz = group_start(goff1, T, kt, ng, n, j + 1) - group_start(goff1, T, kt, ng, n, j);
+  nch[j] = (sz + kPT - 1) / kPT;
+}
+
+// cbase = exclusive scan of nch (cbase[ng] = number of chunks G).  Writes the
+// chunk list (start, group) for c < G, start = n for G <= c <= gmax (the
+// launch grids use gmax, an upper bound known on the host), and cfirst[d] =
+// first chunk of slice d (cfirst[256] = G).
+__global__ void k_chunk_list(const uint32_t* __restrict__ goff1, uint64_t T, uint64_t kt, uint64_t ng, uint32_t n,
+                             const uint32_t* __restrict__ cbase, uint64_t gmax, uint32_t* __restrict__ cstart,
+                             uint32_t* __restrict__ cgov, uint32_t* __restrict__ cfirst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t G = cbase[ng];
+  if (i < ng) {
+    const uint32_t g0 = group_start(goff1, T, kt, ng, n, i), g1 = group_start(goff1, T, kt, ng, n, i + 1);
+    uint32_t c = cbase[i];
+    for (uint32_t e = g0; e < g1; e += kPT, c++) {
+      cstart[c] = e;
+      cgov[c] = (uint32_t)i;
+    }
+  }
+  if (i >= G && i <= gmax) {
+    cstart[i] = n;
+    cgov[i] = (uint32_t)(ng - 1);
+  }
+  if (i <= 256) cfirst[i] = i < 256 ? cbase[i * kt] : G;
+}
+
+// One 16-B descriptor per pass-2 block (the grid is the host bound gmax):
+// {start, end, group, chunk} of chunk xcd_tile(bid, G) for bid < G, empty
+// past G.  Lets the pass-2 kernels start their data loads after one load.
+__global__ void k_chunk_desc(const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ cgov,
+                             const uint32_t* __restrict__ gcount, uint64_t gmax, uint4* __restrict__ desc) {
+  const uint64_t bid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (bid >= gmax) return;
+  const uint32_t G = *gcount;
+  if (bid < G) {
+    const uint32_t c = xcd_tile((uint32_t)bid, G);
+    desc[bid] = make_uint4(cstart[c], cstart[c + 1], cgov[c], c);
+  } else {
+    desc[bid] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// --------------------------------------------------------- byte histogram ---
+// hist[(v >> 24) * ncols + tile] = count over entries [start[tile], start[tile+1]).
+// kVec (v 16-B aligned): whole aligned quads by uint4 loads, the <= 3 entries
+// before the first and after the last quad by single loads.
+constexpr int kHistQ = kPT / 4 / kPThreads;  // uint4 loads per lane
+// Pass 1: tile t = xcd_tile(bid, grid), range [start[t], start[t+1]), T =
+// grid columns.  Pass 2 (desc != nullptr): the block's chunk descriptor and
+// *ncols_dev columns; blocks without a chunk exit.
+template <bool kVec>
+__global__ __launch_bounds__(kPThreads) void k_hist_top(const uint32_t* __restrict__ v,
+                                                        const uint32_t* __restrict__ start,
+                                                        const uint4* __restrict__ desc,
+                                                        const uint32_t* __restrict__ ncols_dev,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t cnt[256];
+  uint32_t t, s0, s1, ncols;
+  if (desc) {
+    const uint4 d = desc[blockIdx.x];
+    s0 = d.x;
+    s1 = d.y;
+    t = d.w;
+    if (s0 >= s1) return;
+    ncols = *ncols_dev;
+  } else {
+    ncols = gridDim.x;
+    t = xcd_tile(blockIdx.x, ncols);
+    s0 = start[t];
+    s1 = start[t + 1];
+  }
+  const int tid = threadIdx.x;
+  if (tid < 256) cnt[tid] = 0;
+  if (kVec) {
+    const uint4* v4 = reinterpret_cast<const uint4*>(v);
+    const uint32_t q0 = (s0 + 3) >> 2, q1 = s1 >> 2;  // whole quads [q0, q1)
+    uint4 x[kHistQ + 1];
+#pragma unroll
+    for (int k = 0; k <= kHistQ; k++) {
+      const uint32_t q = q0 + k * kPThreads + tid;
+      x[k] = q < q1 ? v4[q] : make_uint4(0, 0, 0, 0);
+    }
+    // head (entries before quad q0) and tail (after quad q1), at most 3 each
+    uint32_t e1 = 0xFFFFFFFFu, y = 0;
+    if (tid < 3) e1 = s0 + tid < q0 * 4 && s0 + tid < s1 ? s0 + tid : 0xFFFFFFFFu;
+    else if (tid < 6) e1 = q1 * 4 + (tid - 3) < s1 && q1 * 4 + (tid - 3) >= s0 && q1 >= q0 ? q1 * 4 + (tid - 3)
+                                                                                         : 0xFFFFFFFFu;
+    if (e1 != 0xFFFFFFFFu) y = v[e1];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k <= kHistQ; k++)
+      if (q0 + k * kPThreads + tid < q1) {
+        atomicAdd(&cnt[x[k].x >> 24], 1u);
+        atomicAdd(&cnt[x[k].y >> 24], 1u);
+        atomicAdd(&cnt[x[k].z >> 24], 1u);
+        atomicAdd(&cnt[x[k].w >> 24], 1u);
+      }
+    if (e1 != 0xFFFFFFFFu) atomicAdd(&cnt[y >> 24], 1u);
+  } else {
+    uint32_t x[kPT / kPThreads];
+#pragma unroll
+    for (int k = 0; k < kPT / kPThreads; k++) {
+      const uint32_t e = s0 + k * kPThreads + tid;
+      x[k] = e < s1 ? v[e] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPT / kPThreads; k++)
+      if (s0 + k * kPThreads + tid < s1) atomicAdd(&cnt[x[k] >> 24], 1u);
+  }
+  __syncthreads();
+  if (tid < 256) hist[(uint64_t)tid * ncols + t] = cnt[tid];
+}
+
+// Counting sort of one tile held in registers (kSteps entries per lane) by an
+// 8-bit digit, through LDS: counts, a one-wave exclusive scan, then every
+// entry takes a slot with an LDS atomic (order within a digit is arbitrary).
+// On return dstart[d] is the digit's first slot and pos[k] entry k's slot.
 __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t vmask, uint32_t* cnt,
                                           uint16_t* dstart, uint32_t (&pos)[kSteps]) {
-  constexpr int R = 1 << kBits;
   const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
     if ((vmask >> k) & 1u) atomicAdd(&cnt[dv[k]], 1u);
   __syncthreads();
-  if (tid < 64) {  // one wave scans the R digit counts; cnt becomes the cursor
+  if (tid < 64) {
     uint32_t carry = 0;
-    for (int base = 0; base < R; base += 64) {
+#pragma unroll
+    for (int base = 0; base < 256; base += 64) {
       const uint32_t x = cnt[base + lane];
       uint32_t incl = x;
+#pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
@@ -100,278 +277,263 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
     if ((vmask >> k) & 1u) pos[k] = atomicAdd(&cnt[dv[k]], 1u);
 }
 
-// ---------------------------------------------------------------- pass 1 ---
-
-struct P1Args {
-  const uint32_t* vals;
-  uint64_t n;
-  uint64_t ntiles;
-  const uint64_t* rec_off;  // nrec + 1
-  const uint32_t* tile_rec; // record of each tile's first value (ntiles + 1)
-  uint32_t* hist;           // [coarse digit][tile]
-  const uint64_t* goff;     // scanned hist
-  uint32_t* s_out;          // partitioned signals
-  uint32_t* r_out;          // their records
+// O(1) "largest k with st[k] <= p" inside one tile of <= kPT positions, for
+// sorted segment starts st[0..m) given tile-relative and clamped to [0, kPT]
+// (st[0] == 0, m <= 256).  Non-empty segments that start inside the tile are
+// marked: bit p of sbits <=> one starts at p > 0, sidx[p] = its index;
+// wmax[w] = index of the segment holding position 32w + 31; kinit = the
+// segment holding position 0.  Replaces a per-entry search (segments can be
+// a few entries long: small records, thin slices).
+struct SegLds {
+  uint32_t sbits[kPT / 32];
+  uint8_t wmax[kPT / 32];
+  uint32_t kinit;
 };
 
-__global__ __launch_bounds__(kPThreads) void k_p1_hist(P1Args a) {
-  constexpr int R = 1 << kCBits;
-  __shared__ uint32_t cnt[R];
-  for (int i = threadIdx.x; i < R; i += kPThreads) cnt[i] = 0;
-  __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * kPT;
-  if (t0 + kPT <= a.n && (((uintptr_t)a.vals & 15) == 0)) {  // 16-B loads, 4 per lane
-    const uint4* v4 = reinterpret_cast<const uint4*>(a.vals + t0);
-    uint4 q[kPT / 4 / kPThreads];
-#pragma unroll
-    for (int j = 0; j < kPT / 4 / kPThreads; j++) q[j] = v4[j * kPThreads + threadIdx.x];
-#pragma unroll
-    for (int j = 0; j < kPT / 4 / kPThreads; j++) {
-      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].x)], 1u);
-      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].y)], 1u);
-      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].z)], 1u);
-      atomicAdd(&cnt[digit_of<kCShift, kCBits>(q[j].w)], 1u);
-    }
-  } else {
-    for (int i = threadIdx.x; i < kPT; i += kPThreads) {
-      const uint64_t e = t0 + i;
-      if (e < a.n) atomicAdd(&cnt[digit_of<kCShift, kCBits>(a.vals[e])], 1u);
+__device__ __forceinline__ void seg_clear(SegLds& L, int tid) {
+  for (int w = tid; w < kPT / 32; w += kPThreads) L.sbits[w] = 0;
+  if (tid == 0) L.kinit = 0;
+}
+
+// call after seg_clear + a barrier; ends with a barrier
+template <typename S>
+__device__ __forceinline__ void seg_build(SegLds& L, uint8_t* sidx, const S* st, uint32_t m, uint32_t n, int tid) {
+  for (uint32_t k = tid; k < m; k += kPThreads) {
+    const uint32_t p = st[k], nx = k + 1 < m ? (uint32_t)st[k + 1] : 0xFFFFFFFFu;
+    if (p == 0) {
+      if (nx > 0) atomicMax(&L.kinit, k);
+    } else if (p < n && nx > p) {
+      atomicOr(&L.sbits[p >> 5], 1u << (p & 31));
+      sidx[p] = (uint8_t)k;
     }
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[(uint64_t)d * a.ntiles + blockIdx.x] = cnt[d];
+  if (tid < 64) {  // prefix max over the 256 words, 4 per lane
+    int run = -1;
+    int loc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int w = tid * 4 + j;
+      const uint32_t b = L.sbits[w];
+      if (b) run = max(run, (int)sidx[w * 32 + 31 - __clz(b)]);
+      loc[j] = run;
+    }
+    int incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (tid >= o) incl = max(incl, y);
+    }
+    int ex = __shfl_up(incl, 1);
+    if (tid == 0) ex = -1;
+    ex = max(ex, (int)L.kinit);
+#pragma unroll
+    for (int j = 0; j < 4; j++) L.wmax[tid * 4 + j] = (uint8_t)max(ex, loc[j]);
+  }
+  __syncthreads();
 }
 
+__device__ __forceinline__ uint32_t seg_lookup(const SegLds& L, const uint8_t* sidx, uint32_t p) {
+  const uint32_t w = p >> 5;
+  const uint32_t m = L.sbits[w] & (0xFFFFFFFFu >> (31 - (p & 31)));
+  return m ? sidx[(w << 5) + 31 - __clz(m)] : (w ? L.wmax[w - 1] : L.kinit);
+}
+
+// ---------------------------------------------------------------- pass 1 ---
+struct P1Args {
+  const uint32_t* vals;
+  const uint64_t* rec_off;
+  uint64_t nrec;
+  const uint32_t* tstart;  // T + 1
+  const uint32_t* trec;    // T
+  uint32_t T;
+  const uint32_t* goff1;   // scanned [slice][tile]
+  uint32_t* out;           // s << 8 | rec_in_tile
+};
+
 __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
-  constexpr int R = 1 << kCBits;
-  __shared__ uint64_t stage[kPT];        // the tile grouped by digit: (s << 32) | record (64 KiB)
-  __shared__ uint32_t cnt[R];
-  __shared__ uint16_t dstart[R];         // tile-local start of each digit
-  __shared__ uint64_t gbase[R];          // global start of (digit, this tile)
-  __shared__ uint16_t win[kRecWin];      // record offsets of the tile, clamped to [t0, t0 + kPT] - t0
+  __shared__ uint32_t stage[kPT];
+  __shared__ uint8_t sdig[kPT];
+  __shared__ uint32_t cnt[256];
+  __shared__ uint16_t dstart[256];
+  __shared__ uint32_t gbase[256];
+  __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
+  __shared__ SegLds L;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x), t0 = tile * kPT;
-  const uint64_t ebase = t0 + (uint64_t)w * kPerWave;
-  // this wave's 1024 values in registers, every load in flight at once
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
+  const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
+  if (s0 >= s1) return;
+  const uint32_t r0 = a.trec[t];
+  const uint32_t wn = (uint32_t)(a.nrec + 1 - r0 < kRecCap + 1 ? a.nrec + 1 - r0 : kRecCap + 1);
+  const uint32_t ebase = s0 + w * kPerWave;
   uint32_t sv[kSteps];
   uint32_t vmask = 0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
-    sv[k] = e < a.n ? a.vals[e] : 0u;
-    vmask |= (e < a.n ? 1u : 0u) << k;
+    const uint32_t e = ebase + k * 64 + lane;
+    const bool ok = e < s1;
+    sv[k] = ok ? a.vals[e] : 0u;
+    vmask |= (ok ? 1u : 0u) << k;
   }
-  const uint64_t ra = a.tile_rec[tile], rb = a.tile_rec[tile + 1], wn = rb - ra + 1;
-  const bool inwin = wn <= (uint64_t)kRecWin;
-  if (inwin)
-    for (uint64_t i = tid; i < wn; i += kPThreads) {
-      const uint64_t o = a.rec_off[ra + i];
-      win[i] = (uint16_t)(o <= t0 ? 0 : (o - t0 >= (uint64_t)kPT ? kPT : o - t0));
-    }
-  for (int d = tid; d < R; d += kPThreads) {
-    gbase[d] = a.goff[(uint64_t)d * a.ntiles + tile];
+  for (uint32_t i = tid; i < wn; i += kPThreads) {
+    const uint64_t o = a.rec_off[r0 + i];
+    win[i] = (uint16_t)(o <= s0 ? 0 : (o - s0 >= (uint64_t)kPT ? kPT : o - s0));
+  }
+  for (int d = tid; d < 256; d += kPThreads) {
+    gbase[d] = a.goff1[(uint64_t)d * a.T + t];
     cnt[d] = 0;
   }
+  seg_clear(L, tid);
   __syncthreads();
-  // records: a lane's values are in order, so its record only moves forward
-  uint32_t rv[kSteps];
-  {
-    uint64_t r = 0;
-    const uint64_t e0 = ebase + lane;
-    if (e0 < a.n) r = inwin ? ra + sgd::seg_search(win, 0, wn - 1, e0 - t0) : sgd::seg_search(a.rec_off, ra, rb, e0);
+  const uint32_t nt = s1 - s0;
+  seg_build(L, sdig, win, wn, nt, tid);  // sdig doubles as the segment index until the rank
+  uint32_t dv[kSteps], pk[kSteps];
+  const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
-    for (int k = 0; k < kSteps; k++) {
-      const uint64_t e = ebase + (uint64_t)k * 64 + lane;
-      if ((vmask >> k) & 1u) {
-        if (inwin) {
-          const uint32_t el = (uint32_t)(e - t0);
-          while (r < rb && win[r + 1 - ra] <= el) r++;
-        } else {
-          r = sgd::seg_search(a.rec_off, r, rb, e);
-        }
-      }
-      rv[k] = (uint32_t)r;
-    }
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sdig, el0 + k * 64) : 0u;  // record in tile
+    dv[k] = sv[k] >> 24;
+    pk[k] = (sv[k] << 8) | r;
   }
-  uint32_t dv[kSteps], pos[kSteps];
-#pragma unroll
-  for (int k = 0; k < kSteps; k++) dv[k] = digit_of<kCShift, kCBits>(sv[k]);
-  tile_rank<kCBits>(dv, vmask, cnt, dstart, pos);
+  uint32_t pos[kSteps];
+  tile_rank(dv, vmask, cnt, dstart, pos);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) stage[pos[k]] = ((uint64_t)sv[k] << 32) | rv[k];
-  __syncthreads();
-  // write out in digit runs (consecutive threads -> consecutive addresses)
-  const uint32_t ntile = (uint32_t)(a.n - t0 < (uint64_t)kPT ? a.n - t0 : (uint64_t)kPT);
-  for (uint32_t p = tid; p < ntile; p += kPThreads) {
-    const uint64_t pair = stage[p];
-    const uint32_t d = digit_of<kCShift, kCBits>((uint32_t)(pair >> 32));
-    const uint64_t o = gbase[d] + (p - dstart[d]);
-    a.s_out[o] = (uint32_t)(pair >> 32);
-    a.r_out[o] = (uint32_t)pair;
-  }
-}
-
-// Tiles of pass 2: coarse slice c covers [cs[c], cs[c+1]) of the pass-1
-// output and owns tiles [tb[c], tb[c+1]); tb[512] = number of tiles.
-__global__ __launch_bounds__(kNumCoarse) void k_p2_tiles(const uint64_t* __restrict__ goff1, uint64_t nt, uint64_t n,
-                                                         uint64_t* __restrict__ cs, uint32_t* __restrict__ tb) {
-  __shared__ uint32_t k[kNumCoarse];
-  const uint32_t c = threadIdx.x;
-  const uint64_t lo = goff1[(uint64_t)c * nt];
-  const uint64_t hi = c + 1 < kNumCoarse ? goff1[(uint64_t)(c + 1) * nt] : n;
-  cs[c] = lo;
-  if (c == 0) cs[kNumCoarse] = n;
-  k[c] = (uint32_t)((hi - lo + kPT - 1) / kPT);
-  __syncthreads();
-  if (c < 64) {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < kNumCoarse; base += 64) {
-      const uint32_t x = k[base + c];
-      uint32_t incl = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if ((int)c >= o) incl += y;
-      }
-      tb[base + c] = carry + incl - x;
-      carry += __shfl(incl, 63);
+    if ((vmask >> k) & 1u) {
+      stage[pos[k]] = pk[k];
+      sdig[pos[k]] = (uint8_t)dv[k];
     }
-    if (c == 0) tb[kNumCoarse] = carry;
+  __syncthreads();
+  for (uint32_t p = tid; p < nt; p += kPThreads) {
+    const uint32_t d = sdig[p];
+    a.out[gbase[d] + (p - dstart[d])] = stage[p];
   }
 }
 
+// ---------------------------------------------------------------- pass 2 ---
 struct P2Args {
-  const uint32_t* s_in;
-  const uint32_t* r_in;
-  const uint64_t* cs;       // coarse slice starts (513)
-  const uint32_t* tb;       // coarse slice first tiles (513)
-  uint32_t* hist;           // [c][fine digit][tile of c], base 256 * tb[c]
-  const uint64_t* goff;     // scanned hist
-  uint64_t* out;            // pairs (s << 32) | record grouped by s >> 15
+  const uint32_t* in;      // pass-1 output
+  const uint4* desc;       // per-block chunk descriptors
+  const uint32_t* g2;      // device: number of chunks G2 (the grid is an upper bound)
+  const uint32_t* goff1;   // pass-1 run starts [slice][tile]
+  uint32_t T, kt;
+  uint32_t n;
+  const uint32_t* goff2;   // scanned [byte][chunk]
+  uint32_t* out;           // (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile
 };
-
-struct P2Tile {
-  uint32_t c, j, kc;
-  uint64_t e0, e1;
-  bool live;
-};
-
-__device__ __forceinline__ P2Tile p2_tile(const P2Args& a) {
-  P2Tile t;
-  const uint32_t t2 = xcd_tile(blockIdx.x, gridDim.x);
-  const uint32_t nt2 = a.tb[kNumCoarse];
-  t.live = t2 < nt2;
-  if (!t.live) {
-    t.c = t.kc = 0;
-    t.j = t2;
-    t.e0 = t.e1 = 0;
-    return t;
-  }
-  t.c = (uint32_t)sgd::seg_search(a.tb, 0, kNumCoarse - 1, t2);  // largest c with tb[c] <= t2
-  t.j = t2 - a.tb[t.c];
-  t.kc = a.tb[t.c + 1] - a.tb[t.c];
-  t.e0 = a.cs[t.c] + (uint64_t)t.j * kPT;
-  const uint64_t end = a.cs[t.c + 1];
-  t.e1 = t.e0 + kPT < end ? t.e0 + kPT : end;
-  return t;
-}
-
-__device__ __forceinline__ uint64_t p2_hist_index(const P2Args& a, const P2Tile& t, uint32_t d) {
-  return ((uint64_t)a.tb[t.c] << kFBits) + (uint64_t)d * t.kc + t.j;
-}
-
-__global__ __launch_bounds__(kPThreads) void k_p2_hist(P2Args a) {
-  constexpr int R = 1 << kFBits;
-  __shared__ uint32_t cnt[R];
-  const P2Tile t = p2_tile(a);
-  if (!t.live) {  // tail of the upper-bound grid: zero its own slots
-    for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[((uint64_t)t.j << kFBits) + d] = 0;
-    return;
-  }
-  for (int i = threadIdx.x; i < R; i += kPThreads) cnt[i] = 0;
-  uint32_t sv[kPT / kPThreads];
-#pragma unroll
-  for (int k = 0; k < kPT / kPThreads; k++) {
-    const uint64_t e = t.e0 + (uint64_t)k * kPThreads + threadIdx.x;
-    sv[k] = e < t.e1 ? a.s_in[e] : 0u;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPT / kPThreads; k++)
-    if (t.e0 + (uint64_t)k * kPThreads + threadIdx.x < t.e1) atomicAdd(&cnt[digit_of<kFShift, kFBits>(sv[k])], 1u);
-  __syncthreads();
-  for (int d = threadIdx.x; d < R; d += kPThreads) a.hist[p2_hist_index(a, t, d)] = cnt[d];
-}
 
 __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
-  constexpr int R = 1 << kFBits;
-  __shared__ uint64_t stage[kPT];
-  __shared__ uint32_t cnt[R];
-  __shared__ uint16_t dstart[R];
-  __shared__ uint64_t gbase[R];
-  const P2Tile t = p2_tile(a);
-  if (!t.live) return;
+  __shared__ uint32_t stage[kPT];
+  __shared__ uint8_t sdig[kPT];
+  __shared__ uint32_t cnt[256];
+  __shared__ uint16_t dstart[256];
+  __shared__ uint32_t gbase[256];
+  __shared__ uint16_t runs[kGroupTiles + 1];  // chunk-relative run starts of the group's tiles in this slice
+  __shared__ SegLds L;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint64_t ebase = t.e0 + (uint64_t)w * kPerWave;
-  uint32_t sv[kSteps], rv[kSteps];
+  const uint4 dsc = a.desc[blockIdx.x];
+  const uint32_t s0 = dsc.x, s1 = dsc.y, gov = dsc.z, c = dsc.w;
+  if (s0 >= s1) return;
+  const uint32_t G2 = *a.g2;
+  const uint32_t d = gov / a.kt, tb = (gov % a.kt) * kGroupTiles;
+  const uint32_t ntl = a.T - tb < kGroupTiles ? a.T - tb : kGroupTiles;
+  const uint32_t ebase = s0 + w * kPerWave;
+  uint32_t sv[kSteps];
   uint32_t vmask = 0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint64_t e = ebase + (uint64_t)k * 64 + lane;
-    const bool v = e < t.e1;
-    sv[k] = v ? a.s_in[e] : 0u;
-    rv[k] = v ? a.r_in[e] : 0u;
-    vmask |= (v ? 1u : 0u) << k;
+    const uint32_t e = ebase + k * 64 + lane;
+    const bool ok = e < s1;
+    sv[k] = ok ? a.in[e] : 0u;
+    vmask |= (ok ? 1u : 0u) << k;
   }
-  for (int d = tid; d < R; d += kPThreads) {
-    gbase[d] = a.goff[p2_hist_index(a, t, d)];
-    cnt[d] = 0;
+  for (uint32_t i = tid; i < ntl; i += kPThreads) {
+    const uint32_t o = a.goff1[(uint64_t)d * a.T + tb + i];
+    runs[i] = (uint16_t)(o <= s0 ? 0 : (o - s0 >= (uint32_t)kPT ? kPT : o - s0));
   }
+  for (int f = tid; f < 256; f += kPThreads) {
+    gbase[f] = a.goff2[(uint64_t)f * G2 + c];
+    cnt[f] = 0;
+  }
+  seg_clear(L, tid);
   __syncthreads();
-  uint32_t dv[kSteps], pos[kSteps];
+  const uint32_t nt = s1 - s0;
+  seg_build(L, sdig, runs, ntl, nt, tid);  // sdig doubles as the segment index until the rank
+  uint32_t dv[kSteps], pk[kSteps];
+  const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
-  for (int k = 0; k < kSteps; k++) dv[k] = digit_of<kFShift, kFBits>(sv[k]);
-  tile_rank<kFBits>(dv, vmask, cnt, dstart, pos);
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t k1 = ((vmask >> k) & 1u) ? seg_lookup(L, sdig, el0 + k * 64) : 0u;  // tile in group
+    dv[k] = sv[k] >> 24;
+    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (k1 << 8) | (sv[k] & 0xFFu);
+  }
+  uint32_t pos[kSteps];
+  tile_rank(dv, vmask, cnt, dstart, pos);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) stage[pos[k]] = ((uint64_t)sv[k] << 32) | rv[k];
+    if ((vmask >> k) & 1u) {
+      stage[pos[k]] = pk[k];
+      sdig[pos[k]] = (uint8_t)dv[k];
+    }
   __syncthreads();
-  const uint32_t ntile = (uint32_t)(t.e1 - t.e0);
-  for (uint32_t p = tid; p < ntile; p += kPThreads) {
-    const uint64_t pair = stage[p];
-    const uint32_t d = digit_of<kFShift, kFBits>((uint32_t)(pair >> 32));
-    a.out[gbase[d] + (p - dstart[d])] = pair;
+  for (uint32_t p = tid; p < nt; p += kPThreads) {
+    const uint32_t f = sdig[p];
+    a.out[gbase[f] + (p - dstart[f])] = stage[p];
   }
 }
 
-// First pair of every bucket b = (c << 8) | d, read off the pass-2 scan:
-// (c, d)'s first tile slot; empty slices point at the next slice's start.
-__global__ void k_bucket_bounds(const uint64_t* __restrict__ goff2, const uint32_t* __restrict__ tb,
-                                uint64_t nslots, uint64_t* __restrict__ bounds) {
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > kNumBuckets) return;
-  if (b == kNumBuckets) {
-    bounds[b] = goff2[nslots];
-    return;
-  }
-  const uint32_t c = (uint32_t)(b >> kFBits), d = (uint32_t)(b & ((1u << kFBits) - 1));
-  bounds[b] = goff2[((uint64_t)tb[c] << kFBits) + (uint64_t)d * (tb[c + 1] - tb[c])];
-}
-
+// ---------------------------------------------------------------- bucket ---
 struct BucketArgs {
-  const uint64_t* pairs;  // (s << 32) | record, grouped by bucket s >> 15
-  const uint64_t* bounds;
-  uint32_t* mwords;       // maxSignal
-  uint32_t* nwords;       // newSignal (nullable)
+  const uint32_t* in;      // pass-2 output
+  const uint32_t* goff2;   // [byte][chunk] run starts
+  const uint32_t* g2;      // device: number of chunks
+  const uint4* bdesc;      // per-bucket {lo, hi, c0, nch}
+  uint32_t kt;
+  const uint32_t* cfirst;  // 257
+  const uint32_t* cgov;
+  const uint32_t* trec;
+  uint32_t* mwords;        // maxSignal
+  uint32_t* nwords;        // newSignal (nullable)
   uint8_t* rec_new;
-  uint32_t* spill;        // buckets left for the direct-table kernel
+  uint32_t* spill;         // buckets left for the direct-table kernel
   uint32_t* nspill;
 };
 
-__device__ __forceinline__ uint32_t slot_of(uint32_t sl, int hbits) { return (sl * 2654435761u) >> (32 - hbits); }
+struct BucketRange {
+  uint32_t d, f, c0, nch, lo, hi;
+  const uint32_t* row;  // goff2 + f * G2 + c0: run start of each chunk of slice d
+};
 
-// The bucket's new bits: maxSignal = slice | new, newSignal |= new (this
-// block is the only writer of the bucket's 1024 words).
+// {lo, hi, c0, nch} of every bucket, from the pass-2 scan
+__global__ void k_bucket_desc(const uint32_t* __restrict__ goff2, const uint32_t* __restrict__ gcount,
+                              const uint32_t* __restrict__ cfirst, uint4* __restrict__ bdesc) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= kNumBuckets) return;
+  const uint32_t d = b >> 8, f = b & 255, c0 = cfirst[d], nch = cfirst[d + 1] - c0;
+  const uint32_t* row = goff2 + (uint64_t)f * *gcount + c0;
+  bdesc[b] = make_uint4(row[0], row[nch], c0, nch);
+}
+
+__device__ __forceinline__ BucketRange bucket_range(const BucketArgs& a, uint32_t b) {
+  BucketRange r;
+  const uint4 q = a.bdesc[b];
+  r.d = b >> 8;
+  r.f = b & 255;
+  r.lo = q.x;
+  r.hi = q.y;
+  r.c0 = q.z;
+  r.nch = q.w;
+  r.row = a.goff2 + (uint64_t)r.f * *a.g2 + r.c0;
+  return r;
+}
+
+// record of the pass-2 entry x at position o (chunk index within the slice: ci)
+__device__ __forceinline__ uint32_t entry_record(const BucketArgs& a, const BucketRange& r, uint32_t ci, uint32_t x) {
+  const uint32_t gov = a.cgov[r.c0 + ci];
+  const uint32_t t1 = (gov % a.kt) * kGroupTiles + ((x >> 8) & 255u);
+  return a.trec[t1] + (x & 255u);
+}
+
 __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
                                                const uint32_t* nbits, int tid, int nthreads) {
   uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
@@ -385,248 +547,487 @@ __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, 
   }
 }
 
-__device__ __forceinline__ bool hash_insert(uint32_t* hkey, uint32_t* hval, uint32_t hsize, int hbits,
-                                            uint32_t* nbits, uint32_t sl, uint32_t rec) {
-  uint32_t h = slot_of(sl, hbits);
-  for (uint32_t probes = 0; probes < hsize; probes++) {
-    const uint32_t k = atomicCAS(&hkey[h], ~0u, sl);
-    if (k == ~0u) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
-    if (k == ~0u || k == sl) {
+__device__ __forceinline__ uint32_t slot_of(uint32_t sl) { return (sl * 2654435761u) >> 20; }  // 12 bits
+
+__device__ __forceinline__ bool hash_insert(uint32_t* hkey, uint32_t* hval, uint32_t* nbits, uint32_t sl,
+                                            uint32_t rec) {
+  uint32_t h = slot_of(sl);
+  for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
+    const uint32_t k = atomicCAS(&hkey[h], kEmpty, sl);
+    if (k == kEmpty) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+    if (k == kEmpty || k == sl) {
       atomicMin(&hval[h], rec);
       return true;
     }
-    h = (h + 1) & (hsize - 1);
+    h = (h + 1) & (kHash - 1);
   }
-  return false;  // map full
+  return false;  // map (nearly) full: the bucket spills
 }
 
-__global__ __launch_bounds__(kBTThreads) void k_bucket_triage(BucketArgs a) {
+// record of the candidate entry x at position i of the bucket
+__device__ __forceinline__ uint32_t cand_record(const BucketArgs& a, const BucketRange& r, bool lds_runs,
+                                                const uint32_t* runs, const uint32_t* tb, uint32_t i, uint32_t x) {
+  uint32_t t0;
+  if (lds_runs) {
+    t0 = tb[sgd::seg_search(runs, 0, r.nch - 1, i)];
+  } else {
+    const uint32_t ci = (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
+    t0 = (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
+  }
+  return a.trec[t0 + ((x >> 8) & 255u)] + (x & 255u);
+}
+
+// One workgroup per bucket.  Per round of kBU entries per thread: the LDS
+// new-signal test; candidates are queued in LDS (wave-aggregated slots) and
+// then processed densely -- record lookup (chunk by LDS search, group's first
+// tile from LDS, one trec load), insert into the map.  The next round's
+// loads are in flight meanwhile.
+__global__ __launch_bounds__(kBThreads) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  __shared__ __attribute__((aligned(16))) uint32_t hkey[kHash];
-  __shared__ __attribute__((aligned(16))) uint32_t hval[kHash];
-  __shared__ uint32_t ncand;
+  __shared__ uint32_t hkey[kHash];
+  __shared__ uint32_t hval[kHash];
+  __shared__ uint32_t runs[kRunWin];  // run start of each chunk of the slice in this byte row
+  __shared__ uint32_t tb[kRunWin];    // first pass-1 tile of each chunk's group
+  __shared__ uint32_t qx[kQueue];
+  __shared__ uint32_t qi[kQueue];
+  __shared__ uint32_t qn;
   const uint32_t b = blockIdx.x;
-  const uint64_t lo = a.bounds[b], hi = a.bounds[b + 1];
-  if (lo == hi) return;  // no signal of this batch falls in the bucket
-  const int tid = threadIdx.x;
-  constexpr uint64_t kChunkPairs = (uint64_t)kBTThreads * kBU;
-  // the first chunk of pairs (all of a typical bucket) in flight at once
-  uint64_t p[kBU];
+  const BucketRange r = bucket_range(a, b);
+  if (r.lo >= r.hi) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr uint32_t kRound = kBThreads * kBU;
+  uint32_t x[kBU];
 #pragma unroll
   for (int u = 0; u < kBU; u++) {
-    const uint64_t i = lo + (uint64_t)u * kBTThreads + tid;
-    p[u] = i < hi ? a.pairs[i] : ~0ull;
+    const uint32_t i = r.lo + u * kBThreads + tid;
+    x[u] = i < r.hi ? a.in[i] : 0u;
   }
   const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
-  for (uint32_t i = tid; i < kBucketWords; i += kBTThreads) {
+  for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
     mslice[i] = mg[i];
     nbits[i] = 0;
   }
-  if (tid == 0) ncand = 0;
-  __syncthreads();
-  // candidates = signals not in maxSignal (fuzzer.go:666)
-  uint32_t cm = 0;
-#pragma unroll
-  for (int u = 0; u < kBU; u++) {
-    const uint32_t sl = (uint32_t)(p[u] >> 32) & (kBucketSig - 1);
-    if (p[u] != ~0ull && !((mslice[sl >> 5] >> (sl & 31)) & 1u)) cm |= 1u << u;
+  for (uint32_t i = tid; i < kHash; i += kBThreads) {
+    hkey[i] = kEmpty;
+    hval[i] = kEmpty;
   }
-  if (cm) atomicAdd(&ncand, (uint32_t)__popc(cm));
-  __syncthreads();
-  // map size: >= 2x the candidates (all could be distinct), capped
-  const uint64_t nc = hi - lo > kChunkPairs ? ~0ull : ncand;
-  int hbits = 6;
-  while ((1 << hbits) < kHash && (1ull << hbits) < 2 * nc) hbits++;
-  const uint32_t hsize = 1u << hbits;
-  for (uint32_t i = tid; i < hsize; i += kBTThreads) {
-    hkey[i] = ~0u;
-    hval[i] = ~0u;
-  }
-  __syncthreads();
-  // owner = min record per candidate signal
+  const bool lds_runs = r.nch <= kRunWin;
+  if (lds_runs)
+    for (uint32_t i = tid; i < r.nch; i += kBThreads) {
+      runs[i] = r.row[i];
+      tb[i] = (a.cgov[r.c0 + i] % a.kt) * kGroupTiles;
+    }
   bool ok = true;
-#pragma unroll
-  for (int u = 0; u < kBU; u++)
-    if ((cm >> u) & 1u) ok &= hash_insert(hkey, hval, hsize, hbits, nbits, (uint32_t)(p[u] >> 32) & (kBucketSig - 1),
-                                          (uint32_t)p[u]);
-  for (uint64_t base = lo + kChunkPairs; base < hi; base += kChunkPairs) {  // big buckets
-#pragma unroll
-    for (int u = 0; u < kBU; u++) {
-      const uint64_t i = base + (uint64_t)u * kBTThreads + tid;
-      p[u] = i < hi ? a.pairs[i] : ~0ull;
-    }
+  for (uint32_t base = r.lo;;) {
+    if (tid == 0) qn = 0;
+    __syncthreads();
+    uint32_t cm = 0;
 #pragma unroll
     for (int u = 0; u < kBU; u++) {
-      const uint32_t sl = (uint32_t)(p[u] >> 32) & (kBucketSig - 1);
-      if (p[u] != ~0ull && !((mslice[sl >> 5] >> (sl & 31)) & 1u))
-        ok &= hash_insert(hkey, hval, hsize, hbits, nbits, sl, (uint32_t)p[u]);
+      const uint32_t sl = x[u] >> 16;
+      if (base + u * kBThreads + tid < r.hi && !((mslice[sl >> 5] >> (sl & 31)) & 1u))  // fuzzer.go:666
+        cm |= 1u << u;
     }
+    // wave-aggregated queue slots
+    const uint32_t cnt = __popc(cm);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    uint32_t qb = 0;
+    if (lane == 63 && incl) qb = atomicAdd(&qn, incl);
+    uint32_t my = __shfl(qb, 63) + incl - cnt;
+#pragma unroll
+    for (int u = 0; u < kBU; u++)
+      if ((cm >> u) & 1u) {
+        const uint32_t i = base + u * kBThreads + tid;
+        if (my < kQueue) {
+          qx[my] = x[u];
+          qi[my] = i;
+        } else {  // queue overflow: this entry the sparse way
+          ok &= hash_insert(hkey, hval, nbits, x[u] >> 16, cand_record(a, r, lds_runs, runs, tb, i, x[u]));
+        }
+        my++;
+      }
+    const uint32_t next = base + kRound;
+#pragma unroll
+    for (int u = 0; u < kBU; u++) {
+      const uint32_t i = next + u * kBThreads + tid;
+      x[u] = i < r.hi ? a.in[i] : 0u;
+    }
+    __syncthreads();
+    const uint32_t qt = qn < kQueue ? qn : kQueue;
+    for (uint32_t q = tid; q < qt; q += 2 * kBThreads) {
+      const uint32_t q2 = q + kBThreads;
+      const uint32_t x0 = qx[q], x1 = q2 < qt ? qx[q2] : 0u;
+      const uint32_t r0 = cand_record(a, r, lds_runs, runs, tb, qi[q], x0);
+      const uint32_t r1 = q2 < qt ? cand_record(a, r, lds_runs, runs, tb, qi[q2], x1) : 0u;
+      ok &= hash_insert(hkey, hval, nbits, x0 >> 16, r0);
+      if (q2 < qt) ok &= hash_insert(hkey, hval, nbits, x1 >> 16, r1);
+    }
+    if (__syncthreads_or(!ok)) break;
+    if (next >= r.hi) break;
+    base = next;
   }
-  if (__syncthreads_or(!ok)) {  // redo with the direct table (no global writes yet)
+  if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
     if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
     return;
   }
   // a record is queued iff it owns some signal (fuzzer.go:678-690)
-  for (uint32_t i = tid; i < hsize; i += kBTThreads)
-    if (hkey[i] != ~0u) a.rec_new[hval[i]] = 1;
-  flush_new_bits(a, b, mslice, nbits, tid, kBTThreads);
+  for (uint32_t i = tid; i < kHash; i += kBThreads)
+    if (hkey[i] != kEmpty) a.rec_new[hval[i]] = 1;
+  flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
 }
 
-// Buckets with too many distinct candidates: direct first-owner table in LDS.
-__global__ __launch_bounds__(kPThreads) void k_bucket_triage_direct(BucketArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t owner[kBucketSig];  // 128 KiB
+// Buckets with too many distinct candidates: a direct first-owner table over
+// a quarter of the bucket at a time (16384 signals, 64 KiB of LDS).
+__global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
+  constexpr uint32_t kQ = 16384;
+  __shared__ uint32_t owner[kQ];
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
+  __shared__ uint32_t runs[kRunWin];
+  __shared__ uint32_t tb[kRunWin];
   const int tid = threadIdx.x;
   const uint32_t nsp = *a.nspill;
   for (uint32_t j = blockIdx.x; j < nsp; j += gridDim.x) {
     const uint32_t b = a.spill[j];
-    const uint64_t lo = a.bounds[b], hi = a.bounds[b + 1];
+    const BucketRange r = bucket_range(a, b);
     const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
-    for (uint32_t i = tid; i < kBucketWords; i += kPThreads) {
+    for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
       mslice[i] = mg[i];
       nbits[i] = 0;
     }
-    uint4* o4 = reinterpret_cast<uint4*>(owner);
-    for (uint32_t i = tid; i < kBucketSig / 4; i += kPThreads) o4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    __syncthreads();
-    for (uint64_t i = lo + tid; i < hi; i += kPThreads) {
-      const uint64_t p = a.pairs[i];
-      const uint32_t sl = (uint32_t)(p >> 32) & (kBucketSig - 1);
-      if ((mslice[sl >> 5] >> (sl & 31)) & 1u) continue;
-      atomicMin(&owner[sl], (uint32_t)p);
-      atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+    const bool lds_runs = r.nch <= kRunWin;
+    if (lds_runs)
+      for (uint32_t i = tid; i < r.nch; i += kBThreads) {
+        runs[i] = r.row[i];
+        tb[i] = (a.cgov[r.c0 + i] % a.kt) * kGroupTiles;
+      }
+    for (uint32_t q = 0; q < 65536 / kQ; q++) {
+      for (uint32_t i = tid; i < kQ; i += kBThreads) owner[i] = kEmpty;
+      __syncthreads();
+      for (uint32_t i = r.lo + tid; i < r.hi; i += kBThreads) {
+        const uint32_t x = a.in[i];
+        const uint32_t sl = x >> 16;
+        if (sl / kQ != q || ((mslice[sl >> 5] >> (sl & 31)) & 1u)) continue;
+        atomicMin(&owner[sl % kQ], cand_record(a, r, lds_runs, runs, tb, i, x));
+        atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < kQ; i += kBThreads)
+        if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
+      __syncthreads();
     }
-    __syncthreads();
-    for (uint32_t i = tid; i < kBucketSig; i += kPThreads)
-      if (owner[i] != ~0u) a.rec_new[owner[i]] = 1;
-    flush_new_bits(a, b, mslice, nbits, tid, kPThreads);
+    flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
     __syncthreads();
   }
 }
 
-__global__ void k_tile_rec_pt(const uint64_t* __restrict__ off, uint64_t nseg, uint64_t n, uint64_t ntiles,
-                              uint32_t* __restrict__ tile_rec) {
-  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > ntiles) return;
-  uint64_t e = t * kPT;
-  if (e >= n) e = n - 1;
-  tile_rec[t] = (uint32_t)sgd::seg_search(off, 0, nseg - 1, e);
+// ------------------------------------------------------------------ scan ---
+// Exclusive scan of u32 counts into u32 offsets (totals < 2^32), out[n] = total.
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 16;
+constexpr uint32_t kScanTile = kScanThreads * kScanPer;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  if (tid < 64) {
+    const uint32_t x = tid < (int)(blockDim.x >> 6) ? wsum[tid] : 0u;
+    uint32_t wi = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(wi, o);
+      if (lane >= o) wi += y;
+    }
+    if (tid < (int)(blockDim.x >> 6)) wsum[tid] = wi - x;
+    if (tid == 63) *total = wi;
+  }
+  __syncthreads();
+  return wsum[w] + incl - v;
 }
 
+// n_dev (nullable): the element count is (*n_dev) * mul, <= the host bound n.
+__device__ __forceinline__ uint64_t scan_n(uint64_t n, const uint32_t* n_dev, uint32_t mul) {
+  return n_dev ? (uint64_t)(*n_dev) * mul : n;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan32_reduce(const uint32_t* __restrict__ in, uint64_t n,
+                                                                const uint32_t* __restrict__ n_dev, uint32_t mul,
+                                                                uint32_t* __restrict__ sums) {
+  __shared__ uint32_t wsum[16];
+  n = scan_n(n, n_dev, mul);
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  uint32_t s = 0;
+  if (base < n) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      const uint64_t i = base + (uint64_t)k * kScanThreads + threadIdx.x;
+      s += i < n ? in[i] : 0u;
+    }
+  }
+  for (int o = 32; o; o >>= 1) s += __shfl_down(s, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kScanThreads / 64; w++) t += wsum[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// in place, one block: exclusive scan of nb block sums
+__global__ __launch_bounds__(kScanThreads) void k_scan32_top(uint32_t* __restrict__ sums, uint64_t nb) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t tot;
+  uint32_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += kScanThreads) {
+    const uint64_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? sums[i] : 0u;
+    const uint32_t ex = block_excl_scan(v, wsum, &tot);
+    if (i < nb) sums[i] = carry + ex;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan32_apply(const uint32_t* __restrict__ in, uint64_t n,
+                                                               const uint32_t* __restrict__ n_dev, uint32_t mul,
+                                                               const uint32_t* __restrict__ sums,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t tot;
+  n = scan_n(n, n_dev, mul);
+  const uint64_t b_last = n ? (n - 1) / kScanTile : 0;
+  if (blockIdx.x > b_last) return;
+  // each thread owns kScanPer consecutive counters
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  const bool full = base + kScanPer <= n;  // in / out are 256-B aligned: 16-B accesses
+  uint32_t v[kScanPer];
+  uint32_t s = 0;
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(in + base + k);
+      v[k] = q.x;
+      v[k + 1] = q.y;
+      v[k + 2] = q.z;
+      v[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) v[k] = base + k < n ? in[base + k] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) s += v[k];
+  uint32_t run = sums[blockIdx.x] + block_excl_scan(s, wsum, &tot);
+  uint32_t o[kScanPer];
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) {
+    o[k] = run;
+    run += v[k];
+  }
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k += 4)
+      *reinterpret_cast<uint4*>(out + base + k) = make_uint4(o[k], o[k + 1], o[k + 2], o[k + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++)
+      if (base + k < n) out[base + k] = o[k];
+  }
+  if (blockIdx.x == b_last && threadIdx.x == kScanThreads - 1) out[n] = run;
+}
+
+static size_t scan32_ws(uint64_t n) { return (((n + kScanTile - 1) / kScanTile) * 4 + 255) & ~size_t(255); }
+
+// n = host bound; with n_dev the count is (*n_dev) * mul (<= n)
+static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* scratch,
+                  const uint32_t* n_dev = nullptr, uint32_t mul = 1) {
+  ScopedTimer tm(ctx, "scan");
+  const uint64_t nb = (n + kScanTile - 1) / kScanTile;
+  if (nb == 0) {
+    SG_HIP(hipMemsetAsync(out, 0, 4, ctx->stream));
+    return SG_OK;
+  }
+  hipLaunchKernelGGL(k_scan32_reduce, dim3((uint32_t)nb), dim3(kScanThreads), 0, ctx->stream, in, n, n_dev, mul,
+                     scratch);
+  hipLaunchKernelGGL(k_scan32_top, dim3(1), dim3(kScanThreads), 0, ctx->stream, scratch, nb);
+  hipLaunchKernelGGL(k_scan32_apply, dim3((uint32_t)nb), dim3(kScanThreads), 0, ctx->stream, in, n, n_dev, mul,
+                     scratch, out);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+// ------------------------------------------------------------------ host ---
 struct BucketPlan {
-  uint64_t nt, g2, nslots;
+  uint64_t n, nrec, nA, nB, T, kt, ng, gmax;
   WsPlan p;
-  size_t oS, oR, oB, oH1, oO1, oTR, oCS, oTB, oH2, oO2, oBB, oSP, scan_off;
-  explicit BucketPlan(uint64_t n) {
-    nt = (n + kPT - 1) / kPT;
-    g2 = nt + kNumCoarse;  // upper bound on pass-2 tiles
-    nslots = g2 << kFBits;
-    oS = p.add(n * 4);
-    oR = p.add(n * 4);
-    oB = p.add(n * 8);
-    oH1 = p.add((uint64_t)kNumCoarse * nt * 4);
-    oO1 = p.add(((uint64_t)kNumCoarse * nt + 1) * 8);
-    oTR = p.add((nt + 1) * 4);
-    oCS = p.add((kNumCoarse + 1) * 8);
-    oTB = p.add((kNumCoarse + 1) * 4);
-    oH2 = p.add(nslots * 4);
-    oO2 = p.add((nslots + 1) * 8);
-    oBB = p.add(((uint64_t)kNumBuckets + 1) * 8);
+  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oSC;
+  BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
+    nA = (n + kPT - 1) / kPT;
+    nB = nrec ? (nrec - 1) / kRecCap : 0;
+    T = nA + nB;
+    kt = (T + kGroupTiles - 1) / kGroupTiles;
+    ng = 256 * kt;
+    gmax = ng + nA;  // sum over groups of ceil(size / kPT) <= ng + n / kPT
+    oTS = p.add((T + 1) * 4);
+    oTR = p.add((T + 1) * 4);
+    oH1 = p.add(256 * T * 4);
+    oO1 = p.add((256 * T + 1) * 4);
+    oV1 = p.add(n * 4);
+    oNC = p.add(ng * 4);
+    oCB = p.add((ng + 1) * 4);
+    oCS = p.add((gmax + 1) * 4);
+    oCG = p.add((gmax + 1) * 4);
+    oCF = p.add(257 * 4);
+    oCD = p.add(gmax * 16);
+    oBD = p.add((uint64_t)kNumBuckets * 16);
+    oH2 = p.add(256 * gmax * 4);
+    oO2 = p.add((256 * gmax + 1) * 4);
+    oV2 = p.add(n * 4);
     oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
-    scan_off = p.total;
-  }
-  size_t bytes() const {
-    const uint64_t m = (uint64_t)kNumCoarse * nt > nslots ? (uint64_t)kNumCoarse * nt : nslots;
-    return p.total + scan_ws_bytes(m);
+    oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
   }
 };
 
-size_t bucket_ws_bytes(uint64_t n) { return BucketPlan(n).bytes(); }
+size_t bucket_ws_bytes(uint64_t n, uint64_t nrec) { return BucketPlan(n, nrec).p.total; }
 
 // Flags-only triage of a device-resident batch (ctx lock held).
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
                   uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
-  if (nrec >= 0xFFFFFFFFull) {
-    set_error("bucket triage: record index must fit 32 bits");
+  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
     return SG_EINVAL;
   }
   if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
   if (n == 0) return SG_OK;
-  if ((n + kPT - 1) / kPT + kNumCoarse >= 0xFFFFFFFFull) {
+  if (nrec == 0) {
+    set_error("bucket triage: signal entries without records");
+    return SG_EINVAL;
+  }
+  const BucketPlan bp(n, nrec);
+  if (256 * bp.gmax >= 0xFFFFFFFFull) {
     set_error("bucket triage: batch too large");
     return SG_EINVAL;
   }
-  const BucketPlan bp(n);
-  int rc = ws_reserve(ctx, bp.bytes());
+  int rc = ws_reserve(ctx, bp.p.total);
   if (rc) return rc;
-  const uint64_t nt = bp.nt;
-  P1Args a1{};
-  a1.vals = d_vals;
-  a1.n = n;
-  a1.ntiles = nt;
-  a1.rec_off = d_off;
-  a1.tile_rec = (uint32_t*)ws_at(ctx, bp.oTR);
-  a1.hist = (uint32_t*)ws_at(ctx, bp.oH1);
-  a1.goff = (uint64_t*)ws_at(ctx, bp.oO1);
-  a1.s_out = (uint32_t*)ws_at(ctx, bp.oS);
-  a1.r_out = (uint32_t*)ws_at(ctx, bp.oR);
-  hipLaunchKernelGGL(k_tile_rec_pt, dim3(div_up(nt + 1, 256)), dim3(256), 0, ctx->stream, d_off, nrec, n, nt,
-                     (uint32_t*)a1.tile_rec);
+  uint32_t* tstart = (uint32_t*)ws_at(ctx, bp.oTS);
+  uint32_t* trec = (uint32_t*)ws_at(ctx, bp.oTR);
+  uint32_t* hist1 = (uint32_t*)ws_at(ctx, bp.oH1);
+  uint32_t* goff1 = (uint32_t*)ws_at(ctx, bp.oO1);
+  uint32_t* v1 = (uint32_t*)ws_at(ctx, bp.oV1);
+  uint32_t* nch = (uint32_t*)ws_at(ctx, bp.oNC);
+  uint32_t* cbase = (uint32_t*)ws_at(ctx, bp.oCB);
+  uint32_t* cstart = (uint32_t*)ws_at(ctx, bp.oCS);
+  uint32_t* cgov = (uint32_t*)ws_at(ctx, bp.oCG);
+  uint32_t* cfirst = (uint32_t*)ws_at(ctx, bp.oCF);
+  uint4* cdesc = (uint4*)ws_at(ctx, bp.oCD);
+  uint4* bdesc = (uint4*)ws_at(ctx, bp.oBD);
+  uint32_t* hist2 = (uint32_t*)ws_at(ctx, bp.oH2);
+  uint32_t* goff2 = (uint32_t*)ws_at(ctx, bp.oO2);
+  uint32_t* v2 = (uint32_t*)ws_at(ctx, bp.oV2);
+  uint32_t* nspill = (uint32_t*)ws_at(ctx, bp.oSP);
+  uint32_t* scr = (uint32_t*)ws_at(ctx, bp.oSC);
+  const uint32_t T = (uint32_t)bp.T, G = (uint32_t)bp.gmax;
+  const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
+
+  // pass-1 tiles
+  Cuts c1{};
+  c1.nA = bp.nA;
+  c1.step = kPT;
+  c1.nB = bp.nB;
+  c1.n = n;
+  c1.rec_off = d_off;
+  c1.nrec = nrec;
+  c1.start = tstart;
+  c1.aux = trec;
+  hipLaunchKernelGGL(k_cuts, dim3(div_up(bp.T + 1, 256)), dim3(256), 0, ctx->stream, c1);
   {
-    ScopedTimer tm(ctx, "part1_hist");
-    hipLaunchKernelGGL(k_p1_hist, dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream, a1);
+    ScopedTimer tm(ctx, "p1_hist");
+    if (((uintptr_t)d_vals & 15) == 0)
+      hipLaunchKernelGGL(k_hist_top<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+                         (const uint32_t*)tstart, (const uint4*)nullptr, (const uint32_t*)nullptr, hist1);
+    else
+      hipLaunchKernelGGL(k_hist_top<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+                         (const uint32_t*)tstart, (const uint4*)nullptr, (const uint32_t*)nullptr, hist1);
   }
-  rc = scan_counts(ctx, a1.hist, (uint64_t*)a1.goff, (uint64_t)kNumCoarse * nt, bp.scan_off);
+  rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
+  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, v1};
   {
-    ScopedTimer tm(ctx, "part1_scatter");
-    hipLaunchKernelGGL(k_p1_scatter, dim3((uint32_t)nt), dim3(kPThreads), 0, ctx->stream, a1);
+    ScopedTimer tm(ctx, "p1_scatter");
+    hipLaunchKernelGGL(k_p1_scatter, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
   }
-  P2Args a2{};
-  a2.s_in = a1.s_out;
-  a2.r_in = a1.r_out;
-  a2.cs = (uint64_t*)ws_at(ctx, bp.oCS);
-  a2.tb = (uint32_t*)ws_at(ctx, bp.oTB);
-  a2.hist = (uint32_t*)ws_at(ctx, bp.oH2);
-  a2.goff = (uint64_t*)ws_at(ctx, bp.oO2);
-  a2.out = (uint64_t*)ws_at(ctx, bp.oB);
-  hipLaunchKernelGGL(k_p2_tiles, dim3(1), dim3(kNumCoarse), 0, ctx->stream, a1.goff, nt, n, (uint64_t*)a2.cs,
-                     (uint32_t*)a2.tb);
-  {
-    ScopedTimer tm(ctx, "part2_hist");
-    hipLaunchKernelGGL(k_p2_hist, dim3((uint32_t)bp.g2), dim3(kPThreads), 0, ctx->stream, a2);
-  }
-  rc = scan_counts(ctx, a2.hist, (uint64_t*)a2.goff, bp.nslots, bp.scan_off);
+  // pass-2 chunks
+  hipLaunchKernelGGL(k_group_chunks, dim3(div_up(bp.ng, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)goff1,
+                     bp.T, bp.kt, bp.ng, (uint32_t)n, nch);
+  rc = scan32(ctx, nch, cbase, bp.ng, scr);
   if (rc) return rc;
+  hipLaunchKernelGGL(k_chunk_list, dim3(div_up((bp.ng > bp.gmax ? bp.ng : bp.gmax) + 1, 256)), dim3(256), 0,
+                     ctx->stream, (const uint32_t*)goff1, bp.T, bp.kt, bp.ng, (uint32_t)n, (const uint32_t*)cbase,
+                     bp.gmax, cstart, cgov, cfirst);
+  hipLaunchKernelGGL(k_chunk_desc, dim3(div_up(bp.gmax, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)cstart,
+                     (const uint32_t*)cgov, gcount, bp.gmax, cdesc);
   {
-    ScopedTimer tm(ctx, "part2_scatter");
-    hipLaunchKernelGGL(k_p2_scatter, dim3((uint32_t)bp.g2), dim3(kPThreads), 0, ctx->stream, a2);
+    ScopedTimer tm(ctx, "p2_hist");
+    hipLaunchKernelGGL(k_hist_top<true>, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
+                       (const uint32_t*)nullptr, (const uint4*)cdesc, gcount, hist2);
+  }
+  rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
+  if (rc) return rc;
+  P2Args a2{v1, cdesc, gcount, goff1, T, (uint32_t)bp.kt, (uint32_t)n, goff2, v2};
+  {
+    ScopedTimer tm(ctx, "p2_scatter");
+    hipLaunchKernelGGL(k_p2_scatter, dim3(G), dim3(kPThreads), 0, ctx->stream, a2);
   }
   BucketArgs ba{};
-  ba.pairs = a2.out;
-  ba.bounds = (uint64_t*)ws_at(ctx, bp.oBB);
+  ba.in = v2;
+  ba.goff2 = goff2;
+  ba.g2 = gcount;
+  ba.bdesc = bdesc;
+  ba.kt = (uint32_t)bp.kt;
+  ba.cfirst = cfirst;
+  ba.cgov = cgov;
+  ba.trec = trec;
   ba.mwords = mwords;
   ba.nwords = nwords;
   ba.rec_new = d_rec_new;
-  ba.nspill = (uint32_t*)ws_at(ctx, bp.oSP);
-  ba.spill = ba.nspill + 1;
-  SG_HIP(hipMemsetAsync(ba.nspill, 0, 4, ctx->stream));
-  {
-    ScopedTimer tm(ctx, "bucket_bounds");
-    hipLaunchKernelGGL(k_bucket_bounds, dim3(div_up((uint64_t)kNumBuckets + 1, 256)), dim3(256), 0, ctx->stream,
-                       a2.goff, a2.tb, bp.nslots, (uint64_t*)ba.bounds);
-  }
+  ba.nspill = nspill;
+  ba.spill = nspill + 1;
+  SG_HIP(hipMemsetAsync(nspill, 0, 4, ctx->stream));
+  hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
+                     gcount, (const uint32_t*)cfirst, bdesc);
   {
     ScopedTimer tm(ctx, "bucket_triage");
-    hipLaunchKernelGGL(k_bucket_triage, dim3(kNumBuckets), dim3(kBTThreads), 0, ctx->stream, ba);
+    hipLaunchKernelGGL(k_bucket, dim3(kNumBuckets), dim3(kBThreads), 0, ctx->stream, ba);
   }
   {
     ScopedTimer tm(ctx, "bucket_spill");
-    hipLaunchKernelGGL(k_bucket_triage_direct, dim3(512), dim3(kPThreads), 0, ctx->stream, ba);
+    hipLaunchKernelGGL(k_bucket_direct, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
   }
   SG_HIP(hipGetLastError());
+  if (getenv("SG_DEBUG_PART")) {  // diagnostics: chunk and spill counts (syncs)
+    uint32_t g = 0, sp = 0;
+    SG_HIP(hipMemcpyAsync(&g, gcount, 4, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipMemcpyAsync(&sp, nspill, 4, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    fprintf(stderr, "sg part: n=%llu nrec=%llu tiles=%llu chunks=%u (bound %llu) spilled_buckets=%u\n",
+            (unsigned long long)n, (unsigned long long)nrec, (unsigned long long)bp.T, g,
+            (unsigned long long)bp.gmax, sp);
+  }
   return SG_OK;
 }
 

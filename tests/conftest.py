@@ -11,6 +11,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and runs libsyzsig.so kernels")
+    config.addinivalue_line("markers", "slow: a larger case (tens of millions of entries)")
 
 
 @pytest.fixture(scope="session")

@@ -304,6 +304,60 @@ def test_triage_edge_cases(C):
     assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
 
 
+def test_triage_partition_geometry(C):
+    """Inputs aimed at the partitioned path's tables (sg_bucket.hip): tiles cut
+    by the 256-record cap, runs of >= 256 empty records (coinciding cuts),
+    record counts around multiples of 256, one slice holding the whole batch,
+    and a 2^16-signal bucket with more distinct candidates than its LDS map."""
+    P = TwoPaths(C)
+    om, on = O.OSet(), O.OSet()
+    rng = np.random.default_rng(113)
+
+    def run(vals, lens):
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        assert int(off[-1]) == vals.size
+        _check_triage(P, (om, on), vals.astype(np.uint32), off)
+
+    # tiny records: every tile hits the record cap long before 8192 entries
+    lens = rng.integers(0, 4, size=40000)
+    run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
+    # >= 256 consecutive empty records, at and around cap boundaries
+    for nrec in (255, 256, 257, 511, 512, 513, 1024):
+        lens = np.zeros(nrec, np.int64)
+        lens[rng.integers(0, nrec, size=5)] = rng.integers(1, 3000, size=5)
+        lens[-1] += 7
+        run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
+    lens = np.concatenate([np.full(300, 0), [9000], np.full(700, 0), [20000], np.full(256, 0), [3]])
+    run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
+    # one top byte (slice) for everything: long runs, many chunks in one slice
+    n = 3_000_000
+    vals = (0x5A000000 | rng.integers(0, 1 << 24, size=n)).astype(np.uint64)
+    lens = np.diff(np.concatenate([[0], np.sort(rng.integers(0, n, size=2999)), [n]]))
+    run(vals, lens)
+    # a bucket with ~20k distinct candidates (overflows the 4096-slot map), repeated
+    base = 0x3C7A0000
+    vals = base + rng.permutation(65536)[:20000].astype(np.uint64)
+    vals = np.concatenate([vals, vals[::-1], rng.integers(0, 1 << 32, size=5000, dtype=np.uint64)])
+    lens = np.diff(np.concatenate([[0], np.sort(rng.integers(0, vals.size, size=99)), [vals.size]]))
+    run(vals, lens)
+    m, nn = P.exports()
+    assert np.array_equal(m, om.export()) and np.array_equal(nn, on.export())
+
+
+@pytest.mark.slow
+def test_triage_slice_over_lds_run_window(C):
+    """A slice with more pass-2 chunks than the bucket kernel keeps in LDS
+    (> 2048 chunks: > 16.7M entries sharing a top byte): the global run-search
+    branch."""
+    P = TwoPaths(C)
+    om, on = O.OSet(), O.OSet()
+    rng = np.random.default_rng(114)
+    n = 18_000_000
+    vals = (0xC3000000 | rng.integers(0, 1 << 24, size=n)).astype(np.uint32)
+    off = np.concatenate([[0], np.sort(rng.integers(0, n, size=40000)), [n]]).astype(np.uint64)
+    _check_triage(P, (om, on), vals, off)
+
+
 def test_triage_flags_only_matches(C):
     rng = np.random.default_rng(111)
     ms, om = C.SignalSet(), O.OSet()
