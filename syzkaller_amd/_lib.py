@@ -9,7 +9,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsyzsig.so")
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsyzsig.so")  # override: diagnostics builds
 
 SG_OK = 0
 SG_EINVAL = -1

@@ -35,6 +35,12 @@
 // random HBM access, no 16 GiB owner table.
 #include "sg_internal.h"
 
+#include <algorithm>
+
+#ifndef SG_EXP
+#define SG_EXP 0  // diagnostics builds only
+#endif
+
 namespace sg {
 
 constexpr int kPT = 8192;                    // entries per partition tile / chunk
@@ -50,7 +56,7 @@ constexpr uint32_t kGroupTiles = 240;
 constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
 constexpr int kBThreads = 512;
-constexpr int kBU = 16;                      // entries per thread per round in the bucket kernel
+constexpr int kBU = 8;                       // entries per thread per round in the bucket kernel
 constexpr uint32_t kHash = 4096;             // candidate map slots per bucket
 constexpr uint32_t kRunWin = 1024;           // chunk run starts kept in LDS per bucket
 constexpr uint32_t kQueue = 2048;            // candidates queued per round (dense processing)
@@ -497,6 +503,9 @@ struct BucketArgs {
   uint8_t* rec_new;
   uint32_t* spill;         // buckets left for the direct-table kernel
   uint32_t* nspill;
+  uint32_t* ticket;        // persistent bucket kernel: buckets handed out past the grid
+  uint64_t* dbg;           // diagnostics (k_bucket<true>): per block {start, end, buckets, rounds, 4 phase cycle sums}
+  uint8_t* kflag;          // owner keys (tile * 256 + record in tile) that own some signal
 };
 
 struct BucketRange {
@@ -564,9 +573,14 @@ __device__ __forceinline__ bool hash_insert(uint32_t* hkey, uint32_t* hval, uint
   return false;  // map (nearly) full: the bucket spills
 }
 
-// record of the candidate entry x at position i of the bucket
-__device__ __forceinline__ uint32_t cand_record(const BucketArgs& a, const BucketRange& r, bool lds_runs,
-                                                const uint32_t* runs, const uint32_t* tb, uint32_t i, uint32_t x) {
+// Owner key of the candidate entry x at position i of the bucket:
+// key = pass-1 tile * 256 + record in tile.  Records only grow with the tile
+// and, inside a tile, with the in-tile index, so min(key) names the same
+// record as min(record) (a record cut by a tile boundary has two keys that
+// both map back to it); the map works on keys and the record,
+// trec[key >> 8] + (key & 255), is looked up once per owner at the end.
+__device__ __forceinline__ uint32_t cand_key(const BucketArgs& a, const BucketRange& r, bool lds_runs,
+                                             const uint32_t* runs, const uint32_t* tb, uint32_t i, uint32_t x) {
   uint32_t t0;
   if (lds_runs) {
     t0 = tb[sgd::seg_search(runs, 0, r.nch - 1, i)];
@@ -574,112 +588,404 @@ __device__ __forceinline__ uint32_t cand_record(const BucketArgs& a, const Bucke
     const uint32_t ci = (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
     t0 = (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
   }
-  return a.trec[t0 + ((x >> 8) & 255u)] + (x & 255u);
+  return ((t0 + ((x >> 8) & 255u)) << 8) | (x & 255u);
 }
 
-// One workgroup per bucket.  Per round of kBU entries per thread: the LDS
-// new-signal test; candidates are queued in LDS (wave-aggregated slots) and
-// then processed densely -- record lookup (chunk by LDS search, group's first
-// tile from LDS, one trec load), insert into the map.  The next round's
-// loads are in flight meanwhile.
-__global__ __launch_bounds__(kBThreads) void k_bucket(BucketArgs a) {
+__device__ __forceinline__ uint32_t key_record(const BucketArgs& a, uint32_t key) {
+  return a.trec[key >> 8] + (key & 255u);
+}
+
+// Persistent: each workgroup takes buckets one after another (the first one
+// by its index, then by ticket) and runs through them as one stream of
+// rounds of kBU entries per thread.  Per round: the LDS new-signal test,
+// candidates queued in LDS (wave-aggregated slots) and processed densely --
+// record lookup (chunk by LDS search, the group's first tile from LDS, one
+// trec load), insert into the map.  While a round is processed the next one
+// is in flight -- the same bucket's next round, or the next bucket's first
+// round together with its maxSignal slice and chunk tables.  The ticket after
+// that is fetched a bucket ahead, so no dependent load is exposed.
+struct BucketPre {  // a bucket's first loads, held in registers
+  uint32_t msw[kBucketWords / kBThreads];
+  uint32_t rw[kRunWin / kBThreads];  // its first window of chunk run starts ...
+  uint32_t tw[kRunWin / kBThreads];  // ... and their groups
+  uint32_t lim;                      // first position past that window
+};
+
+// Rounds start 4-aligned (the bucket start rounded down): thread t holds
+// entries base + 16t .. +15 as four 16-B loads (immediate offsets, one
+// address); entry i is live iff lo <= i < hi.  The pass-2 buffer is padded,
+// so the quad reads past hi stay in bounds.
+__device__ __forceinline__ uint32_t round_pos(uint32_t base, int u) { return base + threadIdx.x * kBU + u; }
+
+__device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t base, uint32_t hi,
+                                                  uint32_t (&x)[kBU]) {
+  const uint4* p = reinterpret_cast<const uint4*>(a.in + base) + threadIdx.x * (kBU / 4);
+#pragma unroll
+  for (int j = 0; j < kBU / 4; j++) {
+    const uint4 v = round_pos(base, 4 * j) < hi ? p[j] : make_uint4(0, 0, 0, 0);
+    x[4 * j] = v.x;
+    x[4 * j + 1] = v.y;
+    x[4 * j + 2] = v.z;
+    x[4 * j + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, uint4 q, uint32_t G2,
+                                                BucketPre& P) {
+  static_assert(kBucketWords / kBThreads == 4, "one uint4 of the slice per thread");
+  const uint4 m = reinterpret_cast<const uint4*>(a.mwords + (uint64_t)b * kBucketWords)[threadIdx.x];
+  P.msw[0] = m.x;
+  P.msw[1] = m.y;
+  P.msw[2] = m.z;
+  P.msw[3] = m.w;
+  const uint32_t* row = a.goff2 + (uint64_t)(b & 255) * G2 + q.z;
+#pragma unroll
+  for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+    const uint32_t i = j * kBThreads + threadIdx.x;
+    const bool ok = i < q.w;
+    P.rw[j] = ok ? row[i] : 0u;
+    P.tw[j] = ok ? a.cgov[q.z + i] : 0u;
+  }
+  P.lim = q.w > kRunWin ? row[kRunWin] : q.y;
+}
+
+// thread 0: the next non-empty bucket by ticket (kNumBuckets: none)
+__device__ __forceinline__ uint32_t bucket_ticket(const BucketArgs& a, uint4* q) {
+  for (;;) {
+    const uint32_t nb = gridDim.x + atomicAdd(a.ticket, 1u);
+    if (nb >= kNumBuckets) return kNumBuckets;
+    const uint4 d = a.bdesc[nb];
+    if (d.x < d.y) {
+      *q = d;
+      return nb;
+    }
+  }
+}
+
+constexpr unsigned long long kEmpty64 = ~0ull;
+
+// Map slot = signal (high word) | owner key (low word).  A first insert is one
+// CAS; a repeat of a signal lowers the key with a u64 min (equal high words).
+__device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* nbits, uint32_t sl, uint32_t key) {
+  const unsigned long long mine = ((unsigned long long)sl << 32) | key;
+  uint32_t h = slot_of(sl);
+  for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
+    const unsigned long long old = atomicCAS(&ht[h], kEmpty64, mine);
+    if (old == kEmpty64) {
+      atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+      return true;
+    }
+    if ((uint32_t)(old >> 32) == sl) {
+      if ((uint32_t)old > key) atomicMin(&ht[h], mine);
+      return true;
+    }
+    h = (h + 1) & (kHash - 1);
+  }
+  return false;  // map (nearly) full: the bucket spills
+}
+
+// The chunk tables of a bucket are held in LDS as a sliding window of up to
+// kRunWin chunks [wc, wc + wn), covering positions [runs[0], wlim); a hot
+// slice has thousands of chunks, and the window moves with the rounds.
+// Positions past the window (rounds spanning more than kRunWin chunks) fall
+// back to a search in global memory.
+struct RunWindow {
+  uint32_t wc, wn, wlim;
+};
+
+// chunk (index within the slice) holding bucket position i
+__device__ __forceinline__ uint32_t chunk_of(const BucketRange& r, const RunWindow& W, const uint32_t* runs,
+                                             uint32_t i) {
+  if (i < W.wlim && i >= runs[0]) return W.wc + (uint32_t)sgd::seg_search(runs, 0, W.wn - 1, i);
+  return (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
+}
+
+__device__ __forceinline__ uint32_t chunk_tile(const BucketArgs& a, const BucketRange& r, const RunWindow& W,
+                                               const uint32_t* tb, uint32_t ci) {
+  return ci - W.wc < W.wn ? tb[ci - W.wc] : (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
+}
+
+template <bool kDbg>
+__global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  __shared__ uint32_t hkey[kHash];
-  __shared__ uint32_t hval[kHash];
+  __shared__ unsigned long long ht[kHash];
   __shared__ uint32_t runs[kRunWin];  // run start of each chunk of the slice in this byte row
   __shared__ uint32_t tb[kRunWin];    // first pass-1 tile of each chunk's group
-  __shared__ uint32_t qx[kQueue];
-  __shared__ uint32_t qi[kQueue];
+  __shared__ uint32_t qx[kQueue];     // candidate entries
+  __shared__ uint32_t qk[kQueue];     // their owner keys
   __shared__ uint32_t qn;
-  const uint32_t b = blockIdx.x;
-  const BucketRange r = bucket_range(a, b);
-  if (r.lo >= r.hi) return;
+  __shared__ uint32_t sh_b[2];
+  __shared__ uint4 sh_q[2];
+  __shared__ uint32_t sh_w[2];
+  __shared__ uint32_t slot_c[kBThreads];  // chunk holding each thread's first entry this round ...
+  __shared__ uint32_t slot_t[kBThreads];  // ... valid iff slot_t == this round's tag
+  __shared__ uint32_t sh_ca;
   const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t G2 = *a.g2;
   constexpr uint32_t kRound = kBThreads * kBU;
-  uint32_t x[kBU];
-#pragma unroll
-  for (int u = 0; u < kBU; u++) {
-    const uint32_t i = r.lo + u * kBThreads + tid;
-    x[u] = i < r.hi ? a.in[i] : 0u;
+  // diagnostics (kDbg): block span, buckets, rounds, cycles per phase as wave 0 sees them
+  const uint64_t t_start = kDbg ? wall_clock64() : 0;
+  uint64_t n_buckets = 0, n_rounds = 0;
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};  // install, test+queue, dense, flush | queue: test, search+enqueue, rest
+  uint64_t tk = kDbg ? clock64() : 0;
+  for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
+  for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
+  slot_t[tid] = kEmpty;
+  uint32_t rtag = 0;  // round tag of the slot map
+  if (tid == 0) {  // this block's first two buckets
+    uint4 q0 = a.bdesc[blockIdx.x < kNumBuckets ? blockIdx.x : 0], q1 = make_uint4(0, 0, 0, 0);
+    uint32_t b0 = blockIdx.x;
+    if (b0 >= kNumBuckets || q0.x >= q0.y) b0 = bucket_ticket(a, &q0);
+    const uint32_t b1 = b0 < kNumBuckets ? bucket_ticket(a, &q1) : kNumBuckets;
+    sh_b[0] = b0;
+    sh_q[0] = q0;
+    sh_b[1] = b1;
+    sh_q[1] = q1;
   }
-  const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
-  for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
-    mslice[i] = mg[i];
-    nbits[i] = 0;
-  }
-  for (uint32_t i = tid; i < kHash; i += kBThreads) {
-    hkey[i] = kEmpty;
-    hval[i] = kEmpty;
-  }
-  const bool lds_runs = r.nch <= kRunWin;
-  if (lds_runs)
-    for (uint32_t i = tid; i < r.nch; i += kBThreads) {
-      runs[i] = r.row[i];
-      tb[i] = (a.cgov[r.c0 + i] % a.kt) * kGroupTiles;
+  __syncthreads();
+  uint32_t b = sh_b[0], b1 = sh_b[1];
+  uint4 q = sh_q[0], q1 = sh_q[1];
+  if (b >= kNumBuckets) {
+    if (kDbg && tid == 0) {
+      for (int j = 0; j < 8; j++) a.dbg[8 * blockIdx.x + j] = 0;
+      a.dbg[8 * blockIdx.x] = t_start;
+      a.dbg[8 * blockIdx.x + 1] = wall_clock64();
     }
-  bool ok = true;
-  for (uint32_t base = r.lo;;) {
-    if (tid == 0) qn = 0;
-    __syncthreads();
-    uint32_t cm = 0;
-#pragma unroll
-    for (int u = 0; u < kBU; u++) {
-      const uint32_t sl = x[u] >> 16;
-      if (base + u * kBThreads + tid < r.hi && !((mslice[sl >> 5] >> (sl & 31)) & 1u))  // fuzzer.go:666
-        cm |= 1u << u;
-    }
-    // wave-aggregated queue slots
-    const uint32_t cnt = __popc(cm);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    uint32_t qb = 0;
-    if (lane == 63 && incl) qb = atomicAdd(&qn, incl);
-    uint32_t my = __shfl(qb, 63) + incl - cnt;
-#pragma unroll
-    for (int u = 0; u < kBU; u++)
-      if ((cm >> u) & 1u) {
-        const uint32_t i = base + u * kBThreads + tid;
-        if (my < kQueue) {
-          qx[my] = x[u];
-          qi[my] = i;
-        } else {  // queue overflow: this entry the sparse way
-          ok &= hash_insert(hkey, hval, nbits, x[u] >> 16, cand_record(a, r, lds_runs, runs, tb, i, x[u]));
-        }
-        my++;
-      }
-    const uint32_t next = base + kRound;
-#pragma unroll
-    for (int u = 0; u < kBU; u++) {
-      const uint32_t i = next + u * kBThreads + tid;
-      x[u] = i < r.hi ? a.in[i] : 0u;
-    }
-    __syncthreads();
-    const uint32_t qt = qn < kQueue ? qn : kQueue;
-    for (uint32_t q = tid; q < qt; q += 2 * kBThreads) {
-      const uint32_t q2 = q + kBThreads;
-      const uint32_t x0 = qx[q], x1 = q2 < qt ? qx[q2] : 0u;
-      const uint32_t r0 = cand_record(a, r, lds_runs, runs, tb, qi[q], x0);
-      const uint32_t r1 = q2 < qt ? cand_record(a, r, lds_runs, runs, tb, qi[q2], x1) : 0u;
-      ok &= hash_insert(hkey, hval, nbits, x0 >> 16, r0);
-      if (q2 < qt) ok &= hash_insert(hkey, hval, nbits, x1 >> 16, r1);
-    }
-    if (__syncthreads_or(!ok)) break;
-    if (next >= r.hi) break;
-    base = next;
-  }
-  if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
-    if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
     return;
   }
-  // a record is queued iff it owns some signal (fuzzer.go:678-690)
-  for (uint32_t i = tid; i < kHash; i += kBThreads)
-    if (hkey[i] != kEmpty) a.rec_new[hval[i]] = 1;
-  flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
+  uint32_t x[kBU], y[kBU];
+  BucketPre P;
+  bucket_round_load(a, q.x & ~3u, q.y, x);
+  bucket_pre_load(a, b, q, G2, P);
+  while (b < kNumBuckets) {
+    const BucketRange r = {b >> 8, b & 255, q.z, q.w, q.x, q.y, a.goff2 + (uint64_t)(b & 255) * G2 + q.z};
+    RunWindow W = {0, r.nch < kRunWin ? r.nch : kRunWin, P.lim};
+    __syncthreads();  // the previous bucket is done with the LDS
+    reinterpret_cast<uint4*>(mslice)[tid] = make_uint4(P.msw[0], P.msw[1], P.msw[2], P.msw[3]);
+#pragma unroll
+    for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+      const uint32_t i = j * kBThreads + tid;
+      if (i < W.wn) {
+        runs[i] = P.rw[j];
+        tb[i] = (P.tw[j] % a.kt) * kGroupTiles;
+      }
+    }
+    if (tid == 0) sh_b[0] = b1 < kNumBuckets ? bucket_ticket(a, &sh_q[0]) : kNumBuckets;  // the one after next
+    bool ok = true;
+    n_buckets++;
+    uint32_t ca = 0;  // a chunk at or before the one holding the round's first position
+    for (uint32_t base = r.lo & ~3u;;) {
+      n_rounds++;
+      if (tid == 0) qn = 0;
+      __syncthreads();
+      // move the chunk window when this round runs past it
+      const uint32_t rend = base + kRound < r.hi ? base + kRound : r.hi;
+      if (rend > W.wlim && W.wc + W.wn < r.nch) {
+        if (tid == 0) {
+          const uint32_t ps = base > r.lo ? base : r.lo;
+          sh_w[0] = chunk_of(r, W, runs, ps);
+        }
+        __syncthreads();
+        W.wc = sh_w[0];
+        W.wn = r.nch - W.wc < kRunWin ? r.nch - W.wc : kRunWin;
+        uint32_t rv[kRunWin / kBThreads], gv[kRunWin / kBThreads];
+#pragma unroll
+        for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+          const uint32_t i = j * kBThreads + tid;
+          rv[j] = i < W.wn ? r.row[W.wc + i] : 0u;
+          gv[j] = i < W.wn ? a.cgov[r.c0 + W.wc + i] : 0u;
+        }
+        W.wlim = W.wc + W.wn < r.nch ? r.row[W.wc + W.wn] : r.hi;
+#pragma unroll
+        for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+          const uint32_t i = j * kBThreads + tid;
+          if (i < W.wn) {
+            runs[i] = rv[j];
+            tb[i] = (gv[j] % a.kt) * kGroupTiles;
+          }
+        }
+        __syncthreads();
+      }
+      // slot map: each chunk overlapping the round (from ca, up to kBThreads
+      // of them, inside the window) marks the threads whose first entry it
+      // holds; the chunk holding the next round's start becomes its ca
+      rtag++;
+      {
+        if (ca < W.wc) ca = W.wc;
+        const uint32_t c = ca + tid;
+        if (tid == 0) sh_ca = kEmpty;
+        if (c < W.wc + W.wn) {
+          const uint32_t sc = c == 0 ? base : runs[c - W.wc];
+          const uint32_t sn = c + 1 < W.wc + W.wn ? runs[c + 1 - W.wc] : W.wlim;
+          if (sn > sc && sn > base && sc < rend) {
+            const uint32_t tlo = sc <= base ? 0 : (sc - base + kBU - 1) / kBU;
+            const uint32_t thi = sn >= base + kRound ? kBThreads : (sn - base + kBU - 1) / kBU;
+            for (uint32_t t = tlo; t < thi; t++) {
+              slot_c[t] = c;
+              slot_t[t] = rtag;
+            }
+          }
+        }
+        __syncthreads();  // (sh_ca reset ordered before the writes below)
+        if (c < W.wc + W.wn) {
+          const uint32_t sc = runs[c - W.wc];
+          const uint32_t sn = c + 1 < W.wc + W.wn ? runs[c + 1 - W.wc] : W.wlim;
+          const uint32_t nb = base + kRound;
+          if (sc <= nb && nb < sn) sh_ca = c;
+        }
+      }
+      if (kDbg) {
+        const uint64_t t = clock64();
+        ph[base == (r.lo & ~3u) ? 0 : 1] += t - tk;
+        tk = t;
+      }
+      // this thread's 16 consecutive entries: the new-signal test (fuzzer.go:666)
+      const uint32_t p0 = round_pos(base, 0);
+      uint32_t cm = 0;
+#pragma unroll
+      for (int u = 0; u < kBU; u++) {
+        const uint32_t sl = x[u] >> 16, i = p0 + u;
+        if (i >= r.lo && i < r.hi && !((mslice[sl >> 5] >> (sl & 31)) & 1u)) cm |= 1u << u;
+      }
+      if (kDbg) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const uint64_t t = clock64();
+        ph[4] += t - tk;
+      }
+      // wave-aggregated queue slots
+      const uint32_t cnt = __popc(cm);
+      uint32_t incl = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      uint32_t qb = 0;
+      if (lane == 63 && incl) qb = atomicAdd(&qn, incl);
+      uint32_t my = __shfl(qb, 63) + incl - cnt;
+      uint32_t ov = 0;  // queue overflow: these entries go into the map directly below
+#pragma unroll
+      for (int u = 0; u < kBU; u++)
+        if ((cm >> u) & 1u) {
+          if (my < kQueue) {
+            qx[my] = x[u];
+            qk[my] = p0 + u;  // position; the owner key is made in the dense pass
+          } else {
+            ov |= 1u << u;
+          }
+          my++;
+        }
+      if (kDbg) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t t = clock64();
+        ph[5] += t - tk;
+      }
+      if (ov) {  // rare: the queue holds kQueue candidates per round
+#pragma unroll 1
+        for (int u = 0; u < kBU; u++)
+          if ((ov >> u) & 1u) {
+            uint32_t xu = 0;
+#pragma unroll
+            for (int k = 0; k < kBU; k++) xu = k == u ? x[k] : xu;
+            const uint32_t ci = chunk_of(r, W, runs, p0 + u);
+            ok &= hash_insert64(ht, nbits, xu >> 16,
+                                ((chunk_tile(a, r, W, tb, ci) + ((xu >> 8) & 255u)) << 8) | (xu & 255u));
+          }
+      }
+      // the next round in flight: this bucket's, or the next bucket's first
+      // (one load call: separate calls per case load into different
+      // registers and the join waits for them right here)
+      const uint32_t next = base + kRound;
+      const bool last = next >= r.hi;
+      if (!last || b1 < kNumBuckets)
+        bucket_round_load(a, last ? q1.x & ~3u : next, last ? q1.y : r.hi, y);
+      if (last && b1 < kNumBuckets) bucket_pre_load(a, b1, q1, G2, P);
+      __syncthreads();
+      if (kDbg) {
+        const uint64_t t = clock64();
+        ph[1] += t - tk;
+        tk = t;
+      }
+      const uint32_t qt = qn < kQueue ? qn : kQueue;
+      ca = sh_ca != kEmpty ? sh_ca : ca + kBThreads - 1;
+#if SG_EXP != 2
+      for (uint32_t k = tid; k < qt; k += kBThreads) {
+        // owner key: the chunk from the slot map of the thread that held the
+        // entry, a forward step or two to the entry's own chunk
+        const uint32_t xv = qx[k], i = qk[k], t = (i - base) / kBU;
+        uint32_t ci = slot_t[t] == rtag ? slot_c[t] : chunk_of(r, W, runs, i);
+        if (i < W.wlim && ci >= W.wc)
+          while (ci + 1 < W.wc + W.wn && runs[ci + 1 - W.wc] <= i) ci++;
+        else
+          ci = chunk_of(r, W, runs, i);
+        ok &= hash_insert64(ht, nbits, xv >> 16, ((chunk_tile(a, r, W, tb, ci) + ((xv >> 8) & 255u)) << 8) | (xv & 255u));
+      }
+#endif
+      const bool fail = __syncthreads_or(!ok);
+      if (kDbg) {
+        const uint64_t t = clock64();
+        ph[2] += t - tk;
+        tk = t;
+      }
+      if (last || fail) {
+        if (fail && !last && b1 < kNumBuckets) {  // skip the rest of the bucket (the spill kernel redoes it)
+          bucket_round_load(a, q1.x & ~3u, q1.y, y);
+          bucket_pre_load(a, b1, q1, G2, P);
+        }
+        break;
+      }
+      base = next;
+#pragma unroll
+      for (int u = 0; u < kBU; u++) x[u] = y[u];
+    }
+    if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
+      if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
+      for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
+      for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
+    } else {
+      // a record is queued iff it owns some signal (fuzzer.go:678-690): its
+      // owner key is flagged here, keys become records in k_key_records
+      for (uint32_t i = tid; i < kHash; i += kBThreads) {
+        const unsigned long long v = ht[i];
+        if (v != kEmpty64) {
+          a.kflag[(uint32_t)v] = 1;
+          ht[i] = kEmpty64;
+        }
+      }
+      uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
+      uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords : nullptr;
+      for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
+        const uint32_t nb = nbits[i];
+        if (nb) {
+          mg[i] = mslice[i] | nb;
+          if (ng) atomicOr(&ng[i], nb);  // no return: nothing waits on it
+          nbits[i] = 0;
+        }
+      }
+    }
+    __syncthreads();  // sh_b[0] / sh_q[0] are written
+    if (kDbg) {
+      const uint64_t t = clock64();
+      ph[3] += t - tk;
+      tk = t;
+    }
+    b = b1;
+    q = q1;
+    b1 = sh_b[0];
+    q1 = sh_q[0];
+#pragma unroll
+    for (int u = 0; u < kBU; u++) x[u] = y[u];
+  }
+  if (kDbg && tid == 0) {
+    a.dbg[8 * blockIdx.x] = t_start;
+    a.dbg[8 * blockIdx.x + 1] = wall_clock64();
+    a.dbg[8 * blockIdx.x + 2] = n_buckets;
+    a.dbg[8 * blockIdx.x + 3] = n_rounds;
+    for (int j = 0; j < 4; j++) a.dbg[8 * blockIdx.x + 4 + j] = ph[j];
+    a.dbg[8 * gridDim.x + 3 * blockIdx.x] = ph[4];
+    a.dbg[8 * gridDim.x + 3 * blockIdx.x + 1] = ph[5];
+  }
 }
 
 // Buckets with too many distinct candidates: a direct first-owner table over
@@ -714,17 +1020,31 @@ __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
         const uint32_t x = a.in[i];
         const uint32_t sl = x >> 16;
         if (sl / kQ != q || ((mslice[sl >> 5] >> (sl & 31)) & 1u)) continue;
-        atomicMin(&owner[sl % kQ], cand_record(a, r, lds_runs, runs, tb, i, x));
+        atomicMin(&owner[sl % kQ], cand_key(a, r, lds_runs, runs, tb, i, x));
         atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
       }
       __syncthreads();
       for (uint32_t i = tid; i < kQ; i += kBThreads)
-        if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
+        if (owner[i] != kEmpty) a.kflag[owner[i]] = 1;
       __syncthreads();
     }
     flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
     __syncthreads();
   }
+}
+
+// rec_new[trec[t] + j] = 1 for every flagged owner key t * 256 + j; 4 keys
+// per thread (the flag array is padded to whole words)
+__global__ void k_key_records(const uint32_t* __restrict__ kflag4, const uint32_t* __restrict__ trec, uint64_t nwords,
+                              uint8_t* __restrict__ rec_new) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwords) return;
+  const uint32_t f = kflag4[w];
+  if (!f) return;
+  const uint32_t key0 = (uint32_t)(w * 4), r0 = trec[key0 >> 8] + (key0 & 255u);
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if ((f >> (8 * j)) & 255u) rec_new[r0 + j] = 1;
 }
 
 // ------------------------------------------------------------------ scan ---
@@ -874,7 +1194,7 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, kt, ng, gmax;
   WsPlan p;
-  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oSC;
+  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oTK, oKF, oSC;
   BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
     nA = (n + kPT - 1) / kPT;
     nB = nrec ? (nrec - 1) / kRecCap : 0;
@@ -896,13 +1216,34 @@ struct BucketPlan {
     oBD = p.add((uint64_t)kNumBuckets * 16);
     oH2 = p.add(256 * gmax * 4);
     oO2 = p.add((256 * gmax + 1) * 4);
-    oV2 = p.add(n * 4);
+    oV2 = p.add(n * 4 + 64);  // the bucket kernel's 16-B loads may read past the end
     oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
+    oTK = p.add(4);
+    oKF = p.add(T * 256);
     oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
   }
 };
 
 size_t bucket_ws_bytes(uint64_t n, uint64_t nrec) { return BucketPlan(n, nrec).p.total; }
+
+// Grid of a persistent kernel: every block resident at once (CUs x blocks
+// per CU from the occupancy query), cached per kernel.
+static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, uint32_t> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(ctx->device, kernel);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+    cus = 256;
+  const uint32_t grid = (uint32_t)(per_cu * cus);
+  cache[key] = grid;
+  return grid;
+}
 
 // Flags-only triage of a device-resident batch (ctx lock held).
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
@@ -1007,16 +1348,35 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   ba.rec_new = d_rec_new;
   ba.nspill = nspill;
   ba.spill = nspill + 1;
+  ba.ticket = (uint32_t*)ws_at(ctx, bp.oTK);
+  ba.kflag = (uint8_t*)ws_at(ctx, bp.oKF);
+  SG_HIP(hipMemsetAsync(ba.kflag, 0, bp.T * 256, ctx->stream));
+  const bool dbg = getenv("SG_DEBUG_PART") != nullptr;
+  const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false>, kBThreads);
+  uint64_t* ddbg = nullptr;
+  if (dbg) {
+    SG_HIP(hipMalloc(&ddbg, (size_t)bgrid * 88));
+    ba.dbg = ddbg;
+  }
+  SG_HIP(hipMemsetAsync(ba.ticket, 0, 4, ctx->stream));
   SG_HIP(hipMemsetAsync(nspill, 0, 4, ctx->stream));
   hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
                      gcount, (const uint32_t*)cfirst, bdesc);
   {
     ScopedTimer tm(ctx, "bucket_triage");
-    hipLaunchKernelGGL(k_bucket, dim3(kNumBuckets), dim3(kBThreads), 0, ctx->stream, ba);
+    if (dbg)
+      hipLaunchKernelGGL(k_bucket<true>, dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+    else
+      hipLaunchKernelGGL(k_bucket<false>, dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
   }
   {
     ScopedTimer tm(ctx, "bucket_spill");
     hipLaunchKernelGGL(k_bucket_direct, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
+  }
+  {
+    ScopedTimer tm(ctx, "key_records");
+    hipLaunchKernelGGL(k_key_records, dim3(div_up(bp.T * 64, 256)), dim3(256), 0, ctx->stream,
+                       (const uint32_t*)ba.kflag, (const uint32_t*)trec, bp.T * 64, d_rec_new);
   }
   SG_HIP(hipGetLastError());
   if (getenv("SG_DEBUG_PART")) {  // diagnostics: chunk and spill counts (syncs)
@@ -1027,6 +1387,47 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     fprintf(stderr, "sg part: n=%llu nrec=%llu tiles=%llu chunks=%u (bound %llu) spilled_buckets=%u\n",
             (unsigned long long)n, (unsigned long long)nrec, (unsigned long long)bp.T, g,
             (unsigned long long)bp.gmax, sp);
+    std::vector<uint4> bd(kNumBuckets);
+    std::vector<uint64_t> hd((size_t)bgrid * 11);
+    SG_HIP(hipMemcpy(bd.data(), bdesc, bd.size() * 16, hipMemcpyDeviceToHost));
+    SG_HIP(hipMemcpy(hd.data(), ddbg, hd.size() * 8, hipMemcpyDeviceToHost));
+    double qa = 0, qb = 0;
+    for (uint32_t i = 0; i < bgrid; i++) {
+      qa += hd[8 * bgrid + 3 * i];
+      qb += hd[8 * bgrid + 3 * i + 1];
+    }
+    SG_HIP(hipFree(ddbg));
+    std::vector<uint32_t> sz(kNumBuckets);
+    uint64_t rounds = 0;
+    for (uint32_t b = 0; b < kNumBuckets; b++) {
+      sz[b] = bd[b].y - bd[b].x;
+      rounds += (sz[b] + 8191) / 8192;
+    }
+    std::sort(sz.begin(), sz.end());
+    uint64_t t0 = ~0ull, t1 = 0;
+    std::vector<double> dur;
+    uint64_t maxr = 0;
+    double phs[4] = {0, 0, 0, 0}, nbk = 0, nrd = 0;
+    for (uint32_t i = 0; i < bgrid; i++) {
+      t0 = std::min(t0, hd[8 * i]);
+      t1 = std::max(t1, hd[8 * i + 1]);
+      dur.push_back((hd[8 * i + 1] - hd[8 * i]) / 100.0);  // 100 MHz clock -> us
+      maxr = std::max(maxr, hd[8 * i + 3]);
+      nbk += hd[8 * i + 2];
+      nrd += hd[8 * i + 3];
+      for (int j = 0; j < 4; j++) phs[j] += hd[8 * i + 4 + j];
+    }
+    fprintf(stderr, "sg bucket phases (Mcycles/block): install %.2f queue %.2f dense %.2f flush %.2f; per bucket %.0f"
+            " cycles, per round queue %.0f dense %.0f\n", phs[0] / bgrid / 1e6, phs[1] / bgrid / 1e6,
+            phs[2] / bgrid / 1e6, phs[3] / bgrid / 1e6, (phs[0] + phs[3]) / nbk, phs[1] / nrd, phs[2] / nrd);
+    fprintf(stderr, "sg bucket queue phase per round: to test done %.0f, to enqueue done %.0f cycles (cumulative)\n",
+            qa / nrd, qb / nrd);
+    std::sort(dur.begin(), dur.end());
+    fprintf(stderr,
+            "sg bucket: sizes max=%u p99=%u median=%u rounds=%llu | blocks=%u span=%.1fus dur min=%.1f med=%.1f "
+            "max=%.1f us, max rounds/block=%llu\n",
+            sz.back(), sz[kNumBuckets * 99 / 100], sz[kNumBuckets / 2], (unsigned long long)rounds, bgrid,
+            (t1 - t0) / 100.0, dur.front(), dur[dur.size() / 2], dur.back(), (unsigned long long)maxr);
   }
   return SG_OK;
 }

@@ -97,7 +97,7 @@ int hip_fail(hipError_t e, const char* what);
 int ensure_device(sg_ctx* ctx);
 // Carve `n` bump-allocated regions out of the workspace (each 256-B aligned).
 struct WsPlan {
-  size_t off[16];
+  size_t off[32];
   int n = 0;
   size_t total = 0;
   size_t add(size_t bytes) {
