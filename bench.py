@@ -92,7 +92,7 @@ def triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off):
          diff_off.data_ptr() if diff_off is not None else None)
 
 
-KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan",
+KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "key_records", "scan",
            "triage_claim", "triage_resolve", "emit"]
 
 
@@ -117,7 +117,8 @@ def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords):
         "p1_scatter": 4 * n_in + 4 * n_in + 256 * t * 4,
         "p2_hist": 4 * n_in + 256 * g2 * 4,
         "p2_scatter": 4 * n_in + 4 * n_in + 256 * g2 * 4,
-        "bucket_triage": 4 * n_in + mbits + 8 * n_cand + 16 * n_newwords + n_rec,
+        # entries + the maxSignal and newSignal slices + the two new-word stores + one owner-key flag each
+        "bucket_triage": 4 * n_in + 2 * mbits + 8 * n_newwords + n_diff,
         "triage_claim": 4 * n_in + 4 * n_in + 8 * n_cand + n_in / 8,
         "triage_resolve": n_in / 8 + 4 * n_cand + 4 * n_cand + 16 * n_diff + n_rec + n_in / 8 + n_in / 64,
     }

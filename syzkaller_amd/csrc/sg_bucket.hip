@@ -186,11 +186,9 @@ constexpr int kHistQ = kPT / 4 / kPThreads;  // uint4 loads per lane
 // grid columns.  Pass 2 (desc != nullptr): the block's chunk descriptor and
 // *ncols_dev columns; blocks without a chunk exit.
 template <bool kVec>
-__global__ __launch_bounds__(kPThreads) void k_hist_top(const uint32_t* __restrict__ v,
-                                                        const uint32_t* __restrict__ start,
-                                                        const uint4* __restrict__ desc,
-                                                        const uint32_t* __restrict__ ncols_dev,
-                                                        uint32_t* __restrict__ hist) {
+__device__ __forceinline__ void hist_top(const uint32_t* __restrict__ v, const uint32_t* __restrict__ start,
+                                         const uint4* __restrict__ desc, const uint32_t* __restrict__ ncols_dev,
+                                         uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[256];
   uint32_t t, s0, s1, ncols;
   if (desc) {
@@ -247,6 +245,19 @@ __global__ __launch_bounds__(kPThreads) void k_hist_top(const uint32_t* __restri
   }
   __syncthreads();
   if (tid < 256) hist[(uint64_t)tid * ncols + t] = cnt[tid];
+}
+
+// the two passes' histograms as kernels of their own names (profiles)
+template <bool kVec>
+__global__ __launch_bounds__(kPThreads) void k_p1_hist(const uint32_t* __restrict__ v,
+                                                       const uint32_t* __restrict__ start, uint32_t* __restrict__ hist) {
+  hist_top<kVec>(v, start, nullptr, nullptr, hist);
+}
+
+__global__ __launch_bounds__(kPThreads) void k_p2_hist(const uint32_t* __restrict__ v, const uint4* __restrict__ desc,
+                                                       const uint32_t* __restrict__ ncols_dev,
+                                                       uint32_t* __restrict__ hist) {
+  hist_top<true>(v, nullptr, desc, ncols_dev, hist);
 }
 
 // Counting sort of one tile held in registers (kSteps entries per lane) by an
@@ -503,7 +514,10 @@ struct BucketArgs {
   uint8_t* rec_new;
   uint32_t* spill;         // buckets left for the direct-table kernel
   uint32_t* nspill;
-  uint32_t* ticket;        // persistent bucket kernel: buckets handed out past the grid
+  uint32_t* ticket;        // persistent bucket kernel: list entries handed out past 2 x grid
+  const uint32_t* blist_b; // non-empty buckets, in bucket order ...
+  const uint4* blist_q;    // ... and their descriptors
+  const uint32_t* nlist;   // device: their number
   uint64_t* dbg;           // diagnostics (k_bucket<true>): per block {start, end, buckets, rounds, 4 phase cycle sums}
   uint8_t* kflag;          // owner keys (tile * 256 + record in tile) that own some signal
 };
@@ -512,6 +526,23 @@ struct BucketRange {
   uint32_t d, f, c0, nch, lo, hi;
   const uint32_t* row;  // goff2 + f * G2 + c0: run start of each chunk of slice d
 };
+
+// non-empty flag per bucket (scanned into list positions)
+__global__ void k_bucket_nz(const uint4* __restrict__ bdesc, uint32_t* __restrict__ nz) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < kNumBuckets) nz[b] = bdesc[b].x < bdesc[b].y ? 1u : 0u;
+}
+
+__global__ void k_bucket_compact(const uint4* __restrict__ bdesc, const uint32_t* __restrict__ lpos,
+                                 uint32_t* __restrict__ blist_b, uint4* __restrict__ blist_q) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= kNumBuckets) return;
+  const uint4 q = bdesc[b];
+  if (q.x < q.y) {
+    blist_b[lpos[b]] = b;
+    blist_q[lpos[b]] = q;
+  }
+}
 
 // {lo, hi, c0, nch} of every bucket, from the pass-2 scan
 __global__ void k_bucket_desc(const uint32_t* __restrict__ goff2, const uint32_t* __restrict__ gcount,
@@ -606,6 +637,7 @@ __device__ __forceinline__ uint32_t key_record(const BucketArgs& a, uint32_t key
 // that is fetched a bucket ahead, so no dependent load is exposed.
 struct BucketPre {  // a bucket's first loads, held in registers
   uint32_t msw[kBucketWords / kBThreads];
+  uint32_t nsw[kBucketWords / kBThreads];  // newSignal words (only this block writes them)
   uint32_t rw[kRunWin / kBThreads];  // its first window of chunk run starts ...
   uint32_t tw[kRunWin / kBThreads];  // ... and their groups
   uint32_t lim;                      // first position past that window
@@ -638,6 +670,12 @@ __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b,
   P.msw[1] = m.y;
   P.msw[2] = m.z;
   P.msw[3] = m.w;
+  const uint4 nw = a.nwords ? reinterpret_cast<const uint4*>(a.nwords + (uint64_t)b * kBucketWords)[threadIdx.x]
+                            : make_uint4(0, 0, 0, 0);
+  P.nsw[0] = nw.x;
+  P.nsw[1] = nw.y;
+  P.nsw[2] = nw.z;
+  P.nsw[3] = nw.w;
   const uint32_t* row = a.goff2 + (uint64_t)(b & 255) * G2 + q.z;
 #pragma unroll
   for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
@@ -649,20 +687,18 @@ __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b,
   P.lim = q.w > kRunWin ? row[kRunWin] : q.y;
 }
 
-// thread 0: the next non-empty bucket by ticket (kNumBuckets: none)
-__device__ __forceinline__ uint32_t bucket_ticket(const BucketArgs& a, uint4* q) {
-  for (;;) {
-    const uint32_t nb = gridDim.x + atomicAdd(a.ticket, 1u);
-    if (nb >= kNumBuckets) return kNumBuckets;
-    const uint4 d = a.bdesc[nb];
-    if (d.x < d.y) {
-      *q = d;
-      return nb;
-    }
-  }
+// thread 0: bucket and descriptor of list entry t (kNumBuckets: past the end)
+__device__ __forceinline__ uint32_t list_bucket(const BucketArgs& a, uint32_t t, uint32_t nl, uint4* q) {
+  if (t >= nl) return kNumBuckets;
+  *q = a.blist_q[t];
+  return a.blist_b[t];
 }
 
 constexpr unsigned long long kEmpty64 = ~0ull;
+
+// block-uniform values read from LDS: keep them in scalar registers
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint4 uni(uint4 v) { return make_uint4(uni(v.x), uni(v.y), uni(v.z), uni(v.w)); }
 
 // Map slot = signal (high word) | owner key (low word).  A first insert is one
 // CAS; a repeat of a signal lowers the key with a u64 min (equal high words).
@@ -733,19 +769,22 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
   for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
   slot_t[tid] = kEmpty;
   uint32_t rtag = 0;  // round tag of the slot map
-  if (tid == 0) {  // this block's first two buckets
-    uint4 q0 = a.bdesc[blockIdx.x < kNumBuckets ? blockIdx.x : 0], q1 = make_uint4(0, 0, 0, 0);
-    uint32_t b0 = blockIdx.x;
-    if (b0 >= kNumBuckets || q0.x >= q0.y) b0 = bucket_ticket(a, &q0);
-    const uint32_t b1 = b0 < kNumBuckets ? bucket_ticket(a, &q1) : kNumBuckets;
-    sh_b[0] = b0;
+  // list entries: blockIdx and gridDim + blockIdx first, then tickets from
+  // 2 x gridDim.  Thread 0 takes each ticket a bucket before it resolves it and
+  // resolves it a bucket before it is needed, so neither wait is exposed.
+  const uint32_t nl = *a.nlist;
+  uint32_t pend_t = kEmpty;  // thread 0: ticket taken, not yet resolved
+  if (tid == 0) {
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
+    sh_b[0] = list_bucket(a, blockIdx.x, nl, &q0);
     sh_q[0] = q0;
-    sh_b[1] = b1;
+    sh_b[1] = list_bucket(a, gridDim.x + blockIdx.x, nl, &q1);
     sh_q[1] = q1;
+    pend_t = 2 * gridDim.x + atomicAdd(a.ticket, 1u);
   }
   __syncthreads();
-  uint32_t b = sh_b[0], b1 = sh_b[1];
-  uint4 q = sh_q[0], q1 = sh_q[1];
+  uint32_t b = uni(sh_b[0]), b1 = uni(sh_b[1]);
+  uint4 q = uni(sh_q[0]), q1 = uni(sh_q[1]);
   if (b >= kNumBuckets) {
     if (kDbg && tid == 0) {
       for (int j = 0; j < 8; j++) a.dbg[8 * blockIdx.x + j] = 0;
@@ -763,6 +802,7 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
     RunWindow W = {0, r.nch < kRunWin ? r.nch : kRunWin, P.lim};
     __syncthreads();  // the previous bucket is done with the LDS
     reinterpret_cast<uint4*>(mslice)[tid] = make_uint4(P.msw[0], P.msw[1], P.msw[2], P.msw[3]);
+    const uint4 ns = make_uint4(P.nsw[0], P.nsw[1], P.nsw[2], P.nsw[3]);  // words 4 tid .. +3
 #pragma unroll
     for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
       const uint32_t i = j * kBThreads + tid;
@@ -771,7 +811,13 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
         tb[i] = (P.tw[j] % a.kt) * kGroupTiles;
       }
     }
-    if (tid == 0) sh_b[0] = b1 < kNumBuckets ? bucket_ticket(a, &sh_q[0]) : kNumBuckets;  // the one after next
+    // thread 0: resolve the pending ticket (published after the rounds) and take the next one
+    uint32_t pend_b = kNumBuckets;
+    uint4 pend_q = make_uint4(0, 0, 0, 0);
+    if (tid == 0) {
+      pend_b = list_bucket(a, pend_t, nl, &pend_q);
+      pend_t = pend_b < kNumBuckets ? 2 * gridDim.x + atomicAdd(a.ticket, 1u) : kEmpty;
+    }
     bool ok = true;
     n_buckets++;
     uint32_t ca = 0;  // a chunk at or before the one holding the round's first position
@@ -787,7 +833,7 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
           sh_w[0] = chunk_of(r, W, runs, ps);
         }
         __syncthreads();
-        W.wc = sh_w[0];
+        W.wc = uni(sh_w[0]);
         W.wn = r.nch - W.wc < kRunWin ? r.nch - W.wc : kRunWin;
         uint32_t rv[kRunWin / kBThreads], gv[kRunWin / kBThreads];
 #pragma unroll
@@ -908,7 +954,7 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
         tk = t;
       }
       const uint32_t qt = qn < kQueue ? qn : kQueue;
-      ca = sh_ca != kEmpty ? sh_ca : ca + kBThreads - 1;
+      ca = uni(sh_ca != kEmpty ? sh_ca : ca + kBThreads - 1);
 #if SG_EXP != 2
       for (uint32_t k = tid; k < qt; k += kBThreads) {
         // owner key: the chunk from the slot map of the thread that held the
@@ -939,6 +985,10 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
 #pragma unroll
       for (int u = 0; u < kBU; u++) x[u] = y[u];
     }
+    if (tid == 0) {  // the bucket after next
+      sh_b[0] = pend_b;
+      sh_q[0] = pend_q;
+    }
     if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
       if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
@@ -953,15 +1003,21 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
           ht[i] = kEmpty64;
         }
       }
-      uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
-      uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords : nullptr;
-      for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
-        const uint32_t nb = nbits[i];
-        if (nb) {
-          mg[i] = mslice[i] | nb;
-          if (ng) atomicOr(&ng[i], nb);  // no return: nothing waits on it
-          nbits[i] = 0;
-        }
+      // words 4 tid .. +3: this block is their only writer
+      uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords + 4 * tid;
+      uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords + 4 * tid : nullptr;
+      const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
+      if (nb4.x | nb4.y | nb4.z | nb4.w) {
+        const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
+        const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
+        const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (nb[j]) {
+            mg[j] = mw[j] | nb[j];
+            if (ng) ng[j] = nw[j] | nb[j];
+          }
+        reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
       }
     }
     __syncthreads();  // sh_b[0] / sh_q[0] are written
@@ -972,8 +1028,8 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
     }
     b = b1;
     q = q1;
-    b1 = sh_b[0];
-    q1 = sh_q[0];
+    b1 = uni(sh_b[0]);
+    q1 = uni(sh_q[0]);
 #pragma unroll
     for (int u = 0; u < kBU; u++) x[u] = y[u];
   }
@@ -1194,7 +1250,7 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, kt, ng, gmax;
   WsPlan p;
-  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oTK, oKF, oSC;
+  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oTK, oKF, oBN, oBP, oLB, oLQ, oSC;
   BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
     nA = (n + kPT - 1) / kPT;
     nB = nrec ? (nrec - 1) / kRecCap : 0;
@@ -1220,6 +1276,10 @@ struct BucketPlan {
     oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
     oTK = p.add(4);
     oKF = p.add(T * 256);
+    oBN = p.add((uint64_t)kNumBuckets * 4);
+    oBP = p.add(((uint64_t)kNumBuckets + 1) * 4);
+    oLB = p.add((uint64_t)kNumBuckets * 4);
+    oLQ = p.add((uint64_t)kNumBuckets * 16);
     oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
   }
 };
@@ -1299,11 +1359,11 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   {
     ScopedTimer tm(ctx, "p1_hist");
     if (((uintptr_t)d_vals & 15) == 0)
-      hipLaunchKernelGGL(k_hist_top<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
-                         (const uint32_t*)tstart, (const uint4*)nullptr, (const uint32_t*)nullptr, hist1);
+      hipLaunchKernelGGL(k_p1_hist<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+                         (const uint32_t*)tstart, hist1);
     else
-      hipLaunchKernelGGL(k_hist_top<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
-                         (const uint32_t*)tstart, (const uint4*)nullptr, (const uint32_t*)nullptr, hist1);
+      hipLaunchKernelGGL(k_p1_hist<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+                         (const uint32_t*)tstart, hist1);
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
@@ -1324,8 +1384,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
                      (const uint32_t*)cgov, gcount, bp.gmax, cdesc);
   {
     ScopedTimer tm(ctx, "p2_hist");
-    hipLaunchKernelGGL(k_hist_top<true>, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
-                       (const uint32_t*)nullptr, (const uint4*)cdesc, gcount, hist2);
+    hipLaunchKernelGGL(k_p2_hist, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
+                       (const uint4*)cdesc, gcount, hist2);
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
   if (rc) return rc;
@@ -1362,6 +1422,16 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   SG_HIP(hipMemsetAsync(nspill, 0, 4, ctx->stream));
   hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
                      gcount, (const uint32_t*)cfirst, bdesc);
+  uint32_t* bnz = (uint32_t*)ws_at(ctx, bp.oBN);
+  uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
+  hipLaunchKernelGGL(k_bucket_nz, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc, bnz);
+  rc = scan32(ctx, bnz, blpos, kNumBuckets, scr);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_bucket_compact, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc,
+                     (const uint32_t*)blpos, (uint32_t*)ws_at(ctx, bp.oLB), (uint4*)ws_at(ctx, bp.oLQ));
+  ba.blist_b = (const uint32_t*)ws_at(ctx, bp.oLB);
+  ba.blist_q = (const uint4*)ws_at(ctx, bp.oLQ);
+  ba.nlist = blpos + kNumBuckets;
   {
     ScopedTimer tm(ctx, "bucket_triage");
     if (dbg)
