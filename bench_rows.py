@@ -62,11 +62,13 @@ def row_c1(ctx, rng):
         t0 = time.perf_counter()
         out = C.merge_batch(op, a, a_beg, a_len, corpus, b_beg, b_len, ctx=ctx)
         wall = time.perf_counter() - t0
-        kt = ktime(ctx, ["merge_keep", "merge_scatter", "scan"])
+        kt = ktime(ctx, ["merge_small", "merge_keep", "merge_scatter", "scan"])
         ctx.timing(False)
         dev_ms = sum(kt.values())
-        n_in = int(a.size + 1000 * corpus.size)
         n_out = sum(o.size for o in out)
+        # Union reads both lists of every pair; Difference only has to read
+        # cov0 (its count in cov1 is a search), so cov1 is not charged to it
+        n_in = int(a.size + (1000 * corpus.size if op == 2 else 0))
         algo = 4 * (n_in + n_out)
         # oracle on a sample of 20 pairs
         t1 = time.perf_counter()

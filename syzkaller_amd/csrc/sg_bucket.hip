@@ -264,13 +264,12 @@ __global__ __launch_bounds__(kPThreads) void k_p2_hist(const uint32_t* __restric
 // 8-bit digit, through LDS: counts, a one-wave exclusive scan, then every
 // entry takes a slot with an LDS atomic (order within a digit is arbitrary).
 // On return dstart[d] is the digit's first slot and pos[k] entry k's slot.
+// cnt[] arrives holding the tile's digit counts (read from the histogram
+// pass, not recounted); gbase[d] is lowered by the digit's first slot, so slot
+// p of digit d goes to gbase[d] + p.
 __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t vmask, uint32_t* cnt,
-                                          uint16_t* dstart, uint32_t (&pos)[kSteps]) {
+                                          uint32_t* gbase, uint32_t (&pos)[kSteps]) {
   const int tid = threadIdx.x, lane = tid & 63;
-#pragma unroll
-  for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) atomicAdd(&cnt[dv[k]], 1u);
-  __syncthreads();
   if (tid < 64) {
     uint32_t carry = 0;
 #pragma unroll
@@ -283,7 +282,7 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
         if (lane >= o) incl += y;
       }
       const uint32_t ex = carry + incl - x;
-      dstart[base + lane] = (uint16_t)ex;
+      gbase[base + lane] -= ex;
       cnt[base + lane] = ex;
       carry += __shfl(incl, 63);
     }
@@ -365,14 +364,16 @@ struct P1Args {
   const uint32_t* trec;    // T
   uint32_t T;
   const uint32_t* goff1;   // scanned [slice][tile]
+  const uint32_t* hist1;   // [slice][tile] counts
   uint32_t* out;           // s << 8 | rec_in_tile
+  unsigned long long* dbg; // diagnostics (k_p1_scatter<true>): cycles per phase, summed over blocks
 };
 
+template <bool kDbg>
 __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   __shared__ uint32_t stage[kPT];
   __shared__ uint8_t sdig[kPT];
   __shared__ uint32_t cnt[256];
-  __shared__ uint16_t dstart[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
   __shared__ SegLds L;
@@ -380,6 +381,15 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
   if (s0 >= s1) return;
+  uint64_t tk = kDbg ? clock64() : 0;
+  auto stamp = [&](int ph) {
+    if (kDbg) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t now = clock64();
+      if (tid == 0) atomicAdd(&a.dbg[ph], (unsigned long long)(now - tk));
+      tk = now;
+    }
+  };
   const uint32_t r0 = a.trec[t];
   const uint32_t wn = (uint32_t)(a.nrec + 1 - r0 < kRecCap + 1 ? a.nrec + 1 - r0 : kRecCap + 1);
   const uint32_t ebase = s0 + w * kPerWave;
@@ -398,10 +408,11 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   }
   for (int d = tid; d < 256; d += kPThreads) {
     gbase[d] = a.goff1[(uint64_t)d * a.T + t];
-    cnt[d] = 0;
+    cnt[d] = a.hist1[(uint64_t)d * a.T + t];
   }
   seg_clear(L, tid);
   __syncthreads();
+  stamp(0);
   const uint32_t nt = s1 - s0;
   seg_build(L, sdig, win, wn, nt, tid);  // sdig doubles as the segment index until the rank
   uint32_t dv[kSteps], pk[kSteps];
@@ -412,8 +423,10 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
     dv[k] = sv[k] >> 24;
     pk[k] = (sv[k] << 8) | r;
   }
+  stamp(1);
   uint32_t pos[kSteps];
-  tile_rank(dv, vmask, cnt, dstart, pos);
+  tile_rank(dv, vmask, cnt, gbase, pos);
+  stamp(2);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
     if ((vmask >> k) & 1u) {
@@ -421,10 +434,13 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
       sdig[pos[k]] = (uint8_t)dv[k];
     }
   __syncthreads();
+  stamp(3);
   for (uint32_t p = tid; p < nt; p += kPThreads) {
     const uint32_t d = sdig[p];
-    a.out[gbase[d] + (p - dstart[d])] = stage[p];
+    a.out[gbase[d] + p] = stage[p];
   }
+  stamp(4);
+  if (kDbg && tid == 0) atomicAdd(&a.dbg[5], 1ull);
 }
 
 // ---------------------------------------------------------------- pass 2 ---
@@ -436,6 +452,7 @@ struct P2Args {
   uint32_t T, kt;
   uint32_t n;
   const uint32_t* goff2;   // scanned [byte][chunk]
+  const uint32_t* hist2;   // [byte][chunk] counts
   uint32_t* out;           // (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile
 };
 
@@ -443,7 +460,6 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   __shared__ uint32_t stage[kPT];
   __shared__ uint8_t sdig[kPT];
   __shared__ uint32_t cnt[256];
-  __shared__ uint16_t dstart[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t runs[kGroupTiles + 1];  // chunk-relative run starts of the group's tiles in this slice
   __shared__ SegLds L;
@@ -470,7 +486,7 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   }
   for (int f = tid; f < 256; f += kPThreads) {
     gbase[f] = a.goff2[(uint64_t)f * G2 + c];
-    cnt[f] = 0;
+    cnt[f] = a.hist2[(uint64_t)f * G2 + c];
   }
   seg_clear(L, tid);
   __syncthreads();
@@ -485,7 +501,7 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
     pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (k1 << 8) | (sv[k] & 0xFFu);
   }
   uint32_t pos[kSteps];
-  tile_rank(dv, vmask, cnt, dstart, pos);
+  tile_rank(dv, vmask, cnt, gbase, pos);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
     if ((vmask >> k) & 1u) {
@@ -495,7 +511,7 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   __syncthreads();
   for (uint32_t p = tid; p < nt; p += kPThreads) {
     const uint32_t f = sdig[p];
-    a.out[gbase[f] + (p - dstart[f])] = stage[p];
+    a.out[gbase[f] + p] = stage[p];
   }
 }
 
@@ -1367,10 +1383,28 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
-  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, v1};
+  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, nullptr};
+  const bool dbg = getenv("SG_DEBUG_PART") != nullptr;
+  unsigned long long* p1dbg = nullptr;
+  if (dbg) {
+    SG_HIP(hipMalloc(&p1dbg, 64));
+    SG_HIP(hipMemsetAsync(p1dbg, 0, 64, ctx->stream));
+    a1.dbg = p1dbg;
+  }
   {
     ScopedTimer tm(ctx, "p1_scatter");
-    hipLaunchKernelGGL(k_p1_scatter, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+    if (dbg)
+      hipLaunchKernelGGL(k_p1_scatter<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+    else
+      hipLaunchKernelGGL(k_p1_scatter<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+  }
+  if (dbg) {
+    unsigned long long h[8];
+    SG_HIP(hipMemcpy(h, p1dbg, 64, hipMemcpyDeviceToHost));
+    SG_HIP(hipFree(p1dbg));
+    fprintf(stderr, "sg p1_scatter per tile (cycles, wave 0): load+meta %.0f build+lookup %.0f rank %.0f stage %.0f "
+            "write %.0f (tiles %llu)\n", (double)h[0] / h[5], (double)h[1] / h[5], (double)h[2] / h[5],
+            (double)h[3] / h[5], (double)h[4] / h[5], h[5]);
   }
   // pass-2 chunks
   hipLaunchKernelGGL(k_group_chunks, dim3(div_up(bp.ng, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)goff1,
@@ -1389,7 +1423,7 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
   if (rc) return rc;
-  P2Args a2{v1, cdesc, gcount, goff1, T, (uint32_t)bp.kt, (uint32_t)n, goff2, v2};
+  P2Args a2{v1, cdesc, gcount, goff1, T, (uint32_t)bp.kt, (uint32_t)n, goff2, hist2, v2};
   {
     ScopedTimer tm(ctx, "p2_scatter");
     hipLaunchKernelGGL(k_p2_scatter, dim3(G), dim3(kPThreads), 0, ctx->stream, a2);
@@ -1411,7 +1445,6 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   ba.ticket = (uint32_t*)ws_at(ctx, bp.oTK);
   ba.kflag = (uint8_t*)ws_at(ctx, bp.oKF);
   SG_HIP(hipMemsetAsync(ba.kflag, 0, bp.T * 256, ctx->stream));
-  const bool dbg = getenv("SG_DEBUG_PART") != nullptr;
   const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false>, kBThreads);
   uint64_t* ddbg = nullptr;
   if (dbg) {

@@ -158,6 +158,232 @@ __global__ void k_merge_scatter(MergeArgs m) {
   }
 }
 
+// ---- one small side per pair (C1: traces against one large corpus signal) --
+// Union / SymmetricDifference keep elements of both lists.  When one list of
+// a pair fits in LDS (<= kMS values) a workgroup per pair does the whole
+// merge: the small list S, its keep flags and kept-prefix live in LDS; the
+// large list L streams through once in index order; each L element's count
+// in S and its insertion point come from LDS searches, its rank from wave
+// ballots; S's kept elements land when the L tile holding their insertion
+// point is processed.  Same keep rule and positions as k_merge_keep /
+// k_merge_scatter (copy t of a value against its count c in the other list;
+// ties: cov0's copies first).
+constexpr int kMS = 4096;               // max small side
+constexpr int kMT = 1024;               // threads
+constexpr int kMU = kMS / kMT;          // small elements per thread (consecutive)
+constexpr int kML = 4;                  // large elements per thread per tile
+constexpr int kMTile = kMT * kML;       // 4096
+constexpr int kMWaves = kMT / 64;       // 16
+
+struct SmallArgs {
+  int op;
+  const uint32_t* a;
+  const uint32_t* b;
+  const uint64_t* abeg;
+  const uint64_t* alen;
+  const uint64_t* bbeg;
+  const uint64_t* blen;
+  const uint64_t* obeg;
+  uint64_t* olen;
+  uint32_t* out;
+};
+
+__device__ __forceinline__ bool keep_rule(int op, int side, uint64_t t, uint64_t c) {
+  switch (op) {
+    case SG_OP_DIFFERENCE: return side == 0 && t >= c;
+    case SG_OP_INTERSECT: return side == 0 && t < c;
+    case SG_OP_UNION: return side == 0 ? true : t >= c;
+    default: return t >= c;  // SG_OP_SYMDIFF
+  }
+}
+
+// first index in p[0..n) with p[idx] >= v (kUpper: > v); all kN searches of a
+// thread advance level by level so their loads are in flight together
+template <int kN, bool kUpper, typename P>
+__device__ __forceinline__ void multi_bound(P p, uint64_t n, const uint32_t (&v)[kN], uint64_t (&lo)[kN]) {
+  // branch-free halving: the answer stays in [base, base + len]; len depends
+  // only on n, so every search takes the same steps
+  uint64_t base[kN];
+#pragma unroll
+  for (int u = 0; u < kN; u++) base[u] = 0;
+  uint64_t len = n;
+  while (len > 1) {
+    const uint64_t half = len >> 1;
+#pragma unroll
+    for (int u = 0; u < kN; u++) {
+      const uint32_t pv = p[base[u] + half];
+      if (kUpper ? pv <= v[u] : pv < v[u]) base[u] += half;
+    }
+    len -= half;
+  }
+#pragma unroll
+  for (int u = 0; u < kN; u++) {
+    if (n == 0) {
+      lo[u] = 0;
+    } else {
+      const uint32_t pv = p[base[u]];
+      lo[u] = base[u] + ((kUpper ? pv <= v[u] : pv < v[u]) ? 1 : 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMT) void k_merge_small(SmallArgs m) {
+  __shared__ uint32_t sv[kMS];
+  __shared__ uint32_t skp[kMS + 1];    // kept small elements before j
+  __shared__ uint32_t sidx[kMS];       // insertion point of small element j in L
+  __shared__ unsigned long long tw[kML * kMWaves];
+  __shared__ uint32_t twp[kML * kMWaves + 1];
+  __shared__ uint32_t red[kMWaves + 1];
+  const uint32_t k = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t na = m.alen[k], nb = m.blen[k];
+  const int sS = na <= nb ? 0 : 1, sL = 1 - sS;  // side of S / L (0: cov0)
+  const uint32_t* S = sS == 0 ? m.a + m.abeg[k] : m.b + m.bbeg[k];
+  const uint32_t* L = sS == 0 ? m.b + m.bbeg[k] : m.a + m.abeg[k];
+  const uint32_t ns = (uint32_t)(sS == 0 ? na : nb);
+  const uint64_t nl = sS == 0 ? nb : na;
+  uint32_t* out = m.out + m.obeg[k];
+  for (uint32_t j = tid; j < ns; j += kMT) sv[j] = S[j];
+  __syncthreads();
+  // S: keep flags (copy t against the count in L) and insertion points in L
+  uint32_t flags = 0;
+  {
+    uint32_t x[kMU];
+    uint64_t lb[kMU], ub[kMU];
+#pragma unroll
+    for (int u = 0; u < kMU; u++) {
+      const uint32_t j = tid * kMU + u;
+      x[u] = j < ns ? sv[j] : 0u;
+    }
+    multi_bound<kMU, false>(L, nl, x, lb);
+    multi_bound<kMU, true>(L, nl, x, ub);
+#pragma unroll
+    for (int u = 0; u < kMU; u++) {
+      const uint32_t j = tid * kMU + u;
+      if (j >= ns) continue;
+      uint64_t t = 0;
+      if (j > 0 && sv[j - 1] == x[u]) {  // later copy: t = j - first index of the value
+        uint32_t lo = 0, hi = j;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sv[mid] < x[u]) lo = mid + 1; else hi = mid;
+        }
+        t = j - lo;
+      }
+      const bool kp = x[u] != kSent && keep_rule(m.op, sS, t, ub[u] - lb[u]);  // cover.go:97
+      flags |= (kp ? 1u : 0u) << u;
+      sidx[j] = (uint32_t)(sS == 0 ? lb[u] : ub[u]);
+    }
+  }
+  {  // exclusive scan of the kept counts, thread order = element order
+    const uint32_t c = __popc(flags);
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int i = 0; i < kMWaves; i++) {
+        const uint32_t v = red[i];
+        red[i] = acc;
+        acc += v;
+      }
+      red[kMWaves] = acc;
+    }
+    __syncthreads();
+    uint32_t base = red[w] + incl - c;
+#pragma unroll
+    for (int u = 0; u < kMU; u++) {
+      const uint32_t j = tid * kMU + u;
+      if (j < ns) skp[j] = base;
+      base += (flags >> u) & 1u;
+    }
+    if (tid == 0) skp[ns] = red[kMWaves];
+  }
+  __syncthreads();
+  const uint32_t KS = skp[ns];
+  // L: stream tiles in index order
+  uint32_t KL = 0, jlo = 0;
+  for (uint64_t tb = 0; tb < nl; tb += kMTile) {
+    uint32_t x[kML];
+    uint64_t lbs[kML], ubs[kML];
+    bool valid[kML];
+#pragma unroll
+    for (int s = 0; s < kML; s++) {
+      const uint64_t i = tb + (uint64_t)s * kMT + tid;
+      valid[s] = i < nl;
+      x[s] = valid[s] ? L[i] : kSent;
+    }
+    multi_bound<kML, false>(sv, ns, x, lbs);
+    multi_bound<kML, true>(sv, ns, x, ubs);
+    bool kp[kML];
+#pragma unroll
+    for (int s = 0; s < kML; s++) {
+      const uint64_t i = tb + (uint64_t)s * kMT + tid;
+      uint64_t t = 0;
+      if (valid[s] && i > 0 && L[i - 1] == x[s]) {  // later copy (rare): first index by search
+        uint64_t lo = 0, hi = i;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (L[mid] < x[s]) lo = mid + 1; else hi = mid;
+        }
+        t = i - lo;
+      }
+      kp[s] = valid[s] && x[s] != kSent && keep_rule(m.op, sL, t, ubs[s] - lbs[s]);
+      const unsigned long long bw = __ballot(kp[s]);
+      if (lane == 0) tw[s * kMWaves + w] = bw;
+    }
+    __syncthreads();
+    if (tid < 64) {  // word prefix over the tile (index order = (s, wave))
+      const uint32_t c = tid < kML * kMWaves ? (uint32_t)__popcll(tw[tid]) : 0u;
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (tid < kML * kMWaves) twp[tid] = KL + incl - c;
+      if (tid == kML * kMWaves - 1) twp[kML * kMWaves] = KL + incl;
+    }
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+    for (int s = 0; s < kML; s++)
+      if (kp[s]) {
+        const uint32_t q = s * kMWaves + w;
+        const uint32_t rank = twp[q] + (uint32_t)__popcll(tw[q] & below);
+        out[rank + skp[sL == 0 ? lbs[s] : ubs[s]]] = x[s];
+      }
+    // S elements whose insertion point lies in this tile
+    uint32_t jhi;
+    {
+      uint32_t lo = jlo, hi = ns;
+      const uint64_t end = tb + kMTile;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sidx[mid] < end) lo = mid + 1; else hi = mid;
+      }
+      jhi = lo;
+    }
+    for (uint32_t j = jlo + tid; j < jhi; j += kMT)
+      if (skp[j + 1] > skp[j]) {
+        const uint32_t p = (uint32_t)(sidx[j] - tb), q = (p / kMT) * kMWaves + (p % kMT) / 64, bit = p % 64;
+        const uint32_t kb = twp[q] + (uint32_t)__popcll(tw[q] & ((1ull << bit) - 1));
+        out[skp[j] + kb] = sv[j];
+      }
+    KL = twp[kML * kMWaves];
+    jlo = jhi;
+    __syncthreads();
+  }
+  for (uint32_t j = jlo + tid; j < ns; j += kMT)  // insertion point past the end of L
+    if (skp[j + 1] > skp[j]) out[skp[j] + KL] = sv[j];
+  if (tid == 0) m.olen[k] = (uint64_t)KS + KL;
+}
+
 __global__ void k_merge_len(MergeArgs m) {
   uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m.npair) return;
@@ -411,6 +637,8 @@ static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, con
     boff[k + 1] = boff[k] + b_len[k];
   }
   bool bside = op == SG_OP_UNION || op == SG_OP_SYMDIFF;
+  bool small = bside;  // every pair has a side that fits in LDS: one workgroup per pair
+  for (size_t k = 0; k < npair && small; k++) small = std::min(a_len[k], b_len[k]) <= (uint64_t)kMS;
   uint64_t na = aoff[npair], nb = bside ? boff[npair] : 0;
   uint64_t nca = ((na + kTile - 1) / kTile) * kChunksPerTile, ncb = ((nb + kTile - 1) / kTile) * kChunksPerTile;
   WsPlan p;
@@ -438,6 +666,22 @@ static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, con
   SG_HIP(hipMemcpyAsync(m_blen, b_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_boff, boff.data(), (npair + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_obeg, out_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  if (small) {
+    SmallArgs sm{op, da, db, m_abeg, m_alen, m_bbeg, m_blen, m_obeg, m_olen, dout};
+    {
+      ScopedTimer tm(ctx, "merge_small");
+      hipLaunchKernelGGL(k_merge_small, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
+    }
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipMemcpyAsync(out_len, m_olen, npair * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    for (size_t k = 0; k < npair; k++)
+      if (out_len[k])
+        SG_HIP(hipMemcpyAsync(out + out_beg[k], dout + out_beg[k], out_len[k] * 4, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return SG_OK;
+  }
   MergeArgs m{};
   m.op = op;
   m.a = {da, m_abeg, m_alen, m_aoff};

@@ -89,6 +89,39 @@ def test_ops_large_multiset(C):
         assert C.HasDifference(b, a) == O.has_difference(b, a)
 
 
+def test_merge_batch_small_side_multisets(C):
+    """The one-small-side merge (sg_merge.hip k_merge_small): pairs whose
+    small list fits in LDS against large lists with long runs of one value
+    (across its 4096-element tiles), sentinels on both sides, either side
+    small, and a mix with a pair too large for it (generic path)."""
+    rng = np.random.default_rng(115)
+    lists = []
+    for it in range(24):
+        ns = int(rng.integers(0, 4097))
+        nl = int(rng.integers(0, 30000))
+        hi = [8, 300, 1 << 20, 1 << 32][it % 4]
+        small = np.sort(rng.integers(0, hi, size=ns, dtype=np.uint64)).astype(np.uint32)
+        large = rng.integers(0, hi, size=nl, dtype=np.uint64)
+        if it % 3 == 0 and nl:  # a run of one value over several tiles
+            large[: nl // 2] = large[0]
+        large = np.sort(large).astype(np.uint32)
+        if it % 5 == 0:
+            small = np.sort(np.concatenate([small, np.full(2, SENT, np.uint32)]))
+        if it % 4 == 1:
+            large = np.sort(np.concatenate([large, np.full(3, SENT, np.uint32)]))
+        lists.append((small, large) if it % 2 else (large, small))
+    for op in range(4):
+        a = np.concatenate([x for x, _ in lists])
+        b = np.concatenate([y for _, y in lists])
+        al = np.array([x.size for x, _ in lists], np.uint64)
+        bl = np.array([y.size for _, y in lists], np.uint64)
+        ab = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.uint64)
+        bb = np.concatenate([[0], np.cumsum(bl)[:-1]]).astype(np.uint64)
+        outs = C.merge_batch(op, a, ab, al, b, bb, bl)
+        for k, (x, y) in enumerate(lists):
+            assert np.array_equal(outs[k], O.foreach(op, x, y)), (op, k, x.size, y.size)
+
+
 def test_has_difference_property(C):
     # cover_test.go:210-221
     rng = np.random.default_rng(102)
