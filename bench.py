@@ -66,20 +66,70 @@ class Poll:
     """newSignal drain + manager merge (fuzzer.go:358-364, manager.go:949-962,
     fuzzer.go:392-398): every rank's maxSignal gains every other rank's new
     signal.  Bitmaps are OR-reduced with an all-to-all of 1/N shards, a local
-    OR, and an all-gather (RCCL has no bitwise-OR reduction)."""
+    OR, and an all-gather (RCCL has no bitwise-OR reduction).
 
-    def __init__(self, world, newbuf):
+    The reference polls on its own timer (every 10 s or when candidates run
+    low, fuzzer.go:331-346): triage never waits for a Poll, and other fuzzers'
+    signal reaches maxSignal at arbitrary points.  So the exchange runs one
+    step behind, on a stream of its own:
+      step k triages into newSignal buffer k % 2;
+      that buffer is exchanged while step k + 1 triages into the other one;
+      before step k + 2 the merged bits are OR-ed into maxSignal and the buffer
+      is cleared (the drain).
+    drain() finishes every pending exchange (inside the timed region).  At N=1
+    there is no exchange and the buffer is just drained each step, unless
+    `selftest` runs the same streams and events with an identity exchange."""
+
+    def __init__(self, ctx, world, selftest=False):
         from syzkaller_amd.dist import OrExchange
 
         self.world = world
-        self.newbuf = newbuf
-        self.ex = OrExchange(newbuf) if world > 1 else None
+        self.bufs = [torch.zeros(U32_WORDS, dtype=torch.int32, device="cuda") for _ in range(2)]
+        self.sets = []
+        for buf in self.bufs:
+            h = ctypes_void_p()
+            call("sg_set_wrap_dev", ctx.h, buf.data_ptr(), ctypes_byref(h))
+            self.sets.append(_Wrapped(h))
+        self.active = world > 1 or selftest
+        self.k = 0
+        if self.active:
+            self.comm = torch.cuda.Stream()
+            self.ex = [OrExchange(buf) if world > 1 else None for buf in self.bufs]
+            self.merged = [None, None]
+            self.done = [None, None]
 
-    def __call__(self, maxsig):
-        if self.ex is not None:
-            merged = self.ex(self.newbuf)
-            call("sg_set_or_dev", maxsig.h, merged.data_ptr())
-        self.newbuf.zero_()
+    def newsig(self):
+        """The newSignal set step k triages into."""
+        return self.sets[self.k % 2]
+
+    def after_triage(self, maxsig):
+        """Call once step k's triage is queued on the compute stream."""
+        slot = self.k % 2
+        self.k += 1
+        if not self.active:
+            self.bufs[slot].zero_()  # drained (fuzzer.go:358-364)
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ev)
+            merged = self.ex[slot](self.bufs[slot]) if self.ex[slot] is not None else self.bufs[slot]
+            done = torch.cuda.Event()
+            done.record(self.comm)
+        self.merged[slot], self.done[slot] = merged, done
+        self._apply(self.k % 2, maxsig)  # the slot the next step triages into
+
+    def _apply(self, slot, maxsig):
+        if not self.active or self.done[slot] is None:
+            return
+        torch.cuda.current_stream().wait_event(self.done[slot])
+        call("sg_set_or_dev", maxsig.h, self.merged[slot].data_ptr())  # fuzzer.go:392-398
+        self.bufs[slot].zero_()
+        self.done[slot] = None
+
+    def drain(self, maxsig):
+        for d in (1, 0):  # the older pending exchange first
+            self._apply((self.k + d) % 2, maxsig)
 
 
 def triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off):
@@ -199,6 +249,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-account", action="store_true", help="skip the byte-accounting replay")
     ap.add_argument("--diff", action="store_true", help="also emit the ordered diff lists (claim/resolve path)")
+    ap.add_argument("--poll-selftest", action="store_true",
+                    help="N=1: run the pipelined Poll's streams and events with an identity exchange")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -231,11 +283,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
 
     maxsig = SignalSet(ctx)
-    newbuf = torch.zeros(U32_WORDS, dtype=torch.int32, device="cuda")
-    h = ctypes_void_p()
-    call("sg_set_wrap_dev", ctx.h, newbuf.data_ptr(), ctypes_byref(h))
-    newsig = _Wrapped(h)
-    poll = Poll(world, newbuf)
+    poll = Poll(ctx, world, selftest=args.poll_selftest)
 
     # M0: triage the warm batch program-chunk by program-chunk until >= --m0 entries
     maxnrec = max(b.nrec for b in batches)
@@ -264,10 +312,11 @@ def main():
     gpu_flags0 = None
     dv_t, do_t = (diff_vals, diff_off) if args.diff else (None, None)
     for k in range(args.warmup):
-        triage_step(ctx, maxsig, newsig, batches[k], rec_new, dv_t, do_t)
+        triage_step(ctx, maxsig, poll.newsig(), batches[k], rec_new, dv_t, do_t)
         if k == 0:
             gpu_flags0 = rec_new[: batches[0].nrec].cpu().numpy()
-        poll(maxsig)
+        poll.after_triage(maxsig)
+    poll.drain(maxsig)
     torch.cuda.synchronize()
 
     # snapshot the state for the byte-accounting replay
@@ -285,8 +334,9 @@ def main():
     ctx.timing(True)
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
-        triage_step(ctx, maxsig, newsig, batches[k], rec_new, dv_t, do_t)
-        poll(maxsig)
+        triage_step(ctx, maxsig, poll.newsig(), batches[k], rec_new, dv_t, do_t)
+        poll.after_triage(maxsig)
+    poll.drain(maxsig)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -311,7 +361,8 @@ def main():
     acct = None
     if backup is not None:
         call("sg_set_copy", maxsig.h, backup.h)
-        newbuf.zero_()
+        for buf in poll.bufs:
+            buf.zero_()
         torch.cuda.synchronize()
         n_in = n_cand = n_diff = n_rec = n_new = n_queued = 0
         for k in range(args.warmup, args.warmup + args.steps):
@@ -320,7 +371,7 @@ def main():
             call("sg_set_count_missing_dev", maxsig.h, b.vals.data_ptr(), b.nvals, ctypes_byref(c))
             m_before = len(maxsig)
             # the diff path here, so the diff element count is known too
-            triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off)
+            triage_step(ctx, maxsig, poll.newsig(), b, rec_new, diff_vals, diff_off)
             torch.cuda.synchronize()
             n_diff += int(diff_off[b.nrec].item())
             n_queued += int(rec_new[: b.nrec].sum().item())
@@ -328,7 +379,8 @@ def main():
             n_in += b.nvals
             n_cand += c.value
             n_rec += b.nrec
-            poll(maxsig)
+            poll.after_triage(maxsig)
+        poll.drain(maxsig)
         torch.cuda.synchronize()
         acct = {"n_in": n_in, "n_cand": n_cand, "n_diff": n_diff, "n_rec": n_rec, "n_new_signal": n_new,
                 "n_queued": n_queued}
@@ -382,8 +434,8 @@ def main():
                 "signal_per_step_per_gpu": total_units / args.steps / world,
                 "maxsignal_start": m0_count, "maxsignal_at_timing": m_start,
                 "new_signal_per_step": per_step_new,
-                "parallelism": f"signal-replicated x{world}, newSignal OR-exchange per step" if world > 1
-                else "single GPU",
+                "parallelism": f"one fuzzer per GPU x{world}, newSignal OR-exchange (RCCL all-to-all + all-gather) "
+                               f"per step, pipelined one step behind" if world > 1 else "single GPU",
             },
             "roofline": roof,
             "cpu_baseline": cpu,
