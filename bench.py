@@ -148,11 +148,11 @@ KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "b
 
 def part_geometry(n_in, n_rec):
     """Tile / chunk counts of the partitioned path (sg_bucket.hip BucketPlan):
-    pass-1 tiles, and pass-2 chunks (about one per non-empty group of 240
-    tiles x 256 slices for spread-out signal)."""
+    pass-1 tiles (8192 entries / 64 records each), and pass-2 chunks (about
+    one per non-empty group of 1020 tiles x 256 slices for spread-out signal)."""
     na = -(-int(n_in) // 8192)
-    t = na + (int(n_rec) - 1) // 256
-    kt = -(-t // 240)
+    t = na + (int(n_rec) - 1) // 64
+    kt = -(-t // 1020)
     return t, 256 * kt
 
 

@@ -48,11 +48,19 @@ constexpr int kPThreads = 512;               // 8 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
-constexpr uint32_t kRecCap = 256;            // records per pass-1 tile (8-bit index)
-// pass-1 tiles per pass-2 group (8-bit index).  A full tile puts ~kPT/256
-// entries into each slice, so a group is ~kGroupTiles * 32 entries: 240 keeps
-// it just under one kPT chunk for uniformly spread signal.
-constexpr uint32_t kGroupTiles = 240;
+// Entry layouts.  Pass 1: s << 8 | record-in-tile.  Pass 2: (s & 0xFFFF) << 16
+// | tile-in-group << kRelBits | record-in-tile.  A pass-1 tile spans at most
+// kRecCap records; a pass-2 group at most kGroupTiles tiles of one slice.
+// 6 + 10 bits: records are long in practice (C2: ~840 entries), and groups
+// of ~1000 tiles keep even a thin slice's pass-2 chunks near kPT entries.
+constexpr uint32_t kRelBits = 6;
+constexpr uint32_t kRecCap = 1u << kRelBits;       // records per pass-1 tile
+constexpr uint32_t kTileRelBits = 16 - kRelBits;
+constexpr uint32_t kGroupTiles = 1020;             // pass-1 tiles per pass-2 group (< 2^kTileRelBits)
+static_assert(kGroupTiles < (1u << kTileRelBits), "tile-in-group field");
+// owner key of an entry: pass-1 tile << kRelBits | record-in-tile
+__host__ __device__ constexpr uint32_t entry2_tilerel(uint32_t x) { return (x >> kRelBits) & ((1u << kTileRelBits) - 1); }
+__host__ __device__ constexpr uint32_t entry2_rel(uint32_t x) { return x & (kRecCap - 1); }
 constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
 constexpr int kBThreads = 512;
@@ -295,32 +303,34 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
 
 // O(1) "largest k with st[k] <= p" inside one tile of <= kPT positions, for
 // sorted segment starts st[0..m) given tile-relative and clamped to [0, kPT]
-// (st[0] == 0, m <= 256).  Non-empty segments that start inside the tile are
+// (st[0] == 0, m < 2^16).  Non-empty segments that start inside the tile are
 // marked: bit p of sbits <=> one starts at p > 0, sidx[p] = its index;
 // wmax[w] = index of the segment holding position 32w + 31; kinit = the
 // segment holding position 0.  Replaces a per-entry search (segments can be
 // a few entries long: small records, thin slices).
+template <typename IdxT>
 struct SegLds {
   uint32_t sbits[kPT / 32];
-  uint8_t wmax[kPT / 32];
+  IdxT wmax[kPT / 32];
   uint32_t kinit;
 };
 
-__device__ __forceinline__ void seg_clear(SegLds& L, int tid) {
+template <typename IdxT>
+__device__ __forceinline__ void seg_clear(SegLds<IdxT>& L, int tid) {
   for (int w = tid; w < kPT / 32; w += kPThreads) L.sbits[w] = 0;
   if (tid == 0) L.kinit = 0;
 }
 
 // call after seg_clear + a barrier; ends with a barrier
-template <typename S>
-__device__ __forceinline__ void seg_build(SegLds& L, uint8_t* sidx, const S* st, uint32_t m, uint32_t n, int tid) {
+template <typename IdxT, typename S>
+__device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, const S* st, uint32_t m, uint32_t n, int tid) {
   for (uint32_t k = tid; k < m; k += kPThreads) {
     const uint32_t p = st[k], nx = k + 1 < m ? (uint32_t)st[k + 1] : 0xFFFFFFFFu;
     if (p == 0) {
       if (nx > 0) atomicMax(&L.kinit, k);
     } else if (p < n && nx > p) {
       atomicOr(&L.sbits[p >> 5], 1u << (p & 31));
-      sidx[p] = (uint8_t)k;
+      sidx[p] = (IdxT)k;
     }
   }
   __syncthreads();
@@ -344,12 +354,13 @@ __device__ __forceinline__ void seg_build(SegLds& L, uint8_t* sidx, const S* st,
     if (tid == 0) ex = -1;
     ex = max(ex, (int)L.kinit);
 #pragma unroll
-    for (int j = 0; j < 4; j++) L.wmax[tid * 4 + j] = (uint8_t)max(ex, loc[j]);
+    for (int j = 0; j < 4; j++) L.wmax[tid * 4 + j] = (IdxT)max(ex, loc[j]);
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t seg_lookup(const SegLds& L, const uint8_t* sidx, uint32_t p) {
+template <typename IdxT>
+__device__ __forceinline__ uint32_t seg_lookup(const SegLds<IdxT>& L, const IdxT* sidx, uint32_t p) {
   const uint32_t w = p >> 5;
   const uint32_t m = L.sbits[w] & (0xFFFFFFFFu >> (31 - (p & 31)));
   return m ? sidx[(w << 5) + 31 - __clz(m)] : (w ? L.wmax[w - 1] : L.kinit);
@@ -376,7 +387,7 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
-  __shared__ SegLds L;
+  __shared__ SegLds<uint8_t> L;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
@@ -462,7 +473,8 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t runs[kGroupTiles + 1];  // chunk-relative run starts of the group's tiles in this slice
-  __shared__ SegLds L;
+  __shared__ SegLds<uint16_t> L;
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(stage);  // tile-in-group index; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint4 dsc = a.desc[blockIdx.x];
   const uint32_t s0 = dsc.x, s1 = dsc.y, gov = dsc.z, c = dsc.w;
@@ -491,14 +503,14 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   seg_clear(L, tid);
   __syncthreads();
   const uint32_t nt = s1 - s0;
-  seg_build(L, sdig, runs, ntl, nt, tid);  // sdig doubles as the segment index until the rank
+  seg_build(L, sidx, runs, ntl, nt, tid);
   uint32_t dv[kSteps], pk[kSteps];
   const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint32_t k1 = ((vmask >> k) & 1u) ? seg_lookup(L, sdig, el0 + k * 64) : 0u;  // tile in group
+    const uint32_t k1 = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // tile in group
     dv[k] = sv[k] >> 24;
-    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (k1 << 8) | (sv[k] & 0xFFu);
+    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (k1 << kRelBits) | (sv[k] & (kRecCap - 1));
   }
   uint32_t pos[kSteps];
   tile_rank(dv, vmask, cnt, gbase, pos);
@@ -586,8 +598,8 @@ __device__ __forceinline__ BucketRange bucket_range(const BucketArgs& a, uint32_
 // record of the pass-2 entry x at position o (chunk index within the slice: ci)
 __device__ __forceinline__ uint32_t entry_record(const BucketArgs& a, const BucketRange& r, uint32_t ci, uint32_t x) {
   const uint32_t gov = a.cgov[r.c0 + ci];
-  const uint32_t t1 = (gov % a.kt) * kGroupTiles + ((x >> 8) & 255u);
-  return a.trec[t1] + (x & 255u);
+  const uint32_t t1 = (gov % a.kt) * kGroupTiles + entry2_tilerel(x);
+  return a.trec[t1] + entry2_rel(x);
 }
 
 __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
@@ -635,11 +647,11 @@ __device__ __forceinline__ uint32_t cand_key(const BucketArgs& a, const BucketRa
     const uint32_t ci = (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
     t0 = (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
   }
-  return ((t0 + ((x >> 8) & 255u)) << 8) | (x & 255u);
+  return ((t0 + entry2_tilerel(x)) << kRelBits) | entry2_rel(x);
 }
 
 __device__ __forceinline__ uint32_t key_record(const BucketArgs& a, uint32_t key) {
-  return a.trec[key >> 8] + (key & 255u);
+  return a.trec[key >> kRelBits] + (key & (kRecCap - 1));
 }
 
 // Persistent: each workgroup takes buckets one after another (the first one
@@ -952,7 +964,7 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
             for (int k = 0; k < kBU; k++) xu = k == u ? x[k] : xu;
             const uint32_t ci = chunk_of(r, W, runs, p0 + u);
             ok &= hash_insert64(ht, nbits, xu >> 16,
-                                ((chunk_tile(a, r, W, tb, ci) + ((xu >> 8) & 255u)) << 8) | (xu & 255u));
+                                ((chunk_tile(a, r, W, tb, ci) + entry2_tilerel(xu)) << kRelBits) | entry2_rel(xu));
           }
       }
       // the next round in flight: this bucket's, or the next bucket's first
@@ -981,7 +993,8 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
           while (ci + 1 < W.wc + W.wn && runs[ci + 1 - W.wc] <= i) ci++;
         else
           ci = chunk_of(r, W, runs, i);
-        ok &= hash_insert64(ht, nbits, xv >> 16, ((chunk_tile(a, r, W, tb, ci) + ((xv >> 8) & 255u)) << 8) | (xv & 255u));
+        ok &= hash_insert64(ht, nbits, xv >> 16,
+                            ((chunk_tile(a, r, W, tb, ci) + entry2_tilerel(xv)) << kRelBits) | entry2_rel(xv));
       }
 #endif
       const bool fail = __syncthreads_or(!ok);
@@ -1113,7 +1126,7 @@ __global__ void k_key_records(const uint32_t* __restrict__ kflag4, const uint32_
   if (w >= nwords) return;
   const uint32_t f = kflag4[w];
   if (!f) return;
-  const uint32_t key0 = (uint32_t)(w * 4), r0 = trec[key0 >> 8] + (key0 & 255u);
+  const uint32_t key0 = (uint32_t)(w * 4), r0 = trec[key0 >> kRelBits] + (key0 & (kRecCap - 1));
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if ((f >> (8 * j)) & 255u) rec_new[r0 + j] = 1;
@@ -1291,7 +1304,7 @@ struct BucketPlan {
     oV2 = p.add(n * 4 + 64);  // the bucket kernel's 16-B loads may read past the end
     oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
     oTK = p.add(4);
-    oKF = p.add(T * 256);
+    oKF = p.add(T * kRecCap);
     oBN = p.add((uint64_t)kNumBuckets * 4);
     oBP = p.add(((uint64_t)kNumBuckets + 1) * 4);
     oLB = p.add((uint64_t)kNumBuckets * 4);
@@ -1444,7 +1457,7 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   ba.spill = nspill + 1;
   ba.ticket = (uint32_t*)ws_at(ctx, bp.oTK);
   ba.kflag = (uint8_t*)ws_at(ctx, bp.oKF);
-  SG_HIP(hipMemsetAsync(ba.kflag, 0, bp.T * 256, ctx->stream));
+  SG_HIP(hipMemsetAsync(ba.kflag, 0, bp.T * kRecCap, ctx->stream));
   const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false>, kBThreads);
   uint64_t* ddbg = nullptr;
   if (dbg) {
@@ -1478,8 +1491,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   {
     ScopedTimer tm(ctx, "key_records");
-    hipLaunchKernelGGL(k_key_records, dim3(div_up(bp.T * 64, 256)), dim3(256), 0, ctx->stream,
-                       (const uint32_t*)ba.kflag, (const uint32_t*)trec, bp.T * 64, d_rec_new);
+    hipLaunchKernelGGL(k_key_records, dim3(div_up(bp.T * kRecCap / 4, 256)), dim3(256), 0, ctx->stream,
+                       (const uint32_t*)ba.kflag, (const uint32_t*)trec, bp.T * kRecCap / 4, d_rec_new);
   }
   SG_HIP(hipGetLastError());
   if (getenv("SG_DEBUG_PART")) {  // diagnostics: chunk and spill counts (syncs)

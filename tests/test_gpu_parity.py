@@ -339,9 +339,10 @@ def test_triage_edge_cases(C):
 
 def test_triage_partition_geometry(C):
     """Inputs aimed at the partitioned path's tables (sg_bucket.hip): tiles cut
-    by the 256-record cap, runs of >= 256 empty records (coinciding cuts),
-    record counts around multiples of 256, one slice holding the whole batch,
-    and a 2^16-signal bucket with more distinct candidates than its LDS map."""
+    by the 64-record cap (kRecCap), runs of >= 64 empty records (coinciding
+    cuts), record counts around multiples of 64, several pass-2 groups of 1020
+    tiles (kGroupTiles), one slice holding the whole batch, and a 2^16-signal
+    bucket with more distinct candidates than its LDS map."""
     P = TwoPaths(C)
     om, on = O.OSet(), O.OSet()
     rng = np.random.default_rng(113)
@@ -354,13 +355,16 @@ def test_triage_partition_geometry(C):
     # tiny records: every tile hits the record cap long before 8192 entries
     lens = rng.integers(0, 4, size=40000)
     run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
-    # >= 256 consecutive empty records, at and around cap boundaries
-    for nrec in (255, 256, 257, 511, 512, 513, 1024):
+    # ~3200 tiles: four pass-2 groups, the last one partial
+    lens = rng.integers(0, 3, size=200000)
+    run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
+    # >= 64 consecutive empty records, at and around cap boundaries
+    for nrec in (63, 64, 65, 127, 128, 129, 255, 256, 257, 1024):
         lens = np.zeros(nrec, np.int64)
         lens[rng.integers(0, nrec, size=5)] = rng.integers(1, 3000, size=5)
         lens[-1] += 7
         run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
-    lens = np.concatenate([np.full(300, 0), [9000], np.full(700, 0), [20000], np.full(256, 0), [3]])
+    lens = np.concatenate([np.full(300, 0), [9000], np.full(700, 0), [20000], np.full(64, 0), [3], np.full(130, 0), [5]])
     run(rng.integers(0, 1 << 32, size=int(lens.sum()), dtype=np.uint64), lens)
     # one top byte (slice) for everything: long runs, many chunks in one slice
     n = 3_000_000
