@@ -186,86 +186,124 @@ __global__ void k_chunk_desc(const uint32_t* __restrict__ cstart, const uint32_t
 }
 
 // --------------------------------------------------------- byte histogram ---
-// hist[(v >> 24) * ncols + tile] = count over entries [start[tile], start[tile+1]).
-// kVec (v 16-B aligned): whole aligned quads by uint4 loads, the <= 3 entries
-// before the first and after the last quad by single loads.
+// hist[(v >> 24) * ncols + col] = count over one job's entries [s0, s1).
+// Pass 1: job = tile t = xcd_tile(bid, T), [start[t], start[t+1]), T columns.
+// Pass 2: job = the block's chunk descriptor, *ncols_dev columns; blocks
+// without a chunk exit.  16-B aligned input (always, for pass 2) goes through
+// k_hist_rep; k_p1_hist covers an unaligned caller buffer.
 constexpr int kHistQ = kPT / 4 / kPThreads;  // uint4 loads per lane
-// Pass 1: tile t = xcd_tile(bid, grid), range [start[t], start[t+1]), T =
-// grid columns.  Pass 2 (desc != nullptr): the block's chunk descriptor and
-// *ncols_dev columns; blocks without a chunk exit.
-template <bool kVec>
-__device__ __forceinline__ void hist_top(const uint32_t* __restrict__ v, const uint32_t* __restrict__ start,
-                                         const uint4* __restrict__ desc, const uint32_t* __restrict__ ncols_dev,
-                                         uint32_t* __restrict__ hist) {
+
+__global__ __launch_bounds__(kPThreads) void k_p1_hist(const uint32_t* __restrict__ v,
+                                                       const uint32_t* __restrict__ start, uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[256];
-  uint32_t t, s0, s1, ncols;
-  if (desc) {
-    const uint4 d = desc[blockIdx.x];
-    s0 = d.x;
-    s1 = d.y;
-    t = d.w;
-    if (s0 >= s1) return;
-    ncols = *ncols_dev;
-  } else {
-    ncols = gridDim.x;
-    t = xcd_tile(blockIdx.x, ncols);
-    s0 = start[t];
-    s1 = start[t + 1];
-  }
+  const uint32_t ncols = gridDim.x, t = xcd_tile(blockIdx.x, ncols), s0 = start[t], s1 = start[t + 1];
   const int tid = threadIdx.x;
   if (tid < 256) cnt[tid] = 0;
-  if (kVec) {
-    const uint4* v4 = reinterpret_cast<const uint4*>(v);
-    const uint32_t q0 = (s0 + 3) >> 2, q1 = s1 >> 2;  // whole quads [q0, q1)
-    uint4 x[kHistQ + 1];
+  uint32_t x[kPT / kPThreads];
 #pragma unroll
-    for (int k = 0; k <= kHistQ; k++) {
-      const uint32_t q = q0 + k * kPThreads + tid;
-      x[k] = q < q1 ? v4[q] : make_uint4(0, 0, 0, 0);
-    }
-    // head (entries before quad q0) and tail (after quad q1), at most 3 each
-    uint32_t e1 = 0xFFFFFFFFu, y = 0;
-    if (tid < 3) e1 = s0 + tid < q0 * 4 && s0 + tid < s1 ? s0 + tid : 0xFFFFFFFFu;
-    else if (tid < 6) e1 = q1 * 4 + (tid - 3) < s1 && q1 * 4 + (tid - 3) >= s0 && q1 >= q0 ? q1 * 4 + (tid - 3)
-                                                                                         : 0xFFFFFFFFu;
-    if (e1 != 0xFFFFFFFFu) y = v[e1];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k <= kHistQ; k++)
-      if (q0 + k * kPThreads + tid < q1) {
-        atomicAdd(&cnt[x[k].x >> 24], 1u);
-        atomicAdd(&cnt[x[k].y >> 24], 1u);
-        atomicAdd(&cnt[x[k].z >> 24], 1u);
-        atomicAdd(&cnt[x[k].w >> 24], 1u);
-      }
-    if (e1 != 0xFFFFFFFFu) atomicAdd(&cnt[y >> 24], 1u);
-  } else {
-    uint32_t x[kPT / kPThreads];
-#pragma unroll
-    for (int k = 0; k < kPT / kPThreads; k++) {
-      const uint32_t e = s0 + k * kPThreads + tid;
-      x[k] = e < s1 ? v[e] : 0u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPT / kPThreads; k++)
-      if (s0 + k * kPThreads + tid < s1) atomicAdd(&cnt[x[k] >> 24], 1u);
+  for (int k = 0; k < kPT / kPThreads; k++) {
+    const uint32_t e = s0 + k * kPThreads + tid;
+    x[k] = e < s1 ? v[e] : 0u;
   }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPT / kPThreads; k++)
+    if (s0 + k * kPThreads + tid < s1) atomicAdd(&cnt[x[k] >> 24], 1u);
   __syncthreads();
   if (tid < 256) hist[(uint64_t)tid * ncols + t] = cnt[tid];
 }
 
-// the two passes' histograms as kernels of their own names (profiles)
-template <bool kVec>
-__global__ __launch_bounds__(kPThreads) void k_p1_hist(const uint32_t* __restrict__ v,
-                                                       const uint32_t* __restrict__ start, uint32_t* __restrict__ hist) {
-  hist_top<kVec>(v, start, nullptr, nullptr, hist);
+// Aligned-input histogram jobs: [s0, s1) of the input, output column col.
+struct HistJob {
+  uint32_t s0, s1, col;
+};
+
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct HistRegs {
+  uint4 x[kHistQ + 1];
+  uint32_t y;
+};
+
+// threads 0-2 take the entries before quad q0, threads 3-5 those after quad q1
+__device__ __forceinline__ uint32_t hist_edge(const HistJob& h, int tid) {
+  const uint32_t q0 = (h.s0 + 3) >> 2, q1 = h.s1 >> 2;
+  if (tid < 3) return h.s0 + tid < q0 * 4 && h.s0 + tid < h.s1 ? h.s0 + tid : 0xFFFFFFFFu;
+  if (tid < 6) {
+    const uint32_t e = q1 * 4 + (tid - 3);
+    return e < h.s1 && e >= h.s0 && q1 >= q0 ? e : 0xFFFFFFFFu;
+  }
+  return 0xFFFFFFFFu;
 }
 
-__global__ __launch_bounds__(kPThreads) void k_p2_hist(const uint32_t* __restrict__ v, const uint4* __restrict__ desc,
-                                                       const uint32_t* __restrict__ ncols_dev,
-                                                       uint32_t* __restrict__ hist) {
-  hist_top<true>(v, nullptr, desc, ncols_dev, hist);
+// Unconditional buffer loads: the descriptor spans exactly the job's whole
+// quads (resp. its entries), and the range check returns 0 past the end.
+__device__ __forceinline__ void hist_load(const uint32_t* __restrict__ v, const HistJob& h, int tid, HistRegs& r) {
+  const uint32_t s0 = rfl(h.s0), s1 = rfl(h.s1);
+  const uint32_t q0 = (s0 + 3) >> 2, q1 = s1 >> 2;
+  const uint32_t qbytes = q1 > q0 ? (q1 - q0) * 16u : 0u;
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(v + (uint64_t)q0 * 4), 0, (int)qbytes, 0x00020000);
+#pragma unroll
+  for (int k = 0; k <= kHistQ; k++) {
+    const v4u32 t = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(k * kPThreads + tid) * 16u, 0, 0);
+    r.x[k] = make_uint4(t[0], t[1], t[2], t[3]);
+  }
+  const __amdgpu_buffer_rsrc_t re =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(v + s0), 0, (int)((s1 - s0) * 4u), 0x00020000);
+  const uint32_t e = hist_edge(h, tid);
+  r.y = __builtin_amdgcn_raw_buffer_load_b32(re, (e - s0) * 4u, 0, 0);
+}
+
+// Bank-replicated counting: 32 copies of the 256 counters, copy = lane & 31,
+// laid out so that counter (d, copy) sits in LDS bank copy: the 32 lanes of
+// a half-wave always hit 32 distinct banks (a shared 256-counter table sees
+// ~3.5-way conflicts per half-wave on random digits).  The copies are summed
+// per digit at the end, each lane starting at a different copy.
+template <bool kP2>
+__global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restrict__ v,
+                                                        const uint32_t* __restrict__ start,
+                                                        const uint4* __restrict__ desc, uint32_t njobs,
+                                                        const uint32_t* __restrict__ ncols_dev,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t rc[256 * 32];
+  const int tid = threadIdx.x;
+  HistJob h;
+  if (kP2) {
+    const uint4 d = desc[blockIdx.x];
+    h.s0 = d.x;
+    h.s1 = d.y;
+    h.col = d.w;
+    if (h.s0 >= h.s1) return;
+  } else {
+    h.col = xcd_tile(blockIdx.x, njobs);
+    h.s0 = start[h.col];
+    h.s1 = start[h.col + 1];
+  }
+  const uint32_t ncols = kP2 ? *ncols_dev : njobs;
+  HistRegs r;
+  hist_load(v, h, tid, r);
+#pragma unroll
+  for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const uint32_t q0 = (h.s0 + 3) >> 2, q1 = h.s1 >> 2, cp = tid & 31;
+#pragma unroll
+  for (int k = 0; k <= kHistQ; k++)
+    if (q0 + k * kPThreads + tid < q1) {
+      atomicAdd(&rc[(r.x[k].x >> 24) * 32 + cp], 1u);
+      atomicAdd(&rc[(r.x[k].y >> 24) * 32 + cp], 1u);
+      atomicAdd(&rc[(r.x[k].z >> 24) * 32 + cp], 1u);
+      atomicAdd(&rc[(r.x[k].w >> 24) * 32 + cp], 1u);
+    }
+  if (hist_edge(h, tid) != 0xFFFFFFFFu) atomicAdd(&rc[(r.y >> 24) * 32 + cp], 1u);
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) sum += rc[tid * 32 + ((k + tid) & 31)];
+    hist[(uint64_t)tid * ncols + h.col] = sum;
+  }
 }
 
 // Counting sort of one tile held in registers (kSteps entries per lane) by an
@@ -1388,10 +1426,10 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   {
     ScopedTimer tm(ctx, "p1_hist");
     if (((uintptr_t)d_vals & 15) == 0)
-      hipLaunchKernelGGL(k_p1_hist<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
-                         (const uint32_t*)tstart, hist1);
+      hipLaunchKernelGGL(k_hist_rep<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+                         (const uint32_t*)tstart, (const uint4*)nullptr, T, (const uint32_t*)nullptr, hist1);
     else
-      hipLaunchKernelGGL(k_p1_hist<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
+      hipLaunchKernelGGL(k_p1_hist, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
                          (const uint32_t*)tstart, hist1);
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
@@ -1431,8 +1469,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
                      (const uint32_t*)cgov, gcount, bp.gmax, cdesc);
   {
     ScopedTimer tm(ctx, "p2_hist");
-    hipLaunchKernelGGL(k_p2_hist, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
-                       (const uint4*)cdesc, gcount, hist2);
+    hipLaunchKernelGGL(k_hist_rep<true>, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
+                       (const uint32_t*)nullptr, (const uint4*)cdesc, G, gcount, hist2);
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
   if (rc) return rc;

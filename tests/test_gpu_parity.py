@@ -495,3 +495,37 @@ def test_cover_uncovered_vs_oracle(C):
         got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
         exp = O.cover_uncovered(q, 0xffffffff, starts, ends, sites)
         assert np.array_equal(got, exp), nsym
+
+
+def test_triage_dev_unaligned_input(C):
+    """sg_triage_batch_dev on caller buffers that are not 16-B aligned (the
+    pass-1 histogram then takes its scalar-load kernel): flags and set
+    updates equal the oracle's."""
+    import torch
+    from syzkaller_amd._lib import call
+
+    rng = np.random.default_rng(121)
+    lens = rng.integers(0, 3000, size=700)
+    n = int(lens.sum())
+    vals = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    vals[rng.integers(0, n, size=n // 3)] = vals[rng.integers(0, n, size=n // 3)]  # cross-record repeats
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    m0 = np.unique(vals[rng.integers(0, n, size=n // 4)])
+    for shift in (1, 2, 3):
+        ms, ns = C.SignalSet(), C.SignalSet()
+        C.SignalAdd(ms, m0)
+        om, on = O.OSet(m0), O.OSet()
+        buf = torch.zeros(n + 4, dtype=torch.int32, device="cuda")
+        buf[shift:shift + n] = torch.from_numpy(vals.view(np.int32)).cuda()
+        dv = buf[shift:shift + n]
+        assert dv.data_ptr() % 16 != 0
+        doff = torch.from_numpy(off.view(np.int64)).cuda()
+        flags = torch.zeros(lens.size, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # the library queues on its own stream
+        call("sg_triage_batch_dev", ms.ctx.h, ms.h, ns.h, dv.data_ptr(), doff.data_ptr(), n, lens.size,
+             flags.data_ptr(), None, None)
+        ms.ctx.sync()
+        ef, _, _ = O.triage_batch(om, on, vals, off)
+        assert np.array_equal(flags.cpu().numpy().astype(bool), np.asarray(ef).astype(bool))
+        assert np.array_equal(ms.export(), om.export())
+        assert np.array_equal(ns.export(), on.export())
