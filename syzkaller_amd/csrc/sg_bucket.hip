@@ -339,6 +339,19 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
     if ((vmask >> k) & 1u) pos[k] = atomicAdd(&cnt[dv[k]], 1u);
 }
 
+// Write-out of a ranked tile: after tile_rank and the staging barrier, cnt[d]
+// is the end of digit d's slots.  Each half-wave copies whole digit runs
+// (16 half-waves, 16 digits each): 32 consecutive slots per store, and no
+// per-slot digit array in LDS.
+__device__ __forceinline__ void tile_write(const uint32_t* stage, const uint32_t* cnt, const uint32_t* gbase,
+                                           uint32_t* __restrict__ out, int tid) {
+  const int hw = tid >> 5, hl = tid & 31;
+  for (int d = hw; d < 256; d += kPThreads / 32) {
+    const uint32_t e = cnt[d], gb = gbase[d];
+    for (uint32_t p = (d ? cnt[d - 1] : 0u) + hl; p < e; p += 32) out[gb + p] = stage[p];
+  }
+}
+
 // O(1) "largest k with st[k] <= p" inside one tile of <= kPT positions, for
 // sorted segment starts st[0..m) given tile-relative and clamped to [0, kPT]
 // (st[0] == 0, m < 2^16).  Non-empty segments that start inside the tile are
@@ -419,13 +432,13 @@ struct P1Args {
 };
 
 template <bool kDbg>
-__global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p1_scatter(P1Args a) {
   __shared__ uint32_t stage[kPT];
-  __shared__ uint8_t sdig[kPT];
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
   __shared__ SegLds<uint8_t> L;
+  uint8_t* sidx = reinterpret_cast<uint8_t*>(stage);  // record-in-tile index; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
@@ -463,12 +476,12 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   __syncthreads();
   stamp(0);
   const uint32_t nt = s1 - s0;
-  seg_build(L, sdig, win, wn, nt, tid);  // sdig doubles as the segment index until the rank
+  seg_build(L, sidx, win, wn, nt, tid);
   uint32_t dv[kSteps], pk[kSteps];
   const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sdig, el0 + k * 64) : 0u;  // record in tile
+    const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // record in tile
     dv[k] = sv[k] >> 24;
     pk[k] = (sv[k] << 8) | r;
   }
@@ -478,16 +491,10 @@ __global__ __launch_bounds__(kPThreads) void k_p1_scatter(P1Args a) {
   stamp(2);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) {
-      stage[pos[k]] = pk[k];
-      sdig[pos[k]] = (uint8_t)dv[k];
-    }
+    if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
   __syncthreads();
   stamp(3);
-  for (uint32_t p = tid; p < nt; p += kPThreads) {
-    const uint32_t d = sdig[p];
-    a.out[gbase[d] + p] = stage[p];
-  }
+  tile_write(stage, cnt, gbase, a.out, tid);
   stamp(4);
   if (kDbg && tid == 0) atomicAdd(&a.dbg[5], 1ull);
 }
@@ -505,9 +512,8 @@ struct P2Args {
   uint32_t* out;           // (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile
 };
 
-__global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p2_scatter(P2Args a) {
   __shared__ uint32_t stage[kPT];
-  __shared__ uint8_t sdig[kPT];
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t runs[kGroupTiles + 1];  // chunk-relative run starts of the group's tiles in this slice
@@ -554,15 +560,9 @@ __global__ __launch_bounds__(kPThreads) void k_p2_scatter(P2Args a) {
   tile_rank(dv, vmask, cnt, gbase, pos);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) {
-      stage[pos[k]] = pk[k];
-      sdig[pos[k]] = (uint8_t)dv[k];
-    }
+    if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
   __syncthreads();
-  for (uint32_t p = tid; p < nt; p += kPThreads) {
-    const uint32_t f = sdig[p];
-    a.out[gbase[f] + p] = stage[p];
-  }
+  tile_write(stage, cnt, gbase, a.out, tid);
 }
 
 // ---------------------------------------------------------------- bucket ---
@@ -1026,6 +1026,10 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
         // owner key: the chunk from the slot map of the thread that held the
         // entry, a forward step or two to the entry's own chunk
         const uint32_t xv = qx[k], i = qk[k], t = (i - base) / kBU;
+#if SG_EXP == 3
+        ok &= hash_insert64(ht, nbits, xv >> 16, i & 0xFFFFFFu);
+        continue;
+#endif
         uint32_t ci = slot_t[t] == rtag ? slot_c[t] : chunk_of(r, W, runs, i);
         if (i < W.wlim && ci >= W.wc)
           while (ci + 1 < W.wc + W.wn && runs[ci + 1 - W.wc] <= i) ci++;
