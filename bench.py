@@ -142,18 +142,18 @@ def triage_step(ctx, maxsig, newsig, b, rec_new, diff_vals, diff_off):
          diff_off.data_ptr() if diff_off is not None else None)
 
 
-KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "key_records", "scan",
+KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan",
            "triage_claim", "triage_resolve", "emit"]
 
 
 def part_geometry(n_in, n_rec):
     """Tile / chunk counts of the partitioned path (sg_bucket.hip BucketPlan):
-    pass-1 tiles (8192 entries / 64 records each), and pass-2 chunks (about
-    one per non-empty group of 1020 tiles x 256 slices for spread-out signal)."""
+    pass-1 tiles (8192 entries / 256 records each), and pass-2 chunks (about
+    one per non-empty (slice, 2^16-record group) pair beyond the full ones)."""
     na = -(-int(n_in) // 8192)
-    t = na + (int(n_rec) - 1) // 64
-    kt = -(-t // 1020)
-    return t, 256 * kt
+    t = na + (int(n_rec) - 1) // 256
+    ng = (int(n_rec) - 1) // 65536 + 1
+    return t, na + 256 * ng // 2
 
 
 def algo_bytes(n_in, n_cand, n_diff, n_rec, n_newwords):

@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"p1_hist": "k_hist_rep<false>", "p1_scatter": "k_p1_scatter", "p2_hist": "k_hist_rep<true>", "p2_scatter": "k_p2_scatter",
-           "bucket_triage": "k_bucket<false>", "bucket_spill": "k_bucket_direct", "key_records": "k_key_records",
+           "bucket_triage": "k_bucket<false>", "bucket_spill": "k_bucket_direct",
            "triage_claim": "k_claim<true>", "triage_resolve": "k_resolve<true>", "count_missing": "k_count_missing",
            "emit_scatter": "k_scatter("}
 

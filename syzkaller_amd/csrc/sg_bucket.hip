@@ -16,16 +16,19 @@
 //           <= kRecCap records (cuts at every kPT-th entry and at every
 //           kRecCap-th record offset), so an entry's record is
 //           trec[tile] + an 8-bit in-tile index;
+//   groups  records in runs of 2^16 (group g = records [g << 16, +2^16));
+//           every group boundary is a kRecCap-th record offset, hence a
+//           tile cut, so a group is a run of whole tiles [gt[g], gt[g+1]);
 //   pass 1  partition by the top byte of s (256 slices of 2^24 signals):
 //           entry = s << 8 | rec_in_tile, runs laid out [slice][tile];
-//   pass 2  per slice, groups of kGroupTiles consecutive pass-1 tiles, cut
-//           into chunks of <= kPT entries; partition by bits 16..23
-//           of s: entry = (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile,
-//           runs laid out [byte][chunk];
+//   pass 2  per (slice, group), cut into chunks of <= kPT entries;
+//           partition by bits 16..23 of s: entry = (s & 0xFFFF) << 16 |
+//           record_in_group, runs laid out [byte][chunk];
 //   bucket  one workgroup per 2^16-signal bucket (d, f): its 8 KiB maxSignal
-//           slice in LDS is the new-signal test; candidates (s not in
-//           maxSignal) recover their record through the chunk -> group ->
-//           tile tables and go into an LDS hash map s -> min(record).  The
+//           slice in LDS is the new-signal test; a candidate (s not in
+//           maxSignal) at bucket position i has record (group(i) << 16) |
+//           (entry & 0xFFFF), group(i) from the bucket's group boundaries,
+//           and goes into an LDS hash map s -> min(record).  The
 //           bucket's new bits go back to maxSignal / newSignal from their
 //           only writer.  Buckets whose distinct candidates overflow the map
 //           are redone by a direct-table kernel.
@@ -48,26 +51,18 @@ constexpr int kPThreads = 512;               // 8 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
-// Entry layouts.  Pass 1: s << 8 | record-in-tile.  Pass 2: (s & 0xFFFF) << 16
-// | tile-in-group << kRelBits | record-in-tile.  A pass-1 tile spans at most
-// kRecCap records; a pass-2 group at most kGroupTiles tiles of one slice.
-// 6 + 10 bits: records are long in practice (C2: ~840 entries), and groups
-// of ~1000 tiles keep even a thin slice's pass-2 chunks near kPT entries.
-constexpr uint32_t kRelBits = 6;
-constexpr uint32_t kRecCap = 1u << kRelBits;       // records per pass-1 tile
-constexpr uint32_t kTileRelBits = 16 - kRelBits;
-constexpr uint32_t kGroupTiles = 1020;             // pass-1 tiles per pass-2 group (< 2^kTileRelBits)
-static_assert(kGroupTiles < (1u << kTileRelBits), "tile-in-group field");
-// owner key of an entry: pass-1 tile << kRelBits | record-in-tile
-__host__ __device__ constexpr uint32_t entry2_tilerel(uint32_t x) { return (x >> kRelBits) & ((1u << kTileRelBits) - 1); }
-__host__ __device__ constexpr uint32_t entry2_rel(uint32_t x) { return x & (kRecCap - 1); }
+// Entry layouts.  Pass 1: s << 8 | record-in-tile (kRecCap records per tile
+// at most).  Pass 2: (s & 0xFFFF) << 16 | record-in-group.
+constexpr uint32_t kRecCap = 256;              // records per pass-1 tile
+constexpr uint32_t kGroupBits = 16;
+constexpr uint32_t kGroupRecs = 1u << kGroupBits;  // records per group
+constexpr uint32_t kMaxGroups = 256;           // groups per launch (larger batches run in record slices)
+static_assert(kGroupRecs % kRecCap == 0, "group boundaries must be tile cuts");
 constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
 constexpr int kBThreads = 512;
 constexpr int kBU = 8;                       // entries per thread per round in the bucket kernel
 constexpr uint32_t kHash = 4096;             // candidate map slots per bucket
-constexpr uint32_t kRunWin = 1024;           // chunk run starts kept in LDS per bucket
-constexpr uint32_t kQueue = 2048;            // candidates queued per round (dense processing)
 constexpr uint32_t kMaxProbe = 64;           // linear-probe cap before a bucket spills
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
@@ -129,33 +124,48 @@ __global__ void k_cuts(Cuts c) {
   c.aux[rank] = (uint32_t)sgd::seg_search(c.rec_off, 0, c.nrec - 1, xe);
 }
 
-// Pass-2 groups: group j = (slice j / kt, tiles [(j % kt) * kGroupTiles, +kGroupTiles))
-// covers [gstart(j), gstart(j + 1)) of the pass-1 output; it is cut into
-// ceil(size / kPT) chunks (none when empty).
-__device__ __forceinline__ uint32_t group_start(const uint32_t* goff1, uint64_t T, uint64_t kt, uint64_t ng,
-                                                uint32_t n, uint64_t j) {
-  return j < ng ? goff1[(j / kt) * T + (j % kt) * kGroupTiles] : n;
+// Group g's first tile: the rank of the record cut at rec_off[g << 16] (cut
+// j = g * kGroupRecs / kRecCap - 1 of B; see k_cuts); gt[NG] = T.
+__global__ void k_group_tiles(const uint64_t* __restrict__ rec_off, uint64_t nA, uint32_t NG, uint32_t T,
+                              uint32_t* __restrict__ gt) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > NG) return;
+  if (g == 0 || g == NG) {
+    gt[g] = g ? T : 0u;
+    return;
+  }
+  const uint64_t a = rec_off[(uint64_t)g * kGroupRecs] / kPT + 1;
+  gt[g] = (uint32_t)((uint64_t)g * (kGroupRecs / kRecCap) - 1 + (a < nA ? a : nA));
 }
 
-__global__ void k_group_chunks(const uint32_t* __restrict__ goff1, uint64_t T, uint64_t kt, uint64_t ng, uint32_t n,
-                               uint32_t* __restrict__ nch) {
+// Pass-2 slice-groups: j = (slice j / NG, group j % NG) covers
+// [gstart(j), gstart(j + 1)) of the pass-1 output (gt[NG] = T makes gstart(ng)
+// the end); it is cut into ceil(size / kPT) chunks (none when empty).
+__device__ __forceinline__ uint32_t group_start(const uint32_t* goff1, uint32_t T, uint32_t NG, const uint32_t* gt,
+                                                uint64_t j) {
+  return goff1[(j / NG) * T + gt[j % NG]];
+}
+
+__global__ void k_group_chunks(const uint32_t* __restrict__ goff1, uint32_t T, uint32_t NG,
+                               const uint32_t* __restrict__ gt, uint64_t ng, uint32_t* __restrict__ nch) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= ng) return;
-  const uint32_t sz = group_start(goff1, T, kt, ng, n, j + 1) - group_start(goff1, T, kt, ng, n, j);
+  const uint32_t sz = group_start(goff1, T, NG, gt, j + 1) - group_start(goff1, T, NG, gt, j);
   nch[j] = (sz + kPT - 1) / kPT;
 }
 
 // cbase = exclusive scan of nch (cbase[ng] = number of chunks G).  Writes the
-// chunk list (start, group) for c < G, start = n for G <= c <= gmax (the
+// chunk list (start, slice-group) for c < G, start = n for G <= c <= gmax (the
 // launch grids use gmax, an upper bound known on the host), and cfirst[d] =
 // first chunk of slice d (cfirst[256] = G).
-__global__ void k_chunk_list(const uint32_t* __restrict__ goff1, uint64_t T, uint64_t kt, uint64_t ng, uint32_t n,
+__global__ void k_chunk_list(const uint32_t* __restrict__ goff1, uint32_t T, uint32_t NG,
+                             const uint32_t* __restrict__ gt, uint64_t ng, uint32_t n,
                              const uint32_t* __restrict__ cbase, uint64_t gmax, uint32_t* __restrict__ cstart,
                              uint32_t* __restrict__ cgov, uint32_t* __restrict__ cfirst) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = cbase[ng];
   if (i < ng) {
-    const uint32_t g0 = group_start(goff1, T, kt, ng, n, i), g1 = group_start(goff1, T, kt, ng, n, i + 1);
+    const uint32_t g0 = group_start(goff1, T, NG, gt, i), g1 = group_start(goff1, T, NG, gt, i + 1);
     uint32_t c = cbase[i];
     for (uint32_t e = g0; e < g1; e += kPT, c++) {
       cstart[c] = e;
@@ -166,22 +176,41 @@ __global__ void k_chunk_list(const uint32_t* __restrict__ goff1, uint64_t T, uin
     cstart[i] = n;
     cgov[i] = (uint32_t)(ng - 1);
   }
-  if (i <= 256) cfirst[i] = i < 256 ? cbase[i * kt] : G;
+  if (i <= 256) cfirst[i] = i < 256 ? cbase[i * NG] : G;
 }
 
-// One 16-B descriptor per pass-2 block (the grid is the host bound gmax):
-// {start, end, group, chunk} of chunk xcd_tile(bid, G) for bid < G, empty
-// past G.  Lets the pass-2 kernels start their data loads after one load.
+// last t in [lo, hi) with row[t] <= x (row non-decreasing, row[lo] <= x)
+__device__ __forceinline__ uint32_t last_le(const uint32_t* row, uint32_t lo, uint32_t hi, uint32_t x) {
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (row[mid] <= x)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Per pass-2 block (the grid is the host bound gmax): desc = {start, end,
+// slice-group, chunk} of chunk xcd_tile(bid, G) for bid < G, empty past G;
+// dtile = the pass-1 tiles [first, last + 1) whose runs the chunk holds.
+// Lets the pass-2 kernels start their data loads after one load.
 __global__ void k_chunk_desc(const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ cgov,
-                             const uint32_t* __restrict__ gcount, uint64_t gmax, uint4* __restrict__ desc) {
+                             const uint32_t* __restrict__ gcount, uint64_t gmax, const uint32_t* __restrict__ goff1,
+                             uint32_t T, uint32_t NG, const uint32_t* __restrict__ gt, uint4* __restrict__ desc,
+                             uint2* __restrict__ dtile) {
   const uint64_t bid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (bid >= gmax) return;
   const uint32_t G = *gcount;
   if (bid < G) {
-    const uint32_t c = xcd_tile((uint32_t)bid, G);
-    desc[bid] = make_uint4(cstart[c], cstart[c + 1], cgov[c], c);
+    const uint32_t c = xcd_tile((uint32_t)bid, G), s0 = cstart[c], s1 = cstart[c + 1], j = cgov[c];
+    const uint32_t* row = goff1 + (uint64_t)(j / NG) * T;
+    const uint32_t lo = gt[j % NG], hi = gt[j % NG + 1];
+    desc[bid] = make_uint4(s0, s1, j, c);
+    dtile[bid] = make_uint2(last_le(row, lo, hi, s0), last_le(row, lo, hi, s1 - 1) + 1);
   } else {
     desc[bid] = make_uint4(0, 0, 0, 0);
+    dtile[bid] = make_uint2(0, 0);
   }
 }
 
@@ -352,13 +381,14 @@ __device__ __forceinline__ void tile_write(const uint32_t* stage, const uint32_t
   }
 }
 
-// O(1) "largest k with st[k] <= p" inside one tile of <= kPT positions, for
-// sorted segment starts st[0..m) given tile-relative and clamped to [0, kPT]
-// (st[0] == 0, m < 2^16).  Non-empty segments that start inside the tile are
-// marked: bit p of sbits <=> one starts at p > 0, sidx[p] = its index;
-// wmax[w] = index of the segment holding position 32w + 31; kinit = the
-// segment holding position 0.  Replaces a per-entry search (segments can be
-// a few entries long: small records, thin slices).
+// O(1) "value of the segment holding p" inside one tile of <= kPT positions,
+// for sorted segment starts st(0..m) given tile-relative and clamped to
+// [0, kPT] (st(0) == 0) and segment values val(k) non-decreasing in k
+// (< 2^16).  Non-empty segments that start inside the tile are marked: bit
+// p of sbits <=> one starts at p > 0, sidx[p] = its value; wmax[w] = value of
+// the segment holding position 32w + 31; kinit = that of position 0.
+// Replaces a per-entry search (segments can be a few entries long: small
+// records, thin slices).
 template <typename IdxT>
 struct SegLds {
   uint32_t sbits[kPT / 32];
@@ -373,15 +403,16 @@ __device__ __forceinline__ void seg_clear(SegLds<IdxT>& L, int tid) {
 }
 
 // call after seg_clear + a barrier; ends with a barrier
-template <typename IdxT, typename S>
-__device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, const S* st, uint32_t m, uint32_t n, int tid) {
+template <typename IdxT, typename StF, typename ValF>
+__device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, StF st, ValF val, uint32_t m, uint32_t n,
+                                          int tid) {
   for (uint32_t k = tid; k < m; k += kPThreads) {
-    const uint32_t p = st[k], nx = k + 1 < m ? (uint32_t)st[k + 1] : 0xFFFFFFFFu;
+    const uint32_t p = st(k), nx = k + 1 < m ? st(k + 1) : 0xFFFFFFFFu;
     if (p == 0) {
-      if (nx > 0) atomicMax(&L.kinit, k);
+      if (nx > 0) atomicMax(&L.kinit, val(k));
     } else if (p < n && nx > p) {
       atomicOr(&L.sbits[p >> 5], 1u << (p & 31));
-      sidx[p] = (IdxT)k;
+      sidx[p] = (IdxT)val(k);
     }
   }
   __syncthreads();
@@ -476,7 +507,8 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
   __syncthreads();
   stamp(0);
   const uint32_t nt = s1 - s0;
-  seg_build(L, sidx, win, wn, nt, tid);
+  seg_build(
+      L, sidx, [&](uint32_t k) { return (uint32_t)win[k]; }, [](uint32_t k) { return k; }, wn, nt, tid);
   uint32_t dv[kSteps], pk[kSteps];
   const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
@@ -503,29 +535,29 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
 struct P2Args {
   const uint32_t* in;      // pass-1 output
   const uint4* desc;       // per-block chunk descriptors
+  const uint2* dtile;      // per-block chunk tile ranges
   const uint32_t* g2;      // device: number of chunks G2 (the grid is an upper bound)
   const uint32_t* goff1;   // pass-1 run starts [slice][tile]
-  uint32_t T, kt;
-  uint32_t n;
+  const uint32_t* trec;    // first record of each pass-1 tile
+  uint32_t T, NG;
   const uint32_t* goff2;   // scanned [byte][chunk]
   const uint32_t* hist2;   // [byte][chunk] counts
-  uint32_t* out;           // (s & 0xFFFF) << 16 | tile_in_group << 8 | rec_in_tile
+  uint32_t* out;           // (s & 0xFFFF) << 16 | record_in_group
 };
 
 __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p2_scatter(P2Args a) {
   __shared__ uint32_t stage[kPT];
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
-  __shared__ uint16_t runs[kGroupTiles + 1];  // chunk-relative run starts of the group's tiles in this slice
   __shared__ SegLds<uint16_t> L;
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(stage);  // tile-in-group index; stage is free until the rank
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(stage);  // tile's first record in the group; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint4 dsc = a.desc[blockIdx.x];
+  const uint2 dt = a.dtile[blockIdx.x];
   const uint32_t s0 = dsc.x, s1 = dsc.y, gov = dsc.z, c = dsc.w;
   if (s0 >= s1) return;
   const uint32_t G2 = *a.g2;
-  const uint32_t d = gov / a.kt, tb = (gov % a.kt) * kGroupTiles;
-  const uint32_t ntl = a.T - tb < kGroupTiles ? a.T - tb : kGroupTiles;
+  const uint32_t d = gov / a.NG, rg0 = (gov % a.NG) << kGroupBits, tf = dt.x, m = dt.y - dt.x;
   const uint32_t ebase = s0 + w * kPerWave;
   uint32_t sv[kSteps];
   uint32_t vmask = 0;
@@ -536,10 +568,6 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
     sv[k] = ok ? a.in[e] : 0u;
     vmask |= (ok ? 1u : 0u) << k;
   }
-  for (uint32_t i = tid; i < ntl; i += kPThreads) {
-    const uint32_t o = a.goff1[(uint64_t)d * a.T + tb + i];
-    runs[i] = (uint16_t)(o <= s0 ? 0 : (o - s0 >= (uint32_t)kPT ? kPT : o - s0));
-  }
   for (int f = tid; f < 256; f += kPThreads) {
     gbase[f] = a.goff2[(uint64_t)f * G2 + c];
     cnt[f] = a.hist2[(uint64_t)f * G2 + c];
@@ -547,14 +575,23 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
   seg_clear(L, tid);
   __syncthreads();
   const uint32_t nt = s1 - s0;
-  seg_build(L, sidx, runs, ntl, nt, tid);
+  // segments = the chunk's tiles (runs of this slice); value = the tile's
+  // first record relative to the group
+  const uint32_t* row = a.goff1 + (uint64_t)d * a.T + tf;
+  seg_build(
+      L, sidx,
+      [&](uint32_t k) {
+        const uint32_t o = row[k];
+        return o <= s0 ? 0u : (o - s0 >= (uint32_t)kPT ? (uint32_t)kPT : o - s0);
+      },
+      [&](uint32_t k) { return a.trec[tf + k] - rg0; }, m, nt, tid);
   uint32_t dv[kSteps], pk[kSteps];
   const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint32_t k1 = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // tile in group
+    const uint32_t r1 = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // tile's record in group
     dv[k] = sv[k] >> 24;
-    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (k1 << kRelBits) | (sv[k] & (kRecCap - 1));
+    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (r1 + (sv[k] & (kRecCap - 1)));
   }
   uint32_t pos[kSteps];
   tile_rank(dv, vmask, cnt, gbase, pos);
@@ -568,16 +605,12 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
 // ---------------------------------------------------------------- bucket ---
 struct BucketArgs {
   const uint32_t* in;      // pass-2 output
-  const uint32_t* goff2;   // [byte][chunk] run starts
-  const uint32_t* g2;      // device: number of chunks
   const uint4* bdesc;      // per-bucket {lo, hi, c0, nch}
-  uint32_t kt;
-  const uint32_t* cfirst;  // 257
-  const uint32_t* cgov;
-  const uint32_t* trec;
+  const uint32_t* gbnd;    // [bucket][group]: first bucket position of each group's entries
+  uint32_t NG;             // groups
   uint32_t* mwords;        // maxSignal
   uint32_t* nwords;        // newSignal (nullable)
-  uint8_t* rec_new;
+  uint8_t* rec_new;        // per record: owns some new signal
   uint32_t* spill;         // buckets left for the direct-table kernel
   uint32_t* nspill;
   uint32_t* ticket;        // persistent bucket kernel: list entries handed out past 2 x grid
@@ -585,12 +618,6 @@ struct BucketArgs {
   const uint4* blist_q;    // ... and their descriptors
   const uint32_t* nlist;   // device: their number
   uint64_t* dbg;           // diagnostics (k_bucket<true>): per block {start, end, buckets, rounds, 4 phase cycle sums}
-  uint8_t* kflag;          // owner keys (tile * 256 + record in tile) that own some signal
-};
-
-struct BucketRange {
-  uint32_t d, f, c0, nch, lo, hi;
-  const uint32_t* row;  // goff2 + f * G2 + c0: run start of each chunk of slice d
 };
 
 // non-empty flag per bucket (scanned into list positions)
@@ -620,24 +647,15 @@ __global__ void k_bucket_desc(const uint32_t* __restrict__ goff2, const uint32_t
   bdesc[b] = make_uint4(row[0], row[nch], c0, nch);
 }
 
-__device__ __forceinline__ BucketRange bucket_range(const BucketArgs& a, uint32_t b) {
-  BucketRange r;
-  const uint4 q = a.bdesc[b];
-  r.d = b >> 8;
-  r.f = b & 255;
-  r.lo = q.x;
-  r.hi = q.y;
-  r.c0 = q.z;
-  r.nch = q.w;
-  r.row = a.goff2 + (uint64_t)r.f * *a.g2 + r.c0;
-  return r;
-}
-
-// record of the pass-2 entry x at position o (chunk index within the slice: ci)
-__device__ __forceinline__ uint32_t entry_record(const BucketArgs& a, const BucketRange& r, uint32_t ci, uint32_t x) {
-  const uint32_t gov = a.cgov[r.c0 + ci];
-  const uint32_t t1 = (gov % a.kt) * kGroupTiles + entry2_tilerel(x);
-  return a.trec[t1] + entry2_rel(x);
+// gbnd[b * NG + g]: bucket b = (d, f) holds the runs of slice d's chunks in
+// byte row f, chunk-ordered, so group g's entries start at the run of the
+// first chunk of slice-group (d, g) (an empty slice-group: the next one's)
+__global__ void k_bucket_groups(const uint32_t* __restrict__ goff2, const uint32_t* __restrict__ gcount,
+                                const uint32_t* __restrict__ cbase, uint32_t NG, uint32_t* __restrict__ gbnd) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)kNumBuckets * NG) return;
+  const uint32_t b = (uint32_t)(i / NG), g = (uint32_t)(i % NG);
+  gbnd[i] = goff2[(uint64_t)(b & 255) * *gcount + cbase[(b >> 8) * NG + g]];
 }
 
 __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
@@ -653,64 +671,42 @@ __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, 
   }
 }
 
-__device__ __forceinline__ uint32_t slot_of(uint32_t sl) { return (sl * 2654435761u) >> 20; }  // 12 bits
-
-__device__ __forceinline__ bool hash_insert(uint32_t* hkey, uint32_t* hval, uint32_t* nbits, uint32_t sl,
-                                            uint32_t rec) {
-  uint32_t h = slot_of(sl);
-  for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
-    const uint32_t k = atomicCAS(&hkey[h], kEmpty, sl);
-    if (k == kEmpty) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
-    if (k == kEmpty || k == sl) {
-      atomicMin(&hval[h], rec);
-      return true;
-    }
-    h = (h + 1) & (kHash - 1);
+// group of bucket position p >= gb[0]: last g < NG with gb[g] <= p
+__device__ __forceinline__ uint32_t group_of(const uint32_t* gb, uint32_t NG, uint32_t p) {
+  uint32_t lo = 0, hi = NG;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (gb[mid] <= p)
+      lo = mid;
+    else
+      hi = mid;
   }
-  return false;  // map (nearly) full: the bucket spills
+  return lo;
 }
 
-// Owner key of the candidate entry x at position i of the bucket:
-// key = pass-1 tile * 256 + record in tile.  Records only grow with the tile
-// and, inside a tile, with the in-tile index, so min(key) names the same
-// record as min(record) (a record cut by a tile boundary has two keys that
-// both map back to it); the map works on keys and the record,
-// trec[key >> 8] + (key & 255), is looked up once per owner at the end.
-__device__ __forceinline__ uint32_t cand_key(const BucketArgs& a, const BucketRange& r, bool lds_runs,
-                                             const uint32_t* runs, const uint32_t* tb, uint32_t i, uint32_t x) {
-  uint32_t t0;
-  if (lds_runs) {
-    t0 = tb[sgd::seg_search(runs, 0, r.nch - 1, i)];
-  } else {
-    const uint32_t ci = (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
-    t0 = (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
-  }
-  return ((t0 + entry2_tilerel(x)) << kRelBits) | entry2_rel(x);
-}
-
-__device__ __forceinline__ uint32_t key_record(const BucketArgs& a, uint32_t key) {
-  return a.trec[key >> kRelBits] + (key & (kRecCap - 1));
-}
+// Record of the candidate entry x at a bucket position of group g.  Records
+// are what the first-owner rule takes the minimum of (fuzzer.go:665 order).
+__device__ __forceinline__ uint32_t entry_record(uint32_t g, uint32_t x) { return (g << kGroupBits) | (x & 0xFFFFu); }
 
 // Persistent: each workgroup takes buckets one after another (the first one
 // by its index, then by ticket) and runs through them as one stream of
-// rounds of kBU entries per thread.  Per round: the LDS new-signal test,
-// candidates queued in LDS (wave-aggregated slots) and processed densely --
-// record lookup (chunk by LDS search, the group's first tile from LDS, one
-// trec load), insert into the map.  While a round is processed the next one
-// is in flight -- the same bucket's next round, or the next bucket's first
-// round together with its maxSignal slice and chunk tables.  The ticket after
-// that is fetched a bucket ahead, so no dependent load is exposed.
+// rounds of kBU entries per thread.  Per round and thread: the LDS
+// new-signal test of its kBU entries, then each candidate's record (group by
+// a search over the bucket's group boundaries in LDS) inserted into the map.
+// Rounds have no barrier: the waves of a workgroup meet only at bucket ends.
+// While a round is processed the thread's next one is in flight -- the same
+// bucket's next round, or the next bucket's first round together with its
+// maxSignal slice and group boundaries.  The ticket after that is fetched a
+// bucket ahead, so no dependent load is exposed.
+constexpr uint32_t kGroupWords = (kMaxGroups + kBThreads - 1) / kBThreads;  // group boundaries per thread
 struct BucketPre {  // a bucket's first loads, held in registers
   uint32_t msw[kBucketWords / kBThreads];
   uint32_t nsw[kBucketWords / kBThreads];  // newSignal words (only this block writes them)
-  uint32_t rw[kRunWin / kBThreads];  // its first window of chunk run starts ...
-  uint32_t tw[kRunWin / kBThreads];  // ... and their groups
-  uint32_t lim;                      // first position past that window
+  uint32_t gw[kGroupWords];                // group boundaries
 };
 
 // Rounds start 4-aligned (the bucket start rounded down): thread t holds
-// entries base + 16t .. +15 as four 16-B loads (immediate offsets, one
+// entries base + kBU t .. + kBU - 1 as 16-B loads (immediate offsets, one
 // address); entry i is live iff lo <= i < hi.  The pass-2 buffer is padded,
 // so the quad reads past hi stay in bounds.
 __device__ __forceinline__ uint32_t round_pos(uint32_t base, int u) { return base + threadIdx.x * kBU + u; }
@@ -728,8 +724,7 @@ __device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t 
   }
 }
 
-__device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, uint4 q, uint32_t G2,
-                                                BucketPre& P) {
+__device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, BucketPre& P) {
   static_assert(kBucketWords / kBThreads == 4, "one uint4 of the slice per thread");
   const uint4 m = reinterpret_cast<const uint4*>(a.mwords + (uint64_t)b * kBucketWords)[threadIdx.x];
   P.msw[0] = m.x;
@@ -742,15 +737,12 @@ __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b,
   P.nsw[1] = nw.y;
   P.nsw[2] = nw.z;
   P.nsw[3] = nw.w;
-  const uint32_t* row = a.goff2 + (uint64_t)(b & 255) * G2 + q.z;
+  const uint32_t* gr = a.gbnd + (uint64_t)b * a.NG;
 #pragma unroll
-  for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+  for (int j = 0; j < (int)kGroupWords; j++) {
     const uint32_t i = j * kBThreads + threadIdx.x;
-    const bool ok = i < q.w;
-    P.rw[j] = ok ? row[i] : 0u;
-    P.tw[j] = ok ? a.cgov[q.z + i] : 0u;
+    P.gw[j] = i < a.NG ? gr[i] : 0u;
   }
-  P.lim = q.w > kRunWin ? row[kRunWin] : q.y;
 }
 
 // thread 0: bucket and descriptor of list entry t (kNumBuckets: past the end)
@@ -766,10 +758,12 @@ constexpr unsigned long long kEmpty64 = ~0ull;
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint4 uni(uint4 v) { return make_uint4(uni(v.x), uni(v.y), uni(v.z), uni(v.w)); }
 
-// Map slot = signal (high word) | owner key (low word).  A first insert is one
-// CAS; a repeat of a signal lowers the key with a u64 min (equal high words).
-__device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* nbits, uint32_t sl, uint32_t key) {
-  const unsigned long long mine = ((unsigned long long)sl << 32) | key;
+__device__ __forceinline__ uint32_t slot_of(uint32_t sl) { return (sl * 2654435761u) >> 20; }  // 12 bits
+
+// Map slot = signal (high word) | record (low word).  A first insert is one
+// CAS; a repeat of a signal lowers the record with a u64 min (equal high words).
+__device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* nbits, uint32_t sl, uint32_t rec) {
+  const unsigned long long mine = ((unsigned long long)sl << 32) | rec;
   uint32_t h = slot_of(sl);
   for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
     const unsigned long long old = atomicCAS(&ht[h], kEmpty64, mine);
@@ -778,7 +772,7 @@ __device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* 
       return true;
     }
     if ((uint32_t)(old >> 32) == sl) {
-      if ((uint32_t)old > key) atomicMin(&ht[h], mine);
+      if ((uint32_t)old > rec) atomicMin(&ht[h], mine);
       return true;
     }
     h = (h + 1) & (kHash - 1);
@@ -786,55 +780,26 @@ __device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* 
   return false;  // map (nearly) full: the bucket spills
 }
 
-// The chunk tables of a bucket are held in LDS as a sliding window of up to
-// kRunWin chunks [wc, wc + wn), covering positions [runs[0], wlim); a hot
-// slice has thousands of chunks, and the window moves with the rounds.
-// Positions past the window (rounds spanning more than kRunWin chunks) fall
-// back to a search in global memory.
-struct RunWindow {
-  uint32_t wc, wn, wlim;
-};
-
-// chunk (index within the slice) holding bucket position i
-__device__ __forceinline__ uint32_t chunk_of(const BucketRange& r, const RunWindow& W, const uint32_t* runs,
-                                             uint32_t i) {
-  if (i < W.wlim && i >= runs[0]) return W.wc + (uint32_t)sgd::seg_search(runs, 0, W.wn - 1, i);
-  return (uint32_t)sgd::seg_search(r.row, 0, r.nch - 1, i);
-}
-
-__device__ __forceinline__ uint32_t chunk_tile(const BucketArgs& a, const BucketRange& r, const RunWindow& W,
-                                               const uint32_t* tb, uint32_t ci) {
-  return ci - W.wc < W.wn ? tb[ci - W.wc] : (a.cgov[r.c0 + ci] % a.kt) * kGroupTiles;
-}
-
 template <bool kDbg>
-__global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
+__global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
   __shared__ unsigned long long ht[kHash];
-  __shared__ uint32_t runs[kRunWin];  // run start of each chunk of the slice in this byte row
-  __shared__ uint32_t tb[kRunWin];    // first pass-1 tile of each chunk's group
-  __shared__ uint32_t qx[kQueue];     // candidate entries
-  __shared__ uint32_t qk[kQueue];     // their owner keys
-  __shared__ uint32_t qn;
+  __shared__ uint32_t gb[kMaxGroups];  // the bucket's group boundaries
+  __shared__ uint32_t sh_fail;         // some insert found the map full: the bucket spills
   __shared__ uint32_t sh_b[2];
   __shared__ uint4 sh_q[2];
-  __shared__ uint32_t sh_w[2];
-  __shared__ uint32_t slot_c[kBThreads];  // chunk holding each thread's first entry this round ...
-  __shared__ uint32_t slot_t[kBThreads];  // ... valid iff slot_t == this round's tag
-  __shared__ uint32_t sh_ca;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t G2 = *a.g2;
+  const int tid = threadIdx.x;
+  const uint32_t NG = a.NG;
   constexpr uint32_t kRound = kBThreads * kBU;
   // diagnostics (kDbg): block span, buckets, rounds, cycles per phase as wave 0 sees them
   const uint64_t t_start = kDbg ? wall_clock64() : 0;
   uint64_t n_buckets = 0, n_rounds = 0;
-  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};  // install, test+queue, dense, flush | queue: test, search+enqueue, rest
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};  // install, rounds, -, flush | rounds: test, inserts, -
   uint64_t tk = kDbg ? clock64() : 0;
   for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
   for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
-  slot_t[tid] = kEmpty;
-  uint32_t rtag = 0;  // round tag of the slot map
+  if (tid == 0) sh_fail = 0;
   // list entries: blockIdx and gridDim + blockIdx first, then tickets from
   // 2 x gridDim.  Thread 0 takes each ticket a bucket before it resolves it and
   // resolves it a bucket before it is needed, so neither wait is exposed.
@@ -862,20 +827,16 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
   uint32_t x[kBU], y[kBU];
   BucketPre P;
   bucket_round_load(a, q.x & ~3u, q.y, x);
-  bucket_pre_load(a, b, q, G2, P);
+  bucket_pre_load(a, b, P);
   while (b < kNumBuckets) {
-    const BucketRange r = {b >> 8, b & 255, q.z, q.w, q.x, q.y, a.goff2 + (uint64_t)(b & 255) * G2 + q.z};
-    RunWindow W = {0, r.nch < kRunWin ? r.nch : kRunWin, P.lim};
+    const uint32_t lo = q.x, hi = q.y;
     __syncthreads();  // the previous bucket is done with the LDS
     reinterpret_cast<uint4*>(mslice)[tid] = make_uint4(P.msw[0], P.msw[1], P.msw[2], P.msw[3]);
     const uint4 ns = make_uint4(P.nsw[0], P.nsw[1], P.nsw[2], P.nsw[3]);  // words 4 tid .. +3
 #pragma unroll
-    for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
+    for (int j = 0; j < (int)kGroupWords; j++) {
       const uint32_t i = j * kBThreads + tid;
-      if (i < W.wn) {
-        runs[i] = P.rw[j];
-        tb[i] = (P.tw[j] % a.kt) * kGroupTiles;
-      }
+      if (i < NG) gb[i] = P.gw[j];
     }
     // thread 0: resolve the pending ticket (published after the rounds) and take the next one
     uint32_t pend_b = kNumBuckets;
@@ -884,174 +845,68 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
       pend_b = list_bucket(a, pend_t, nl, &pend_q);
       pend_t = pend_b < kNumBuckets ? 2 * gridDim.x + atomicAdd(a.ticket, 1u) : kEmpty;
     }
-    bool ok = true;
+    __syncthreads();
+    if (kDbg) {
+      const uint64_t t = clock64();
+      ph[0] += t - tk;
+      tk = t;
+    }
     n_buckets++;
-    uint32_t ca = 0;  // a chunk at or before the one holding the round's first position
-    for (uint32_t base = r.lo & ~3u;;) {
+    // Rounds: no barrier inside -- the waves run through the bucket on their
+    // own, meeting only in the map's atomics.
+    bool ok = true;
+    for (uint32_t base = lo & ~3u;;) {
       n_rounds++;
-      if (tid == 0) qn = 0;
-      __syncthreads();
-      // move the chunk window when this round runs past it
-      const uint32_t rend = base + kRound < r.hi ? base + kRound : r.hi;
-      if (rend > W.wlim && W.wc + W.wn < r.nch) {
-        if (tid == 0) {
-          const uint32_t ps = base > r.lo ? base : r.lo;
-          sh_w[0] = chunk_of(r, W, runs, ps);
-        }
-        __syncthreads();
-        W.wc = uni(sh_w[0]);
-        W.wn = r.nch - W.wc < kRunWin ? r.nch - W.wc : kRunWin;
-        uint32_t rv[kRunWin / kBThreads], gv[kRunWin / kBThreads];
-#pragma unroll
-        for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
-          const uint32_t i = j * kBThreads + tid;
-          rv[j] = i < W.wn ? r.row[W.wc + i] : 0u;
-          gv[j] = i < W.wn ? a.cgov[r.c0 + W.wc + i] : 0u;
-        }
-        W.wlim = W.wc + W.wn < r.nch ? r.row[W.wc + W.wn] : r.hi;
-#pragma unroll
-        for (int j = 0; j < (int)(kRunWin / kBThreads); j++) {
-          const uint32_t i = j * kBThreads + tid;
-          if (i < W.wn) {
-            runs[i] = rv[j];
-            tb[i] = (gv[j] % a.kt) * kGroupTiles;
-          }
-        }
-        __syncthreads();
-      }
-      // slot map: each chunk overlapping the round (from ca, up to kBThreads
-      // of them, inside the window) marks the threads whose first entry it
-      // holds; the chunk holding the next round's start becomes its ca
-      rtag++;
-      {
-        if (ca < W.wc) ca = W.wc;
-        const uint32_t c = ca + tid;
-        if (tid == 0) sh_ca = kEmpty;
-        if (c < W.wc + W.wn) {
-          const uint32_t sc = c == 0 ? base : runs[c - W.wc];
-          const uint32_t sn = c + 1 < W.wc + W.wn ? runs[c + 1 - W.wc] : W.wlim;
-          if (sn > sc && sn > base && sc < rend) {
-            const uint32_t tlo = sc <= base ? 0 : (sc - base + kBU - 1) / kBU;
-            const uint32_t thi = sn >= base + kRound ? kBThreads : (sn - base + kBU - 1) / kBU;
-            for (uint32_t t = tlo; t < thi; t++) {
-              slot_c[t] = c;
-              slot_t[t] = rtag;
-            }
-          }
-        }
-        __syncthreads();  // (sh_ca reset ordered before the writes below)
-        if (c < W.wc + W.wn) {
-          const uint32_t sc = runs[c - W.wc];
-          const uint32_t sn = c + 1 < W.wc + W.wn ? runs[c + 1 - W.wc] : W.wlim;
-          const uint32_t nb = base + kRound;
-          if (sc <= nb && nb < sn) sh_ca = c;
-        }
-      }
-      if (kDbg) {
-        const uint64_t t = clock64();
-        ph[base == (r.lo & ~3u) ? 0 : 1] += t - tk;
-        tk = t;
-      }
-      // this thread's 16 consecutive entries: the new-signal test (fuzzer.go:666)
+      // the next round in flight: this bucket's, or the next bucket's first
+      // (one load call: separate calls per case load into different
+      // registers and their join would wait for them)
+      const uint32_t next = base + kRound;
+      const bool last = next >= hi;
+      if (!last || b1 < kNumBuckets) bucket_round_load(a, last ? q1.x & ~3u : next, last ? q1.y : hi, y);
+      if (last && b1 < kNumBuckets) bucket_pre_load(a, b1, P);
+      // this thread's kBU consecutive entries: the new-signal test (fuzzer.go:666),
+      // all LDS reads issued before the first use
       const uint32_t p0 = round_pos(base, 0);
+      uint32_t mw[kBU];
+#pragma unroll
+      for (int u = 0; u < kBU; u++) mw[u] = mslice[x[u] >> 21];
       uint32_t cm = 0;
 #pragma unroll
       for (int u = 0; u < kBU; u++) {
-        const uint32_t sl = x[u] >> 16, i = p0 + u;
-        if (i >= r.lo && i < r.hi && !((mslice[sl >> 5] >> (sl & 31)) & 1u)) cm |= 1u << u;
+        const uint32_t i = p0 + u;
+        const uint32_t miss = ((~mw[u]) >> ((x[u] >> 16) & 31)) & 1u;
+        cm |= (miss & (i >= lo ? 1u : 0u) & (i < hi ? 1u : 0u)) << u;
       }
-      if (kDbg) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const uint64_t t = clock64();
-        ph[4] += t - tk;
-      }
-      // wave-aggregated queue slots
-      const uint32_t cnt = __popc(cm);
-      uint32_t incl = cnt;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-      }
-      uint32_t qb = 0;
-      if (lane == 63 && incl) qb = atomicAdd(&qn, incl);
-      uint32_t my = __shfl(qb, 63) + incl - cnt;
-      uint32_t ov = 0;  // queue overflow: these entries go into the map directly below
-#pragma unroll
-      for (int u = 0; u < kBU; u++)
-        if ((cm >> u) & 1u) {
-          if (my < kQueue) {
-            qx[my] = x[u];
-            qk[my] = p0 + u;  // position; the owner key is made in the dense pass
-          } else {
-            ov |= 1u << u;
-          }
-          my++;
-        }
       if (kDbg) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const uint64_t t = clock64();
-        ph[5] += t - tk;
+        ph[4] += t - tk;
+        tk = t;
       }
-      if (ov) {  // rare: the queue holds kQueue candidates per round
-#pragma unroll 1
-        for (int u = 0; u < kBU; u++)
-          if ((ov >> u) & 1u) {
-            uint32_t xu = 0;
+      if (cm && *(volatile uint32_t*)&sh_fail == 0) {
+        // the record of each candidate: its group, found once per thread
+        // and stepped forward (entries are in group order)
+        uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
+        do {
+          const int u = __builtin_ctz(cm);
+          cm &= cm - 1;
+          uint32_t xu = x[0];
 #pragma unroll
-            for (int k = 0; k < kBU; k++) xu = k == u ? x[k] : xu;
-            const uint32_t ci = chunk_of(r, W, runs, p0 + u);
-            ok &= hash_insert64(ht, nbits, xu >> 16,
-                                ((chunk_tile(a, r, W, tb, ci) + entry2_tilerel(xu)) << kRelBits) | entry2_rel(xu));
+          for (int k = 1; k < kBU; k++) xu = k == u ? x[k] : xu;
+          while (g + 1 < NG && gb[g + 1] <= p0 + u) g++;
+          if (!hash_insert64(ht, nbits, xu >> 16, entry_record(g, xu))) {
+            ok = false;
+            *(volatile uint32_t*)&sh_fail = 1;  // the others stop inserting (the bucket is redone)
+            break;
           }
+        } while (cm);
       }
-      // the next round in flight: this bucket's, or the next bucket's first
-      // (one load call: separate calls per case load into different
-      // registers and the join waits for them right here)
-      const uint32_t next = base + kRound;
-      const bool last = next >= r.hi;
-      if (!last || b1 < kNumBuckets)
-        bucket_round_load(a, last ? q1.x & ~3u : next, last ? q1.y : r.hi, y);
-      if (last && b1 < kNumBuckets) bucket_pre_load(a, b1, q1, G2, P);
-      __syncthreads();
       if (kDbg) {
         const uint64_t t = clock64();
-        ph[1] += t - tk;
+        ph[5] += t - tk;
         tk = t;
       }
-      const uint32_t qt = qn < kQueue ? qn : kQueue;
-      ca = uni(sh_ca != kEmpty ? sh_ca : ca + kBThreads - 1);
-#if SG_EXP != 2
-      for (uint32_t k = tid; k < qt; k += kBThreads) {
-        // owner key: the chunk from the slot map of the thread that held the
-        // entry, a forward step or two to the entry's own chunk
-        const uint32_t xv = qx[k], i = qk[k], t = (i - base) / kBU;
-#if SG_EXP == 3
-        ok &= hash_insert64(ht, nbits, xv >> 16, i & 0xFFFFFFu);
-        continue;
-#endif
-        uint32_t ci = slot_t[t] == rtag ? slot_c[t] : chunk_of(r, W, runs, i);
-        if (i < W.wlim && ci >= W.wc)
-          while (ci + 1 < W.wc + W.wn && runs[ci + 1 - W.wc] <= i) ci++;
-        else
-          ci = chunk_of(r, W, runs, i);
-        ok &= hash_insert64(ht, nbits, xv >> 16,
-                            ((chunk_tile(a, r, W, tb, ci) + entry2_tilerel(xv)) << kRelBits) | entry2_rel(xv));
-      }
-#endif
-      const bool fail = __syncthreads_or(!ok);
-      if (kDbg) {
-        const uint64_t t = clock64();
-        ph[2] += t - tk;
-        tk = t;
-      }
-      if (last || fail) {
-        if (fail && !last && b1 < kNumBuckets) {  // skip the rest of the bucket (the spill kernel redoes it)
-          bucket_round_load(a, q1.x & ~3u, q1.y, y);
-          bucket_pre_load(a, b1, q1, G2, P);
-        }
-        break;
-      }
+      if (last) break;
       base = next;
 #pragma unroll
       for (int u = 0; u < kBU; u++) x[u] = y[u];
@@ -1060,17 +915,24 @@ __global__ __launch_bounds__(kBThreads, 4) void k_bucket(BucketArgs a) {
       sh_b[0] = pend_b;
       sh_q[0] = pend_q;
     }
+    if (kDbg) {
+      const uint64_t t = clock64();
+      ph[1] += t - tk;
+      tk = t;
+    }
     if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
-      if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
+      if (tid == 0) {
+        a.spill[atomicAdd(a.nspill, 1u)] = b;
+        sh_fail = 0;
+      }
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
     } else {
-      // a record is queued iff it owns some signal (fuzzer.go:678-690): its
-      // owner key is flagged here, keys become records in k_key_records
+      // a record is queued iff it owns some signal (fuzzer.go:678-690)
       for (uint32_t i = tid; i < kHash; i += kBThreads) {
         const unsigned long long v = ht[i];
         if (v != kEmpty64) {
-          a.kflag[(uint32_t)v] = 1;
+          a.rec_new[(uint32_t)v] = 1;
           ht[i] = kEmpty64;
         }
       }
@@ -1122,56 +984,36 @@ __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
   __shared__ uint32_t owner[kQ];
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  __shared__ uint32_t runs[kRunWin];
-  __shared__ uint32_t tb[kRunWin];
+  __shared__ uint32_t gb[kMaxGroups];
   const int tid = threadIdx.x;
-  const uint32_t nsp = *a.nspill;
+  const uint32_t nsp = *a.nspill, NG = a.NG;
   for (uint32_t j = blockIdx.x; j < nsp; j += gridDim.x) {
     const uint32_t b = a.spill[j];
-    const BucketRange r = bucket_range(a, b);
+    const uint4 q = a.bdesc[b];
     const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
     for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
       mslice[i] = mg[i];
       nbits[i] = 0;
     }
-    const bool lds_runs = r.nch <= kRunWin;
-    if (lds_runs)
-      for (uint32_t i = tid; i < r.nch; i += kBThreads) {
-        runs[i] = r.row[i];
-        tb[i] = (a.cgov[r.c0 + i] % a.kt) * kGroupTiles;
-      }
-    for (uint32_t q = 0; q < 65536 / kQ; q++) {
+    for (uint32_t i = tid; i < NG; i += kBThreads) gb[i] = a.gbnd[(uint64_t)b * NG + i];
+    for (uint32_t qq = 0; qq < 65536 / kQ; qq++) {
       for (uint32_t i = tid; i < kQ; i += kBThreads) owner[i] = kEmpty;
       __syncthreads();
-      for (uint32_t i = r.lo + tid; i < r.hi; i += kBThreads) {
+      for (uint32_t i = q.x + tid; i < q.y; i += kBThreads) {
         const uint32_t x = a.in[i];
         const uint32_t sl = x >> 16;
-        if (sl / kQ != q || ((mslice[sl >> 5] >> (sl & 31)) & 1u)) continue;
-        atomicMin(&owner[sl % kQ], cand_key(a, r, lds_runs, runs, tb, i, x));
+        if (sl / kQ != qq || ((mslice[sl >> 5] >> (sl & 31)) & 1u)) continue;
+        atomicMin(&owner[sl % kQ], entry_record(group_of(gb, NG, i), x));
         atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
       }
       __syncthreads();
       for (uint32_t i = tid; i < kQ; i += kBThreads)
-        if (owner[i] != kEmpty) a.kflag[owner[i]] = 1;
+        if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
       __syncthreads();
     }
     flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
     __syncthreads();
   }
-}
-
-// rec_new[trec[t] + j] = 1 for every flagged owner key t * 256 + j; 4 keys
-// per thread (the flag array is padded to whole words)
-__global__ void k_key_records(const uint32_t* __restrict__ kflag4, const uint32_t* __restrict__ trec, uint64_t nwords,
-                              uint8_t* __restrict__ rec_new) {
-  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nwords) return;
-  const uint32_t f = kflag4[w];
-  if (!f) return;
-  const uint32_t key0 = (uint32_t)(w * 4), r0 = trec[key0 >> kRelBits] + (key0 & (kRecCap - 1));
-#pragma unroll
-  for (int j = 0; j < 4; j++)
-    if ((f >> (8 * j)) & 255u) rec_new[r0 + j] = 1;
 }
 
 // ------------------------------------------------------------------ scan ---
@@ -1319,18 +1161,20 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 
 // ------------------------------------------------------------------ host ---
 struct BucketPlan {
-  uint64_t n, nrec, nA, nB, T, kt, ng, gmax;
+  uint64_t n, nrec, nA, nB, T, NG, ng, gmax;
   WsPlan p;
-  size_t oTS, oTR, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oBD, oH2, oO2, oV2, oSP, oTK, oKF, oBN, oBP, oLB, oLQ, oSC;
+  size_t oTS, oTR, oGT, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oDT, oBD, oGB, oH2, oO2, oV2, oSP, oTK, oBN, oBP,
+      oLB, oLQ, oSC;
   BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
     nA = (n + kPT - 1) / kPT;
     nB = nrec ? (nrec - 1) / kRecCap : 0;
     T = nA + nB;
-    kt = (T + kGroupTiles - 1) / kGroupTiles;
-    ng = 256 * kt;
-    gmax = ng + nA;  // sum over groups of ceil(size / kPT) <= ng + n / kPT
+    NG = nrec ? (nrec - 1) / kGroupRecs + 1 : 1;
+    ng = 256 * NG;
+    gmax = ng + nA;  // sum over slice-groups of ceil(size / kPT) <= ng + n / kPT
     oTS = p.add((T + 1) * 4);
     oTR = p.add((T + 1) * 4);
+    oGT = p.add((NG + 1) * 4);
     oH1 = p.add(256 * T * 4);
     oO1 = p.add((256 * T + 1) * 4);
     oV1 = p.add(n * 4);
@@ -1340,13 +1184,14 @@ struct BucketPlan {
     oCG = p.add((gmax + 1) * 4);
     oCF = p.add(257 * 4);
     oCD = p.add(gmax * 16);
+    oDT = p.add(gmax * 8);
     oBD = p.add((uint64_t)kNumBuckets * 16);
+    oGB = p.add((uint64_t)kNumBuckets * NG * 4);
     oH2 = p.add(256 * gmax * 4);
     oO2 = p.add((256 * gmax + 1) * 4);
     oV2 = p.add(n * 4 + 64);  // the bucket kernel's 16-B loads may read past the end
     oSP = p.add(((uint64_t)kNumBuckets + 1) * 4);
     oTK = p.add(4);
-    oKF = p.add(T * kRecCap);
     oBN = p.add((uint64_t)kNumBuckets * 4);
     oBP = p.add(((uint64_t)kNumBuckets + 1) * 4);
     oLB = p.add((uint64_t)kNumBuckets * 4);
@@ -1355,7 +1200,22 @@ struct BucketPlan {
   }
 };
 
-size_t bucket_ws_bytes(uint64_t n, uint64_t nrec) { return BucketPlan(n, nrec).p.total; }
+// records per launch of the partitioned path (kMaxGroups groups); larger
+// batches run as consecutive record slices.  SG_TRIAGE_MAX_RECS lowers it
+// (tests of the slicing).
+static uint64_t max_launch_records() {
+  uint64_t m = (uint64_t)kMaxGroups * kGroupRecs;
+  if (const char* e = getenv("SG_TRIAGE_MAX_RECS")) {
+    const unsigned long long v = strtoull(e, nullptr, 10);
+    if (v > 0 && v < m) m = v;
+  }
+  return m;
+}
+
+size_t bucket_ws_bytes(uint64_t n, uint64_t nrec) {
+  const uint64_t m = max_launch_records();
+  return BucketPlan(n, nrec < m ? nrec : m).p.total;
+}
 
 // Grid of a persistent kernel: every block resident at once (CUs x blocks
 // per CU from the occupancy query), cached per kernel.
@@ -1376,21 +1236,16 @@ static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
   return grid;
 }
 
-// Flags-only triage of a device-resident batch (ctx lock held).
-int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
-                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
-  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
-    set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
-    return SG_EINVAL;
-  }
-  if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
+// One launch sequence over a batch of <= kMaxGroups groups (rec_new zeroed).
+static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
+                             const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
   if (n == 0) return SG_OK;
   if (nrec == 0) {
     set_error("bucket triage: signal entries without records");
     return SG_EINVAL;
   }
   const BucketPlan bp(n, nrec);
-  if (256 * bp.gmax >= 0xFFFFFFFFull) {
+  if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
     set_error("bucket triage: batch too large");
     return SG_EINVAL;
   }
@@ -1398,6 +1253,7 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   if (rc) return rc;
   uint32_t* tstart = (uint32_t*)ws_at(ctx, bp.oTS);
   uint32_t* trec = (uint32_t*)ws_at(ctx, bp.oTR);
+  uint32_t* gt = (uint32_t*)ws_at(ctx, bp.oGT);
   uint32_t* hist1 = (uint32_t*)ws_at(ctx, bp.oH1);
   uint32_t* goff1 = (uint32_t*)ws_at(ctx, bp.oO1);
   uint32_t* v1 = (uint32_t*)ws_at(ctx, bp.oV1);
@@ -1407,13 +1263,15 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   uint32_t* cgov = (uint32_t*)ws_at(ctx, bp.oCG);
   uint32_t* cfirst = (uint32_t*)ws_at(ctx, bp.oCF);
   uint4* cdesc = (uint4*)ws_at(ctx, bp.oCD);
+  uint2* dtile = (uint2*)ws_at(ctx, bp.oDT);
   uint4* bdesc = (uint4*)ws_at(ctx, bp.oBD);
+  uint32_t* gbnd = (uint32_t*)ws_at(ctx, bp.oGB);
   uint32_t* hist2 = (uint32_t*)ws_at(ctx, bp.oH2);
   uint32_t* goff2 = (uint32_t*)ws_at(ctx, bp.oO2);
   uint32_t* v2 = (uint32_t*)ws_at(ctx, bp.oV2);
   uint32_t* nspill = (uint32_t*)ws_at(ctx, bp.oSP);
   uint32_t* scr = (uint32_t*)ws_at(ctx, bp.oSC);
-  const uint32_t T = (uint32_t)bp.T, G = (uint32_t)bp.gmax;
+  const uint32_t T = (uint32_t)bp.T, G = (uint32_t)bp.gmax, NG = (uint32_t)bp.NG;
   const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
 
   // pass-1 tiles
@@ -1427,6 +1285,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   c1.start = tstart;
   c1.aux = trec;
   hipLaunchKernelGGL(k_cuts, dim3(div_up(bp.T + 1, 256)), dim3(256), 0, ctx->stream, c1);
+  hipLaunchKernelGGL(k_group_tiles, dim3(div_up(bp.NG + 1, 256)), dim3(256), 0, ctx->stream, d_off, bp.nA, NG, T,
+                     gt);
   {
     ScopedTimer tm(ctx, "p1_hist");
     if (((uintptr_t)d_vals & 15) == 0)
@@ -1463,14 +1323,15 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   // pass-2 chunks
   hipLaunchKernelGGL(k_group_chunks, dim3(div_up(bp.ng, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)goff1,
-                     bp.T, bp.kt, bp.ng, (uint32_t)n, nch);
+                     T, NG, (const uint32_t*)gt, bp.ng, nch);
   rc = scan32(ctx, nch, cbase, bp.ng, scr);
   if (rc) return rc;
   hipLaunchKernelGGL(k_chunk_list, dim3(div_up((bp.ng > bp.gmax ? bp.ng : bp.gmax) + 1, 256)), dim3(256), 0,
-                     ctx->stream, (const uint32_t*)goff1, bp.T, bp.kt, bp.ng, (uint32_t)n, (const uint32_t*)cbase,
-                     bp.gmax, cstart, cgov, cfirst);
+                     ctx->stream, (const uint32_t*)goff1, T, NG, (const uint32_t*)gt, bp.ng, (uint32_t)n,
+                     (const uint32_t*)cbase, bp.gmax, cstart, cgov, cfirst);
   hipLaunchKernelGGL(k_chunk_desc, dim3(div_up(bp.gmax, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)cstart,
-                     (const uint32_t*)cgov, gcount, bp.gmax, cdesc);
+                     (const uint32_t*)cgov, gcount, bp.gmax, (const uint32_t*)goff1, T, NG, (const uint32_t*)gt,
+                     cdesc, dtile);
   {
     ScopedTimer tm(ctx, "p2_hist");
     hipLaunchKernelGGL(k_hist_rep<true>, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
@@ -1478,28 +1339,22 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
   if (rc) return rc;
-  P2Args a2{v1, cdesc, gcount, goff1, T, (uint32_t)bp.kt, (uint32_t)n, goff2, hist2, v2};
+  P2Args a2{v1, cdesc, dtile, gcount, goff1, trec, T, NG, goff2, hist2, v2};
   {
     ScopedTimer tm(ctx, "p2_scatter");
     hipLaunchKernelGGL(k_p2_scatter, dim3(G), dim3(kPThreads), 0, ctx->stream, a2);
   }
   BucketArgs ba{};
   ba.in = v2;
-  ba.goff2 = goff2;
-  ba.g2 = gcount;
   ba.bdesc = bdesc;
-  ba.kt = (uint32_t)bp.kt;
-  ba.cfirst = cfirst;
-  ba.cgov = cgov;
-  ba.trec = trec;
+  ba.gbnd = gbnd;
+  ba.NG = NG;
   ba.mwords = mwords;
   ba.nwords = nwords;
   ba.rec_new = d_rec_new;
   ba.nspill = nspill;
   ba.spill = nspill + 1;
   ba.ticket = (uint32_t*)ws_at(ctx, bp.oTK);
-  ba.kflag = (uint8_t*)ws_at(ctx, bp.oKF);
-  SG_HIP(hipMemsetAsync(ba.kflag, 0, bp.T * kRecCap, ctx->stream));
   const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false>, kBThreads);
   uint64_t* ddbg = nullptr;
   if (dbg) {
@@ -1510,6 +1365,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   SG_HIP(hipMemsetAsync(nspill, 0, 4, ctx->stream));
   hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
                      gcount, (const uint32_t*)cfirst, bdesc);
+  hipLaunchKernelGGL(k_bucket_groups, dim3(div_up((uint64_t)kNumBuckets * NG, 256)), dim3(256), 0, ctx->stream,
+                     (const uint32_t*)goff2, gcount, (const uint32_t*)cbase, NG, gbnd);
   uint32_t* bnz = (uint32_t*)ws_at(ctx, bp.oBN);
   uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
   hipLaunchKernelGGL(k_bucket_nz, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc, bnz);
@@ -1530,11 +1387,6 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   {
     ScopedTimer tm(ctx, "bucket_spill");
     hipLaunchKernelGGL(k_bucket_direct, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
-  }
-  {
-    ScopedTimer tm(ctx, "key_records");
-    hipLaunchKernelGGL(k_key_records, dim3(div_up(bp.T * kRecCap / 4, 256)), dim3(256), 0, ctx->stream,
-                       (const uint32_t*)ba.kflag, (const uint32_t*)trec, bp.T * kRecCap / 4, d_rec_new);
   }
   SG_HIP(hipGetLastError());
   if (getenv("SG_DEBUG_PART")) {  // diagnostics: chunk and spill counts (syncs)
@@ -1588,6 +1440,42 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
             (t1 - t0) / 100.0, dur.front(), dur[dur.size() / 2], dur.back(), (unsigned long long)maxr);
   }
   return SG_OK;
+}
+
+__global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = off[i] - base;
+}
+
+// Flags-only triage of a device-resident batch (ctx lock held).  Batches of
+// more than max_launch_records() records run as consecutive record slices:
+// the sequential loop (fuzzer.go:665) cut between two records sees the same
+// maxSignal at every record.
+int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
+  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
+    return SG_EINVAL;
+  }
+  if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
+  const uint64_t m = max_launch_records();
+  if (nrec <= m) return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new);
+  uint64_t* roff = nullptr;
+  SG_HIP(hipMalloc(&roff, (m + 1) * 8));
+  int rc = SG_OK;
+  for (uint64_t r0 = 0; r0 < nrec && rc == SG_OK; r0 += m) {
+    const uint64_t r1 = nrec - r0 < m ? nrec : r0 + m;
+    uint64_t e[2] = {0, 0};
+    SG_HIP(hipMemcpyAsync(&e[0], d_off + r0, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipMemcpyAsync(&e[1], d_off + r1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1,
+                       e[0], roff);
+    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e[0], roff, e[1] - e[0], r1 - r0, d_rec_new + r0);
+  }
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  SG_HIP(hipFree(roff));
+  return rc;
 }
 
 }  // namespace sg

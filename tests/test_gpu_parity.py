@@ -529,3 +529,25 @@ def test_triage_dev_unaligned_input(C):
         assert np.array_equal(flags.cpu().numpy().astype(bool), np.asarray(ef).astype(bool))
         assert np.array_equal(ms.export(), om.export())
         assert np.array_equal(ns.export(), on.export())
+
+
+def test_triage_record_slices(C, monkeypatch):
+    """Batches above the per-launch record limit run as consecutive record
+    slices (sg_bucket.hip bucket_triage); the limit is lowered here so that
+    slices start mid-batch, at empty records and at group boundaries."""
+    rng = np.random.default_rng(131)
+    for limit, nrec in ((1000, 4321), (100000, 240000), (7, 50)):
+        monkeypatch.setenv("SG_TRIAGE_MAX_RECS", str(limit))
+        P = TwoPaths(C)
+        om, on = O.OSet(), O.OSet()
+        lens = rng.integers(0, 40, size=nrec)
+        lens[rng.integers(0, nrec, size=nrec // 5)] = 0
+        vals = rng.integers(0, 1 << 22, size=int(lens.sum()), dtype=np.uint64).astype(np.uint32)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        m0 = np.unique(vals[rng.integers(0, vals.size, size=vals.size // 3)])
+        P.add(m0)
+        om.add(m0)
+        _check_triage(P, (om, on), vals, off)
+        m, n = P.exports()
+        assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
+    monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
