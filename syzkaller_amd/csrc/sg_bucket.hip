@@ -785,7 +785,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
   __shared__ unsigned long long ht[kHash];
-  __shared__ uint32_t gb[kMaxGroups];  // the bucket's group boundaries
+  __shared__ alignas(16) uint32_t gb[kMaxGroups];  // the bucket's group boundaries (kEmpty past NG)
   __shared__ uint32_t sh_fail;         // some insert found the map full: the bucket spills
   __shared__ uint32_t sh_b[2];
   __shared__ uint4 sh_q[2];
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
 #pragma unroll
     for (int j = 0; j < (int)kGroupWords; j++) {
       const uint32_t i = j * kBThreads + tid;
-      if (i < NG) gb[i] = P.gw[j];
+      if (i < kMaxGroups) gb[i] = i < NG ? P.gw[j] : kEmpty;
     }
     // thread 0: resolve the pending ticket (published after the rounds) and take the next one
     uint32_t pend_b = kNumBuckets;
@@ -887,13 +887,17 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         // the record of each candidate: its group, found once per thread
         // and stepped forward (entries are in group order)
         uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
+        uint32_t nb = g + 1 < NG ? gb[g + 1] : kEmpty;  // next boundary
         do {
           const int u = __builtin_ctz(cm);
           cm &= cm - 1;
           uint32_t xu = x[0];
 #pragma unroll
           for (int k = 1; k < kBU; k++) xu = k == u ? x[k] : xu;
-          while (g + 1 < NG && gb[g + 1] <= p0 + u) g++;
+          while (nb <= p0 + u) {
+            g++;
+            nb = g + 1 < NG ? gb[g + 1] : kEmpty;
+          }
           if (!hash_insert64(ht, nbits, xu >> 16, entry_record(g, xu))) {
             ok = false;
             *(volatile uint32_t*)&sh_fail = 1;  // the others stop inserting (the bucket is redone)
