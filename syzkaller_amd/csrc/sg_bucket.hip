@@ -883,7 +883,8 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         ph[4] += t - tk;
         tk = t;
       }
-      if (cm && *(volatile uint32_t*)&sh_fail == 0) {
+      // (a relaxed atomic read: a volatile one would wait for every load in flight)
+      if (cm && __hip_atomic_load(&sh_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
         // the record of each candidate: its group, found once per thread
         // and stepped forward (entries are in group order)
         uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
@@ -900,7 +901,8 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
           }
           if (!hash_insert64(ht, nbits, xu >> 16, entry_record(g, xu))) {
             ok = false;
-            *(volatile uint32_t*)&sh_fail = 1;  // the others stop inserting (the bucket is redone)
+            // the others stop inserting (the bucket is redone)
+            __hip_atomic_store(&sh_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             break;
           }
         } while (cm);
