@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round profile: all GPU tests, smoke, the default bench, a kernel-trace
-# profile of a short bench, and separate FETCH_SIZE / WRITE_SIZE PMC passes
-# (plus the calibration kernels).  Outputs under gpurun_out/, TAG names them.
+# Round profile: all GPU tests, smoke, the default bench, the same default
+# bench under rocprofv3 --kernel-trace --stats, and separate FETCH_SIZE /
+# WRITE_SIZE PMC passes over a short bench (plus the calibration kernels).
+# Outputs under gpurun_out/, TAG names them.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -15,13 +16,11 @@ rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_$TAG.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --no-account > gpurun_out/prof_bench_$TAG.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py > gpurun_out/prof_bench_$TAG.log 2>&1
 rc=$?; echo "rocprof stats rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 -s KILL 300 rocprofv3 --pmc $C -d gpurun_out/pmc_${C}_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-account > gpurun_out/pmc_${C}_$TAG.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 -s KILL 300 rocprofv3 --pmc $C -d gpurun_out/pmccal_${C}_$TAG -o run --output-format csv -- python3 scripts/pmc_calib.py > gpurun_out/pmccal_${C}_$TAG.log 2>&1
-  rc=$?; echo "pmc calib $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 exit 0

@@ -5,7 +5,7 @@ the same bench command) into profiles/pmc_traffic.json.
 Per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half of the bytes of a wide coalesced streaming read, so the
 read side is doubled ("fetch_bytes_x2"); the raw value is kept too.  Only the
-full-size launches of each kernel are summarised (the largest grid)."""
+last STEPS launches of each kernel are summarised (the timed steps)."""
 import csv
 import json
 import sys
@@ -24,12 +24,12 @@ def load(path, counter):
             continue
         for key, pat in KERNELS.items():
             if pat in r["Kernel_Name"]:
-                out[key].append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0,
-                                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-    return out
+                out[key].append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"]) * 1024.0))
+    return {k: [(0, v) for _, v in sorted(x)] for k, x in out.items()}
 
 
-def main(fetch_csv, write_csv, out_json, tag):
+def main(fetch_csv, write_csv, out_json, tag, steps="2"):
+    steps = int(steps)
     f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     res = {"tag": tag, "source": [fetch_csv, write_csv],
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the same command; "
@@ -40,10 +40,8 @@ def main(fetch_csv, write_csv, out_json, tag):
         wl = w.get(k, [])
         if not fl or not wl:
             continue
-        g = max(x[0] for x in fl)
-        fb = [x[1] for x in fl if x[0] >= 0.9 * g]
-        gw = max(x[0] for x in wl)
-        wb = [x[1] for x in wl if x[0] >= 0.9 * gw]
+        fb = [x[1] for x in fl[-steps:]]  # the timed steps are the last launches
+        wb = [x[1] for x in wl[-steps:]]
         fetch = sum(fb) / len(fb)
         write = sum(wb) / len(wb)
         res["kernels"][k] = {"launches": len(fb), "fetch_bytes_raw": fetch, "fetch_bytes_x2": 2 * fetch,
@@ -53,4 +51,4 @@ def main(fetch_csv, write_csv, out_json, tag):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])

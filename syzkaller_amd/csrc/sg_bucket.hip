@@ -934,14 +934,24 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
     } else {
-      // a record is queued iff it owns some signal (fuzzer.go:678-690)
-      for (uint32_t i = tid; i < kHash; i += kBThreads) {
+      // a record is queued iff it owns some signal (fuzzer.go:678-690).  A
+      // record owns signals in many buckets: its flag is read first and
+      // written only while still clear, so its line is not dirtied (and
+      // written back) once per bucket
+      uint32_t own[kHash / kBThreads];
+      uint8_t seen[kHash / kBThreads];
+#pragma unroll
+      for (int k = 0; k < (int)(kHash / kBThreads); k++) {
+        const uint32_t i = k * kBThreads + tid;
         const unsigned long long v = ht[i];
-        if (v != kEmpty64) {
-          a.rec_new[(uint32_t)v] = 1;
-          ht[i] = kEmpty64;
-        }
+        own[k] = v != kEmpty64 ? (uint32_t)v : kEmpty;
+        ht[i] = kEmpty64;
       }
+#pragma unroll
+      for (int k = 0; k < (int)(kHash / kBThreads); k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
+#pragma unroll
+      for (int k = 0; k < (int)(kHash / kBThreads); k++)
+        if (!seen[k]) a.rec_new[own[k]] = 1;
       // words 4 tid .. +3: this block is their only writer
       uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords + 4 * tid;
       uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords + 4 * tid : nullptr;
