@@ -123,7 +123,7 @@ def row_c5(ctx, rng):
     t0 = time.perf_counter()
     got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites, ctx=ctx)
     wall = time.perf_counter() - t0
-    kt = ktime(ctx, ["report_query"])
+    kt = ktime(ctx, ["report_index", "report_query", "report_sites"])
     ctx.timing(False)
     sample = 2_000_000
     t1 = time.perf_counter()
@@ -131,9 +131,10 @@ def row_c5(ctx, rng):
     cpu = time.perf_counter() - t1
     got_s = C.cover_uncovered(q[:sample], 0xffffffff, starts, ends, sites, ctx=ctx)
     algo = 16 * nq
+    dev = sum(v for v in kt.values() if v)
     return {"row": "c5 cover report", "queries": nq, "sites": int(sites.size), "symbols": nsym,
-            "uncovered": int(got.size), "device_ms_query_kernel": kt.get("report_query"),
-            "wall_ms_host_api": wall * 1e3,
+            "uncovered": int(got.size), "kernels_ms": kt, "device_ms": dev,
+            "device_ms_query_kernel": kt.get("report_query"), "wall_ms_host_api": wall * 1e3,
             "query_GBs_algo": algo / (kt["report_query"] / 1e3) / 1e9 if kt.get("report_query") else None,
             "parity_2M_prefix": bool(np.array_equal(got_s, ref)), "cpu_oracle_s_2M": cpu, "cpu_cores": 1}
 

@@ -551,3 +551,34 @@ def test_triage_record_slices(C, monkeypatch):
         m, n = P.exports()
         assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
     monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
+
+
+def test_cover_uncovered_radix_edges(C):
+    """The report's radix indexes (sg_report.hip): symbol tables with gaps
+    spanning many index buckets (filled by the search pass), clusters far
+    apart, tables ending at the top of the u64 range, queries below the first
+    and above the last symbol, and base 0 with PCs that wrap below zero."""
+    rng = np.random.default_rng(141)
+    cases = []
+    # two clusters 2^40 apart: most buckets empty, one huge gap
+    s1, e1, p1 = _symtab(rng, 300, base=0x1000000)
+    far = np.uint64(1 << 40)
+    cases.append((np.concatenate([s1, s1 + far]), np.concatenate([e1, e1 + far]), np.concatenate([p1, p1 + far]), 0))
+    # a table ending at 2^64 - 1
+    s2, e2, p2 = _symtab(rng, 200)
+    top = np.uint64(0xffffffffffffffff) - max(e2[-1], p2[-1])
+    cases.append((s2 + top, e2 + top, p2 + top, 0xffffffff))
+    for starts, ends, sites, base in cases:
+        hi32 = np.uint64(base) << np.uint64(32)
+        q = (rng.choice(sites, size=20000) + np.uint64(5) - hi32).astype(np.uint32)
+        q = np.concatenate([q, rng.integers(0, 1 << 32, size=3000, dtype=np.uint64).astype(np.uint32),
+                            np.array([0, 1, 4, 5, 0xffffffff], np.uint32)])
+        got = C.cover_uncovered(q, base, starts, ends, sites)
+        exp = O.cover_uncovered(q, base, starts, ends, sites)
+        assert np.array_equal(got, exp)
+    # base 0: PCs below 5 wrap to the top of the range (Go uint64 arithmetic)
+    s3, e3, p3 = _symtab(rng, 100)
+    q = np.array([0, 3, 4, 5, 6, 100], np.uint32)
+    got = C.cover_uncovered(q, 0, s3, e3, p3)
+    exp = O.cover_uncovered(q, 0, s3, e3, p3)
+    assert np.array_equal(got, exp)
