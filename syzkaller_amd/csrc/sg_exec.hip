@@ -10,9 +10,10 @@
 // insert can change later lookups), so one wave owns one program and its
 // 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 64
 // edges at a time in parallel (pc ^ hash(prev pc) needs only a neighbour
-// shuffle); the table walk of one edge is one 4-lane LDS probe plus two
-// ballots, decided in scalar registers; kept edges are written with one
-// coalesced compaction store per 64 PCs.
+// shuffle) and decides their dedup speculatively: all 64 probe the table at
+// once, and the decisions are kept up to the first edge whose probe window
+// an earlier edge of the batch writes into (then the rest probe again);
+// kept edges are written with one coalesced compaction store per 64 PCs.
 #include "sg_internal.h"
 
 #include <cmath>
@@ -42,38 +43,64 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
   __syncthreads();
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const uint64_t c0 = prog_off[p], c1 = prog_off[p + 1];
+  // the program's calls are contiguous in the trace: the next 64 PCs are
+  // always in flight (the next batch of this call, or the next call's first)
+  const uint64_t pend = call_off[c1];
+  uint32_t npc = call_off[c0] + lane < pend ? pcs[call_off[c0] + lane] : 0u;
   for (uint64_t c = c0; c < c1; c++) {
     const uint64_t b = call_off[c], e = call_off[c + 1];
     uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
     uint64_t outpos = b;
     for (uint64_t j = b; j < e; j += 64) {
-      const uint64_t idx = j + lane;
-      const bool valid = idx < e;
-      const uint32_t pc = valid ? pcs[idx] : 0u;
+      const bool valid = j + lane < e;
+      const uint32_t pc = valid ? npc : 0u;
+      const uint64_t nj = j + 64 < e ? j + 64 : e;
+      npc = nj + lane < pend ? pcs[nj + lane] : 0u;
       const uint32_t h = exec_hash(pc);
       uint32_t hprev = __shfl_up(h, 1);
       if (lane == 0) hprev = carry;
       const uint32_t sig = pc ^ hprev;  // executor.h:393-395
       const int nvalid = (int)((e - j) < 64 ? (e - j) : 64);
       carry = __shfl(h, nvalid - 1);
+      // The 64 edges' dedup decisions, speculatively in parallel: every
+      // lane from `start` decides against the table as it stands (its four
+      // probe slots), and the decisions stand up to the first lane whose
+      // probe window holds a slot that an earlier undecided lane writes.
+      // Those are committed (their writes hit distinct slots); the rest
+      // decide again.  Each pass commits at least one edge; a pass usually
+      // commits a few dozen (8192 slots, 4-slot windows).
       uint64_t keep = 0;
-      for (int i = 0; i < nvalid; i++) {
-        const uint32_t s = __builtin_amdgcn_readlane(sig, i);
+      for (int start = 0; start < nvalid;) {
+        const bool act = lane >= start && lane < nvalid;
+        uint32_t t[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) t[q] = act ? table[(sig + (uint32_t)q) & (kDedupSize - 1)] : 1u;
         // executor.h:509-525: probe (s+q) % 8192 for q = 0..3 in order; a
         // slot equal to s means duplicate, an empty slot takes s, and when
         // all four are taken slot s % 8192 is overwritten.
-        const uint32_t t = lane < 4 ? table[(s + (uint32_t)lane) & (kDedupSize - 1)] : 1u;
-        const uint64_t eqm = __ballot(lane < 4 && t == s);
-        const uint64_t zm = __ballot(lane < 4 && t == 0u);
-        const uint64_t any = (eqm | zm) & 0xFull;
-        if (any) {
-          const int q = __ffsll((unsigned long long)any) - 1;
-          if ((eqm >> q) & 1ull) continue;  // dedup() == true: not written
-          if (lane == 0) table[(s + (uint32_t)q) & (kDedupSize - 1)] = s;
-        } else {
-          if (lane == 0) table[s & (kDedupSize - 1)] = s;
+        int q = 4;
+        bool dup = false;
+#pragma unroll
+        for (int k = 3; k >= 0; k--)
+          if (t[k] == sig || t[k] == 0u) {
+            q = k;
+            dup = t[k] == sig;
+          }
+        const uint32_t w = !act || dup ? 0xFFFFFFFFu : ((sig + (uint32_t)(q < 4 ? q : 0)) & (kDedupSize - 1));
+        // only the pass's writers can dirty a later edge: walk them (most
+        // edges of a trace are repeats, so writers are few)
+        bool dirty = false;
+        for (uint64_t wm = __ballot(w != 0xFFFFFFFFu); wm; wm &= wm - 1) {
+          const int i = __ffsll((unsigned long long)wm) - 1;
+          const uint32_t wi = __builtin_amdgcn_readlane(w, i);
+          dirty |= lane > i && ((wi - sig) & (kDedupSize - 1)) < 4u;
         }
-        keep |= 1ull << i;
+        const uint64_t dm = __ballot(act && dirty);
+        const int f = dm ? __ffsll((unsigned long long)dm) - 1 : nvalid;
+        const bool commit = lane >= start && lane < f && !dup;
+        if (commit) table[w] = sig;
+        keep |= __ballot(commit);
+        start = f;
       }
       if ((keep >> lane) & 1ull) tmp[outpos + __popcll(keep & lt)] = sig;
       outpos += __popcll(keep);
