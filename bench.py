@@ -148,9 +148,9 @@ KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "b
 
 def part_geometry(n_in, n_rec):
     """Tile / chunk counts of the partitioned path (sg_bucket.hip BucketPlan):
-    pass-1 tiles (8192 entries / 256 records each), and pass-2 chunks (about
+    pass-1 tiles (16384 entries / 256 records each), and pass-2 chunks (about
     one per non-empty (slice, 2^16-record group) pair beyond the full ones)."""
-    na = -(-int(n_in) // 8192)
+    na = -(-int(n_in) // 16384)
     t = na + (int(n_rec) - 1) // 256
     ng = (int(n_rec) - 1) // 65536 + 1
     return t, na + 256 * ng // 2

@@ -46,8 +46,8 @@
 
 namespace sg {
 
-constexpr int kPT = 8192;                    // entries per partition tile / chunk
-constexpr int kPThreads = 512;               // 8 waves
+constexpr int kPT = 16384;                   // entries per partition tile / chunk
+constexpr int kPThreads = 1024;              // 16 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
@@ -314,7 +314,8 @@ __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restri
   HistRegs r;
   hist_load(v, h, tid, r);
 #pragma unroll
-  for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < 256 * 32 / 4 / kPThreads; k++)
+    reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const uint32_t q0 = (h.s0 + 3) >> 2, q1 = h.s1 >> 2, cp = tid & 31;
 #pragma unroll
@@ -416,12 +417,13 @@ __device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, StF st, V
     }
   }
   __syncthreads();
-  if (tid < 64) {  // prefix max over the 256 words, 4 per lane
+  constexpr int kWL = kPT / 32 / 64;  // bitmap words per lane
+  if (tid < 64) {  // prefix max over the kPT / 32 words
     int run = -1;
-    int loc[4];
+    int loc[kWL];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int w = tid * 4 + j;
+    for (int j = 0; j < kWL; j++) {
+      const int w = tid * kWL + j;
       const uint32_t b = L.sbits[w];
       if (b) run = max(run, (int)sidx[w * 32 + 31 - __clz(b)]);
       loc[j] = run;
@@ -436,7 +438,7 @@ __device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, StF st, V
     if (tid == 0) ex = -1;
     ex = max(ex, (int)L.kinit);
 #pragma unroll
-    for (int j = 0; j < 4; j++) L.wmax[tid * 4 + j] = (IdxT)max(ex, loc[j]);
+    for (int j = 0; j < kWL; j++) L.wmax[tid * kWL + j] = (IdxT)max(ex, loc[j]);
   }
   __syncthreads();
 }
