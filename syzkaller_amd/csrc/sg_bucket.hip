@@ -951,9 +951,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       }
 #pragma unroll
       for (int k = 0; k < (int)(kHash / kBThreads); k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
-#pragma unroll
-      for (int k = 0; k < (int)(kHash / kBThreads); k++)
-        if (!seen[k]) a.rec_new[own[k]] = 1;
+      // (the flag reads are in flight while the slice's words go out)
       // words 4 tid .. +3: this block is their only writer
       uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords + 4 * tid;
       uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords + 4 * tid : nullptr;
@@ -970,6 +968,9 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
           }
         reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
       }
+#pragma unroll
+      for (int k = 0; k < (int)(kHash / kBThreads); k++)
+        if (!seen[k]) a.rec_new[own[k]] = 1;
     }
     __syncthreads();  // sh_b[0] / sh_q[0] are written
     if (kDbg) {
