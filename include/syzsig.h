@@ -116,7 +116,10 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
 		    size_t nrec, uint8_t* rec_new, uint32_t* diff_vals, uint64_t* diff_off, uint64_t* n_diff);
 /* Same, device-resident: d_vals (nvals = rec_off[nrec] elements), d_rec_off
  * (nrec+1), outputs d_rec_new (nrec bytes), optional d_diff_vals (capacity
- * nvals), d_diff_off (nrec+1).  Stream-ordered, no host synchronisation. */
+ * nvals), d_diff_off (nrec+1).  Stream-ordered, no host synchronisation,
+ * except that a flags-only batch of more than 8M records runs as record
+ * slices with one small device-to-host read per slice.  Limits: nvals <
+ * 2^32 - 2^15, nrec < 2^32 - 1. */
 int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_vals,
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec, uint8_t* d_rec_new,
 			uint32_t* d_diff_vals, uint64_t* d_diff_off);
