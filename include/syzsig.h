@@ -117,7 +117,7 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
 /* Same, device-resident: d_vals (nvals = rec_off[nrec] elements), d_rec_off
  * (nrec+1), outputs d_rec_new (nrec bytes), optional d_diff_vals (capacity
  * nvals), d_diff_off (nrec+1).  Stream-ordered, no host synchronisation,
- * except that a flags-only batch of more than 8M records runs as record
+ * except that a flags-only batch of more than 2^24 records runs as record
  * slices with one small device-to-host read per slice.  Limits: nvals <
  * 2^32 - 2^15, nrec < 2^32 - 1. */
 int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_vals,
