@@ -210,6 +210,38 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
 		       const uint64_t* sym_end, size_t nsym, const uint64_t* all_pcs, size_t nall, uint64_t* out,
 		       size_t* nout);
 
+/* ---- executor output ingest (pkg/ipc/ipc_linux.go:168-307) ---------------- */
+/* readOutCoverage over a batch of programs.  Program p's output region (the
+ * layout executor/executor.h:369-427 writes) is out[out_off[p] ..
+ * out_off[p+1]); its calls are records call_off[p] .. call_off[p+1]
+ * (len(p.Calls)); call_nums[r] = c.Meta.ID of record r, or NULL to skip that
+ * check (ipc_linux.go:225-230).  Per record: err = Errno (-1 = not executed,
+ * else the executor's u32 errno), fault = FaultInjected, its Signal words at
+ * sig_vals[sig_off[r] .. sig_off[r+1]) and, when cov_off / cov_vals are
+ * given, its Cover words likewise.  Comparisons are walked, not decoded.
+ * status[p] = SG_IPC_OK or the Go error path the reader took; the records
+ * keep what the reader had set before it (partial info, as in Go).
+ * sig_vals / cov_vals capacity: out_off[nprog] words always suffices.
+ * Record order is program-major, call index ascending (fuzzer.go:665). */
+#define SG_IPC_OK 0
+#define SG_IPC_NO_NCMD 1      /* ipc_linux.go:197-200 */
+#define SG_IPC_SHORT_HEADER 2 /* :216-219 */
+#define SG_IPC_BAD_INDEX 3    /* :220-224 */
+#define SG_IPC_BAD_CALLNUM 4  /* :225-230 */
+#define SG_IPC_DOUBLE 5       /* :231-235 */
+#define SG_IPC_SIGNAL_SIZE 6  /* :238-242 */
+#define SG_IPC_COVER_SIZE 7   /* :247-251 */
+#define SG_IPC_COMPS_SHORT 8  /* :258-290 */
+#define SG_IPC_COMPS_TYPE 9   /* :266-270 */
+int sg_ipc_parse(sg_ctx* ctx, const uint32_t* out, const uint64_t* out_off, const uint64_t* call_off,
+		 const uint32_t* call_nums, size_t nprog, int64_t* err, uint8_t* fault, int32_t* status,
+		 uint64_t* sig_off, uint32_t* sig_vals, uint64_t* cov_off, uint32_t* cov_vals);
+/* Device form: every pointer is device memory, stream-ordered, no host sync. */
+int sg_ipc_parse_dev(sg_ctx* ctx, const uint32_t* d_out, const uint64_t* d_out_off, const uint64_t* d_call_off,
+		     const uint32_t* d_call_nums, uint64_t nprog, uint64_t nrec, int64_t* d_errno, uint8_t* d_fault,
+		     int32_t* d_status, uint64_t* d_sig_off, uint32_t* d_sig_vals, uint64_t* d_cov_off,
+		     uint32_t* d_cov_vals);
+
 #ifdef __cplusplus
 }
 #endif

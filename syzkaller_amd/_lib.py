@@ -6,7 +6,7 @@ calls fail loudly (ImportError here, SyzSigError from compute calls).
 """
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsyzsig.so")  # override: diagnostics builds
@@ -73,6 +73,10 @@ SIGNATURES = {
     "sg_gen_zipf_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_double, c_uint32, c_uint64, c_uint64, c_uint32,
                                        c_uint32, c_void_p]),
     "sg_cover_uncovered": (c_int, [c_void_p, P32, c_size_t, c_uint32, P64, P64, c_size_t, P64, c_size_t, P64, PSZ]),
+    "sg_ipc_parse": (c_int, [c_void_p, P32, P64, P64, P32, c_size_t, POINTER(c_int64), P8, POINTER(c_int32), P64, P32,
+                             P64, P32]),
+    "sg_ipc_parse_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 

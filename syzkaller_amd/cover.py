@@ -331,3 +331,34 @@ def cover_uncovered(cov, base, sym_start, sym_end, all_pcs, ctx=None):
     call("sg_cover_uncovered", _ctx(ctx).h, _p32(c), c.size, base, _p64(ss), _p64(se), ss.size, _p64(ap), ap.size,
          _p64(out), byref(n))
     return out[: n.value]
+
+
+# pkg/ipc/ipc_linux.go:168-307 status codes (include/syzsig.h SG_IPC_*)
+IPC_OK, IPC_NO_NCMD, IPC_SHORT_HEADER, IPC_BAD_INDEX, IPC_BAD_CALLNUM, IPC_DOUBLE = 0, 1, 2, 3, 4, 5
+IPC_SIGNAL_SIZE, IPC_COVER_SIZE, IPC_COMPS_SHORT, IPC_COMPS_TYPE = 6, 7, 8, 9
+
+
+def ipc_parse(out, out_off, call_off, call_nums=None, cover=True, ctx=None):
+    """readOutCoverage (pkg/ipc/ipc_linux.go:168-307) over a batch of program
+    output regions.  Returns (errno int64[nrec], fault u8[nrec], status
+    int32[nprog], sig_vals, sig_off, cov_vals, cov_off); cov_* are None when
+    cover=False."""
+    w, oo, co = _u32(out), _u64(out_off), _u64(call_off)
+    nprog = oo.size - 1
+    assert co.size == nprog + 1
+    nrec = int(co[-1])
+    nums = None if call_nums is None else _u32(call_nums)
+    assert nums is None or nums.size == nrec
+    err = np.empty(max(nrec, 1), dtype=np.int64)
+    fault = np.empty(max(nrec, 1), dtype=np.uint8)
+    status = np.empty(max(nprog, 1), dtype=np.int32)
+    sv = np.empty(max(w.size, 1), dtype=U32)
+    so = np.empty(nrec + 1, dtype=U64)
+    cv = np.empty(max(w.size, 1), dtype=U32) if cover else None
+    cvo = np.empty(nrec + 1, dtype=U64) if cover else None
+    call("sg_ipc_parse", _ctx(ctx).h, _p32(w), _p64(oo), _p64(co), _p32(nums) if nums is not None else None, nprog,
+         err.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _p8(fault),
+         status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _p64(so), _p32(sv),
+         _p64(cvo) if cover else None, _p32(cv) if cover else None)
+    return (err[:nrec], fault[:nrec], status[:nprog], sv[: int(so[-1])], so,
+            cv[: int(cvo[-1])] if cover else None, cvo)
