@@ -14,7 +14,9 @@ point (PCIe staging included), and the oracle on a bounded sample:
       sites and 50k symbols.
   a0  executor edge signal (executor.h:389-401, :497-526): 8192 programs x 16
       calls x 1024 PCs.
-Usage: python bench_rows.py [c1 c4 c5 a0]
+  ipc executor output ingest (pkg/ipc/ipc_linux.go:168-307): 16Ki program
+      output regions x 16 calls x 1024 signal words.
+Usage: python bench_rows.py [c1 c4 c5 a0 ipc]
 """
 import json
 import os
@@ -161,11 +163,56 @@ def row_a0(ctx, rng):
             "pcs_per_s": npcs / (sum(kt.values()) / 1e3)}
 
 
+def row_ipc(ctx, rng):
+    """pkg/ipc/ipc_linux.go:168-307 over 16Ki program output regions x 16
+    calls x 1024 signal words (executor.h:369-427 layout), HBM-resident."""
+    import torch
+
+    from syzkaller_amd._lib import call
+
+    nprog, calls, nsig = 16384, 16, 1024
+    rec_w = 7 + nsig
+    reg_w = 1 + calls * rec_w
+    reg = np.empty((nprog, reg_w), np.uint32)
+    reg[:, 0] = calls
+    body = reg[:, 1:].reshape(nprog, calls, rec_w)
+    body[:, :, 0] = np.arange(calls, dtype=np.uint32)  # call index
+    body[:, :, 1] = 7  # call number
+    body[:, :, 2:4] = 0
+    body[:, :, 4] = nsig
+    body[:, :, 5:7] = 0
+    body[:, :, 7:] = rng.integers(0, 1 << 32, size=(nprog, calls, nsig), dtype=np.uint32)
+    nrec, nw = nprog * calls, reg.size
+    d_out = torch.from_numpy(reg.reshape(-1).view(np.int32)).cuda()
+    oo = torch.arange(0, nw + 1, reg_w, dtype=torch.int64, device="cuda")
+    co = torch.arange(0, nrec + 1, calls, dtype=torch.int64, device="cuda")
+    err = torch.empty(nrec, dtype=torch.int64, device="cuda")
+    fi = torch.empty(nrec, dtype=torch.uint8, device="cuda")
+    st = torch.empty(nprog, dtype=torch.int32, device="cuda")
+    so = torch.empty(nrec + 1, dtype=torch.int64, device="cuda")
+    sv = torch.empty(nw, dtype=torch.int32, device="cuda")
+    args = (ctx.h, d_out.data_ptr(), oo.data_ptr(), co.data_ptr(), None, nprog, nrec, err.data_ptr(), fi.data_ptr(),
+            st.data_ptr(), so.data_ptr(), sv.data_ptr(), None, None)
+    call("sg_ipc_parse_dev", *args)  # warm
+    ctx.timing(True)
+    call("sg_ipc_parse_dev", *args)
+    kt = ktime(ctx, ["ipc_walk", "ipc_gather", "scan"])
+    ctx.timing(False)
+    torch.cuda.synchronize()
+    src = d_out.view(nprog, reg_w)[:, 1:].reshape(nprog, calls, rec_w)[:, :, 7:].reshape(-1)
+    parity = bool((st == 0).all().item() and (so[-1].item() == nrec * nsig) and torch.equal(sv[: nrec * nsig], src))
+    dev = sum(kt.values())
+    algo = 4 * nprog + 28 * nrec + 8 * nrec * nsig + 8 * nrec + 9 * nrec
+    return {"row": "f3 executor output ingest", "programs": nprog, "records": nrec, "signal_words": nrec * nsig,
+            "kernels_ms": kt, "device_ms": dev, "device_GBs_algo": algo / (dev / 1e3) / 1e9,
+            "frac_hbm": algo / (dev / 1e3) / 1e9 / HBM, "parity_full": parity}
+
+
 def main():
     import torch
 
     torch.cuda.set_device(0)
-    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0"]
+    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc"]
     ctx = C.Context(0)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(2026)
