@@ -143,7 +143,16 @@ __global__ __launch_bounds__(256) void k_ipc_gather(const uint32_t* __restrict__
   if (r >= nrec) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t n = off[r + 1] - off[r], s = src[r], d = off[r];
-  for (uint64_t i = lane; i < n; i += 64) vals[d + i] = out[s + i];
+  uint64_t i = lane;
+  // eight loads in flight per lane before their stores
+  for (; i + 7 * 64 < n; i += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = __builtin_nontemporal_load(out + s + i + 64 * k);
+#pragma unroll
+    for (int k = 0; k < 8; k++) vals[d + i + 64 * k] = v[k];
+  }
+  for (; i < n; i += 64) vals[d + i] = out[s + i];
 }
 
 }  // namespace sg
