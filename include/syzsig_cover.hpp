@@ -230,4 +230,40 @@ inline Records Poll(cover::SignalMap& maxSignal, const Records& polls) {
 }
 
 }  // namespace manager
+
+namespace ipc {
+
+// readOutCoverage (pkg/ipc/ipc_linux.go:168-307) over a batch of programs:
+// program p's output words are out[out_off[p] .. out_off[p+1]), its calls
+// records call_off[p] .. call_off[p+1]; call_nums (c.Meta.ID per record) may
+// be empty to skip that check.  status[p] is SG_IPC_OK or the Go error path.
+struct CallInfos {
+  std::vector<int64_t> errno_;  // Errno: -1 = not executed
+  std::vector<uint8_t> fault;   // FaultInjected
+  std::vector<int32_t> status;  // per program
+  Records signal, cover;        // per record, in record order
+};
+
+inline CallInfos ReadOutBatch(const std::vector<uint32_t>& out, const std::vector<uint64_t>& out_off,
+                              const std::vector<uint64_t>& call_off, const std::vector<uint32_t>& call_nums = {},
+                              Context& ctx = Context::Default()) {
+  const size_t nprog = out_off.size() - 1, nrec = call_off.back();
+  CallInfos r;
+  r.errno_.resize(nrec);
+  r.fault.resize(nrec);
+  r.status.resize(nprog);
+  r.signal.vals.resize(out.size());
+  r.signal.off.resize(nrec + 1);
+  r.cover.vals.resize(out.size());
+  r.cover.off.resize(nrec + 1);
+  check("sg_ipc_parse",
+        sg_ipc_parse(ctx.get(), out.data(), out_off.data(), call_off.data(), call_nums.empty() ? nullptr : call_nums.data(),
+                     nprog, r.errno_.data(), r.fault.data(), r.status.data(), r.signal.off.data(), r.signal.vals.data(),
+                     r.cover.off.data(), r.cover.vals.data()));
+  r.signal.vals.resize(r.signal.off.back());
+  r.cover.vals.resize(r.cover.off.back());
+  return r;
+}
+
+}  // namespace ipc
 }  // namespace syz

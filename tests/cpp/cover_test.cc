@@ -153,6 +153,18 @@ int main(int argc, char** argv) {
   EXPECT((t.diff == std::vector<uint32_t>{5, 5, 6, 7}), "Execute diff");
   EXPECT((newSignal.Export() == std::vector<uint32_t>{5, 6, 7}), "newSignal");
   EXPECT(maxSignal.size() == 6, "maxSignal size");
+  // executor output reader (ipc_linux.go:168-307): program 0 runs call 1 then
+  // call 0; program 1 claims call index 5 of 2 (the Go reader's index error)
+  std::vector<uint32_t> out = {2, 1, 20, 14, 1, 2, 1, 0, 7, 8, 0x81000010,
+                               0, 10, 0, 0, 1, 0, 0, 9,
+                               1, 5, 0, 0, 0, 0, 0, 0};
+  auto ci = syz::ipc::ReadOutBatch(out, {0, 19, 27}, {0, 2, 4}, {10, 20, 0, 0});
+  EXPECT((ci.status == std::vector<int32_t>{SG_IPC_OK, SG_IPC_BAD_INDEX}), "ReadOutBatch status");
+  EXPECT((ci.errno_ == std::vector<int64_t>{0, 14, -1, -1}), "ReadOutBatch errno");
+  EXPECT((ci.fault == std::vector<uint8_t>{0, 1, 0, 0}), "ReadOutBatch fault");
+  EXPECT((ci.signal.vals == std::vector<uint32_t>{9, 7, 8}), "ReadOutBatch signal");
+  EXPECT((ci.signal.off == std::vector<uint64_t>{0, 1, 3, 3, 3}), "ReadOutBatch signal offsets");
+  EXPECT((ci.cover.vals == std::vector<uint32_t>{0x81000010}), "ReadOutBatch cover");
   if (failures) {
     std::fprintf(stderr, "FAIL: %d\n", failures);
     return 1;
