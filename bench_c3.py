@@ -1,0 +1,247 @@
+"""bench.py's multi-GPU workloads (one process per GPU, RCCL over xGMI).
+
+C3 (BASELINE.json configs[2]): ONE batch of N x 128Ki programs (16 calls x
+1024 Zipf PCs each, the C2 recipe; N=8 is C3's 1Mi-program batch), its records
+split contiguously over the N ranks, triaged as the single sequential loop of
+syz-fuzzer/fuzzer.go:645-693 by the hash-sharded protocol of
+syzkaller_amd/shard.py against a replicated 16M-entry maxSignal snapshot
+(restored before every step, as at N=1).  Weak scaling: 128Ki programs per GPU.
+
+fuzzers: one independent fuzzer per GPU, each triaging its own batches, with
+the Poll merge (fuzzer.go:358-364, manager.go:949-962, fuzzer.go:392-398) as an
+RCCL OR-exchange of the newSignal bitmaps (syzkaller_amd/dist.py).
+"""
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, kernel_table, n_uniq, pmc_bytes_per_step, step_bytes,
+                   triage, HBM_PEAK_GBS, SignalSet, U32_WORDS, StepTimer)
+from syzkaller_amd.shard import Comm, HipStages, ShardedTriage
+
+SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
+                                "set_add"]
+
+
+def _max_over_ranks(x, world):
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum_over_ranks(x, world):
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def run_c3(ctx, args, cfg, rank, world):
+    calls, nprog = cfg["calls"], cfg["programs"]
+    g = Gen(cfg)
+    t_gen = time.perf_counter()
+    # the replicated snapshot: every rank builds the same 16M-entry maxSignal
+    # from the same warm batch (deterministic, so no broadcast is needed)
+    warm = g.zipf(ctx, dict(cfg, programs=nprog), 2_000_000, prog_base=0)
+    batches = [g.zipf(ctx, cfg, 3_000 + k, prog_base=rank * nprog) for k in range(args.warmup + args.steps)]
+    del g
+    t_gen = time.perf_counter() - t_gen
+    rec_new = torch.empty(max(b.nrec for b in batches), dtype=torch.uint8, device="cuda")
+    maxsig, newsig, m0set = SignalSet(ctx), SignalSet(ctx), SignalSet(ctx)
+    build_m0(ctx, m0set, warm, calls, args.m0, rec_new)
+    del warm
+    m0_count = len(m0set)
+    if world > 1:
+        counts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
+        dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device="cuda"))
+        assert len({int(c.item()) for c in counts}) == 1, "maxSignal snapshots differ between ranks"
+    tri = ShardedTriage(HipStages(ctx), Comm())
+    rec_base = rank * nprog * calls
+
+    def step(b):
+        call("sg_set_copy", maxsig.h, m0set.h)
+        tri.step(maxsig, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
+
+    for b in batches[: args.warmup]:
+        step(b)
+    torch.cuda.synchronize()
+    timed = batches[args.warmup:]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    for b in timed:
+        step(b)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernels = kernel_table(ctx, SHARD_KERNELS, args.steps)
+    ctx.timing(False)
+    wall = _max_over_ranks(wall, world)
+    units = _sum_over_ranks(sum(b.nvals for b in timed), world)
+    # accounting, outside the timed region: first timed batch
+    b = timed[0]
+    call("sg_set_copy", maxsig.h, m0set.h)
+    import ctypes
+    c = ctypes.c_uint64()
+    call("sg_set_count_missing_dev", maxsig.h, b.vals.data_ptr(), b.nvals, ctypes.byref(c))
+    tri.step(maxsig, None, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
+    torch.cuda.synchronize()
+    last = dict(tri.last)
+    queued = int(rec_new[: b.nrec].sum().item())
+    acct_rank = {"n_in": b.nvals, "n_uniq": n_uniq(b, calls), "n_cand": c.value, "n_rec": b.nrec,
+                 "n_queued": queued, "pairs_sent": last["pairs_sent"], "pairs_received": last["pairs_received"]}
+    acct = {k: _sum_over_ranks(v, world) for k, v in acct_rank.items()}
+    acct["n_new_signal"] = last["new_signal"]
+    acct["n_diff"] = last["new_signal"]  # diff multiplicity not emitted by the sharded path
+    acct["queued_frac"] = acct["n_queued"] / acct["n_rec"] if acct["n_rec"] else None
+    acct["maxsignal_after"] = len(maxsig)
+    acct["consistent"] = acct["maxsignal_after"] == m0_count + last["new_signal"]
+    ms_step = wall * 1e3 / args.steps
+    # roofline: whole-job step bytes over all ranks / step time / aggregate peak
+    bpr = step_bytes(acct) / world
+    roof = {"bound": "hbm", "achieved": round(bpr / (ms_step / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(bpr / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "scope": "whole sharded step per GPU (wall clock, max over ranks; exchanges included)",
+            "algo_bytes_per_step_per_gpu": bpr,
+            "formula": "SURVEY.md §8(d) C2/C3 bytes over all ranks / N (N_out taken as the new-signal count)"}
+    xgmi = 8 * acct["pairs_sent"] / world + 4 * (acct["n_rec"] / 32) / world + 4 * last["new_signal"]
+    if rank != 0:
+        return None
+    return {
+        "metric": METRIC,
+        "value": units / wall,
+        "unit": "PCs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (Zipf(1.1) PC traces generated on the GPU, counter-based PRNG)",
+        "config": {
+            "workload": f"C3 recipe: one batch of {world} x {nprog} programs x {calls} calls x {cfg['pcs_per_call']} "
+                        f"Zipf PCs (N=8: C3's 1Mi programs), records split contiguously, {nprog} programs "
+                        f"({nprog * calls} call records) per rank; one sequential triage loop hash-sharded by signal "
+                        f"(RCCL all-to-all of candidates, OR of record-flag slices, all-gather of new signal) vs a "
+                        f"replicated {m0_count}-entry maxSignal restored before every step",
+            "programs_per_gpu": nprog, "batch_programs": world * nprog, "calls": calls,
+            "pcs_per_call": cfg["pcs_per_call"], "signal_per_step": units / args.steps,
+            "maxsignal_start": m0_count, "queued_frac": acct["queued_frac"],
+            "parallelism": f"signal-sharded x{world} (one rank per GPU, RCCL)",
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+        "kernels": kernels,
+        "accounting": acct,
+        "exchange_bytes_per_rank_per_step": xgmi,
+        "path": "sharded (syzkaller_amd/shard.py + sg_shard.hip)",
+        "gen_s": round(t_gen, 2),
+    }
+
+
+class Poll:
+    """newSignal drain + manager merge (fuzzer.go:358-364, manager.go:949-962,
+    fuzzer.go:392-398) between independent per-GPU fuzzers: every rank's
+    maxSignal gains every other rank's new signal, as an OR-exchange of the
+    newSignal bitmaps (syzkaller_amd/dist.py), one step behind on its own
+    stream (the reference polls asynchronously, fuzzer.go:331-346)."""
+
+    def __init__(self, ctx, world):
+        import ctypes
+        from syzkaller_amd.dist import OrExchange
+        from syzkaller_amd._lib import lib
+
+        self.lib = lib
+        self.bufs = [torch.zeros(U32_WORDS, dtype=torch.int32, device="cuda") for _ in range(2)]
+        self.sets = []
+        for buf in self.bufs:
+            h = ctypes.c_void_p()
+            call("sg_set_wrap_dev", ctx.h, buf.data_ptr(), ctypes.byref(h))
+            self.sets.append(h)
+        self.k = 0
+        self.comm = torch.cuda.Stream()
+        self.ex = [OrExchange(buf) for buf in self.bufs]
+        self.merged = [None, None]
+        self.done = [None, None]
+
+    def newsig(self):
+        class _H:
+            pass
+        h = _H()
+        h.h = self.sets[self.k % 2]
+        return h
+
+    def after_triage(self, maxsig):
+        slot = self.k % 2
+        self.k += 1
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ev)
+            merged = self.ex[slot](self.bufs[slot])
+            done = torch.cuda.Event()
+            done.record(self.comm)
+        self.merged[slot], self.done[slot] = merged, done
+        self._apply(self.k % 2, maxsig)
+
+    def _apply(self, slot, maxsig):
+        if self.done[slot] is None:
+            return
+        torch.cuda.current_stream().wait_event(self.done[slot])
+        call("sg_set_or_dev", maxsig.h, self.merged[slot].data_ptr())  # fuzzer.go:392-398
+        self.bufs[slot].zero_()
+        self.done[slot] = None
+
+    def drain(self, maxsig):
+        for d in (1, 0):
+            self._apply((self.k + d) % 2, maxsig)
+
+    def close(self):
+        for h in self.sets:
+            self.lib.sg_set_destroy(h)
+
+
+def run_fuzzers(ctx, args, cfg, rank, world):
+    calls = cfg["calls"]
+    g = Gen(cfg)
+    warm = g.zipf(ctx, cfg, 2_000_000 + rank)
+    batches = [g.zipf(ctx, cfg, 1_000 + 100_000 * rank + k) for k in range(args.warmup + args.steps)]
+    del g
+    rec_new = torch.empty(max(b.nrec for b in batches), dtype=torch.uint8, device="cuda")
+    maxsig = SignalSet(ctx)
+    build_m0(ctx, maxsig, warm, calls, args.m0, rec_new)
+    del warm
+    poll = Poll(ctx, world)
+    for b in batches[: args.warmup]:
+        triage(ctx, maxsig, poll.newsig(), b, rec_new)
+        poll.after_triage(maxsig)
+    poll.drain(maxsig)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for b in batches[args.warmup:]:
+        triage(ctx, maxsig, poll.newsig(), b, rec_new)
+        poll.after_triage(maxsig)
+    poll.drain(maxsig)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = _max_over_ranks(time.perf_counter() - t0, world)
+    units = _sum_over_ranks(sum(b.nvals for b in batches[args.warmup:]), world)
+    poll.close()
+    if rank != 0:
+        return None
+    return {"metric": METRIC, "value": units / wall, "unit": "PCs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "fuzzers: one independent C2 fuzzer per GPU, Poll as an RCCL OR-exchange of "
+                                   "newSignal bitmaps (maxSignal grows across steps)",
+                       "programs_per_gpu": cfg["programs"], "parallelism": f"independent fuzzers x{world}"},
+            "roofline": None, "cpu_baseline": None, "path": "partitioned per rank + OR-exchange"}

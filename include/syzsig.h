@@ -68,6 +68,12 @@ int sg_ctx_timing(sg_ctx* ctx, int enable);
 /* Total device milliseconds and launch count recorded for kernel `name`
  * (e.g. "triage_claim"); syncs the stream. */
 int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* launches);
+/* Context counters: "owner_resets" (first-owner table generations started
+ * after the key space ran out), "owner_floor", "owner_key_space",
+ * "max_launch_records".  The environment switches SG_OWNER_KEY_SPACE and
+ * SG_TRIAGE_MAX_RECS (test knobs that lower the key space / the records per
+ * partitioned launch) are read once, by sg_ctx_create. */
+int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
 
 /* ---- signal sets: replace map[uint32]struct{} ---------------------------- */
 /* maxSignal / corpusSignal / newSignal (syz-fuzzer/fuzzer.go:65-68) and
@@ -123,6 +129,39 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
 int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_vals,
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec, uint8_t* d_rec_new,
 			uint32_t* d_diff_vals, uint64_t* d_diff_off);
+
+/* ---- one batch hash-sharded by signal across GPUs ------ */
+/* The sequential loop of sg_triage_batch (syz-fuzzer/fuzzer.go:645-693) over a
+ * batch whose call records are split contiguously across G ranks, one GPU each
+ * (the host protocol and its RCCL exchanges: syzkaller_amd/shard.py).  The
+ * signal space is sharded by sg_shard_of(s, G), the murmur3 finaliser of s
+ * scaled to [0, G); G <= 64.  Every rank holds the same maxSignal snapshot. */
+int sg_shard_of(uint32_t s, uint32_t nshards);
+/* Local stage, on the rank holding records rec_base .. rec_base+nrec-1 of the
+ * batch (d_rec_off[0] == 0, rec_base + nrec < 2^32): every distinct s of those
+ * records that is not in `snapshot`, once, as the pair {s, rec_base + its
+ * first record}, grouped by owning shard: shard k's pairs are pairs
+ * d_shard_off[k] .. d_shard_off[k+1]-1 of d_pairs (u32 pairs, capacity nvals
+ * pairs; d_shard_off: G+1 device u64).  The snapshot is only read.  Any
+ * number of entries (record slices of < 2^31 entries each). */
+int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_vals, const uint64_t* d_rec_off,
+			    uint64_t nvals, uint64_t nrec, uint64_t rec_base, uint32_t nshards, uint32_t* d_pairs,
+			    uint64_t* d_shard_off);
+/* Owner stage, on the shard's rank, over the npairs pairs {s, record} it
+ * received from all ranks (record < nrec_total, the batch's record count):
+ * owner(s) = the smallest record holding s.  Sets bit r of d_rec_bits (nrec_total
+ * bits, cleared first) for every owner record r -- record r is queued for
+ * triage iff some shard sets its bit (fuzzer.go:678-690) -- and writes every
+ * distinct s once to d_new_vals (capacity npairs); *d_nnew (device u64) = count. */
+int sg_shard_owners_dev(sg_ctx* ctx, const uint32_t* d_pairs, uint64_t npairs, uint64_t nrec_total,
+			uint32_t* d_rec_bits, uint32_t* d_new_vals, uint64_t* d_nnew);
+/* d_rec_new[i] = bit rec_lo + i of the OR of nparts record bitsets, part k
+ * being words k*words_per_part .. of d_bits, each starting at word rec_lo/32. */
+int sg_shard_flags_dev(sg_ctx* ctx, const uint32_t* d_bits, uint32_t nparts, uint64_t words_per_part, uint64_t rec_lo,
+		       uint64_t nrec, uint8_t* d_rec_new);
+/* SignalAdd of n device-resident values (fuzzer.go:673-674 for the new signal
+ * every shard found). */
+int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
 
 /* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:
  * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */
@@ -200,6 +239,14 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
  * prog_base .. prog_base+nprog-1, program-major. */
 int sg_gen_zipf_traces_dev(sg_ctx* ctx, uint64_t universe_seed, uint64_t trace_seed, double zipf_s, uint32_t nranks,
 			   uint64_t prog_base, uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs);
+/* A fuzzer's steady state: programs drawn from a fixed population of npop
+ * programs (member m's trace is the one sg_gen_zipf_traces_dev gives program m
+ * under trace seed pop_seed), re-executed with flaky coverage -- each PC is
+ * replaced by a fresh Zipf draw with probability `noise`.  The member of
+ * program p and its noise are counter-based in (trace_seed, p). */
+int sg_gen_population_traces_dev(sg_ctx* ctx, uint64_t universe_seed, uint64_t pop_seed, uint64_t npop,
+				 uint64_t trace_seed, double noise, double zipf_s, uint32_t nranks, uint64_t prog_base,
+				 uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs);
 
 /* ---- cover report (syz-manager/cover.go:91-103, :257-307) ----------------- */
 /* pcs[i] = RestorePC(cov[i], base) - 5; returns the uncovered PC set of

@@ -90,7 +90,11 @@ def write_call(call_index, call_num, errno, fault, signal, cover=(), comps=(), w
 
 def parse_batch(out, out_off, call_off, call_nums=None):
     """The batch contract of sg_ipc_parse, one read_out_coverage per program:
-    (errno[], fault[], status[], sig_lists[], cov_lists[]) in record order."""
+    (errno[], fault[], status[], sig_lists[], cov_lists[]) in record order.
+    A program whose read failed keeps its records' errno / fault (the reader's
+    partial state) but contributes empty signal / cover lists: execute1
+    retries or panics on the error and never returns that info to the triage
+    loop (syz-fuzzer/fuzzer.go:752-768)."""
     errs, faults, status, sigs, covs = [], [], [], [], []
     for p in range(len(out_off) - 1):
         r0, r1 = int(call_off[p]), int(call_off[p + 1])
@@ -100,6 +104,6 @@ def parse_batch(out, out_off, call_off, call_nums=None):
         for i in info:
             errs.append(i["errno"])
             faults.append(i["fault"])
-            sigs.append(i["signal"] or [])
-            covs.append(i["cover"] or [])
+            sigs.append((i["signal"] or []) if st == OK else [])
+            covs.append((i["cover"] or []) if st == OK else [])
     return errs, faults, status, sigs, covs

@@ -46,6 +46,7 @@ def _load():
         "orc_signal_diff": (c_size_t, [c_void_p, P32, c_size_t, P32]),
         "orc_signal_add": (None, [c_void_p, P32, c_size_t]),
         "orc_triage_batch": (c_uint64, [c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64]),
+        "orc_triage_procs": (c_int, [c_void_p, c_void_p, P32, P64, P64, c_size_t, c_int, P8]),
         "orc_add_inputs": (None, [c_void_p, c_void_p, P32, P64, c_size_t]),
         "orc_accept_batch": (None, [c_void_p, c_void_p, P32, P64, P32, P64, c_size_t, P8]),
         "orc_merge_poll": (c_uint64, [c_void_p, P32, P64, c_size_t, P32, P64]),
@@ -161,6 +162,16 @@ def triage_flags_only(maxset, newset, vals, off):
     rec_new = np.zeros(nrec, dtype=np.uint8)
     L.orc_triage_batch(maxset.h, newset.h if newset is not None else None, p32(vals), p64(off), nrec, p8(rec_new), None, None)
     return rec_new
+
+
+def triage_procs(maxset, newset, vals, off, prog_rec, nthreads):
+    """The fuzzer's concurrent procs (timing only: racy by design, like the
+    reference).  Returns (rec_new, threads used)."""
+    vals, off, pr = _u32(vals), _u64(off), _u64(prog_rec)
+    rec_new = np.zeros(off.size - 1, dtype=np.uint8)
+    t = L.orc_triage_procs(maxset.h, newset.h if newset is not None else None, p32(vals), p64(off), p64(pr),
+                           pr.size - 1, int(nthreads), p8(rec_new))
+    return rec_new, t
 
 
 def add_inputs(corpus, maxset, vals, off):

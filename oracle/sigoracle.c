@@ -16,6 +16,7 @@
  * so that the CPU baseline pays the same kind of per-element probe cost as the
  * reference does.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -303,6 +304,96 @@ uint64_t orc_triage_batch(orc_set* maxset, orc_set* newset, const uint32_t* vals
 		diff_off[nrec] = nd;
 	free(tmp);
 	return nd;
+}
+
+/* ------------------------------------------------------------------------- */
+/* The fuzzer's concurrent form, for the CPU baseline's all-cores leg only:   */
+/* nthreads "procs" (syz-fuzzer/fuzzer.go:248-327) each take whole programs   */
+/* from a shared counter and run execute()'s loop (fuzzer.go:661-691) over    */
+/* their calls, sharing maxSignal / newSignal under one reader-writer lock    */
+/* (signalMu, fuzzer.go:65): RLock for SignalNew / SignalDiff, the RUnlock -> */
+/* Lock upgrade for the two SignalAdd (fuzzer.go:671-676).  As in the         */
+/* reference, the outcome depends on the interleaving (two procs can triage   */
+/* the same signal in the upgrade window); it is timed, never compared.       */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+	orc_set *maxset, *newset;
+	const uint32_t* vals;
+	const uint64_t* rec_off;
+	const uint64_t* prog_rec; /* program p owns records prog_rec[p] .. prog_rec[p+1] */
+	size_t nprog;
+	uint8_t* rec_new;
+	pthread_rwlock_t mu;
+	size_t next; /* next program, taken under __atomic */
+} orc_procs;
+
+static void* orc_proc_main(void* arg)
+{
+	orc_procs* a = (orc_procs*)arg;
+	uint32_t* diff = NULL;
+	size_t cap = 0;
+	for (;;) {
+		size_t p = __atomic_fetch_add(&a->next, 1, __ATOMIC_RELAXED);
+		if (p >= a->nprog)
+			break;
+		pthread_rwlock_rdlock(&a->mu); /* fuzzer.go:662 */
+		for (uint64_t r = a->prog_rec[p]; r < a->prog_rec[p + 1]; r++) {
+			const uint32_t* sig = a->vals + a->rec_off[r];
+			size_t n = (size_t)(a->rec_off[r + 1] - a->rec_off[r]);
+			a->rec_new[r] = 0;
+			if (!orc_signal_new(a->maxset, sig, n)) /* fuzzer.go:666 */
+				continue;
+			if (cap < n) {
+				free(diff);
+				cap = n;
+				diff = (uint32_t*)malloc(cap * sizeof(uint32_t));
+			}
+			size_t m = orc_signal_diff(a->maxset, sig, n, diff); /* fuzzer.go:669 */
+			pthread_rwlock_unlock(&a->mu);                       /* fuzzer.go:671-672 */
+			pthread_rwlock_wrlock(&a->mu);
+			orc_signal_add(a->maxset, diff, m); /* fuzzer.go:673-674 */
+			if (a->newset)
+				orc_signal_add(a->newset, diff, m);
+			pthread_rwlock_unlock(&a->mu); /* fuzzer.go:675-676 */
+			pthread_rwlock_rdlock(&a->mu);
+			a->rec_new[r] = 1;
+		}
+		pthread_rwlock_unlock(&a->mu);
+	}
+	free(diff);
+	return NULL;
+}
+
+/* Returns the number of threads that ran. */
+int orc_triage_procs(orc_set* maxset, orc_set* newset, const uint32_t* vals, const uint64_t* rec_off,
+		     const uint64_t* prog_rec, size_t nprog, int nthreads, uint8_t* rec_new)
+{
+	orc_procs a;
+	memset(&a, 0, sizeof(a));
+	a.maxset = maxset;
+	a.newset = newset;
+	a.vals = vals;
+	a.rec_off = rec_off;
+	a.prog_rec = prog_rec;
+	a.nprog = nprog;
+	a.rec_new = rec_new;
+	pthread_rwlock_init(&a.mu, NULL);
+	if (nthreads < 1)
+		nthreads = 1;
+	pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+	int started = 0;
+	for (int i = 0; i < nthreads; i++)
+		if (pthread_create(&th[i], NULL, orc_proc_main, &a) == 0)
+			started++;
+		else
+			break;
+	if (started == 0)
+		orc_proc_main(&a);
+	for (int i = 0; i < started; i++)
+		pthread_join(th[i], NULL);
+	free(th);
+	pthread_rwlock_destroy(&a.mu);
+	return started ? started : 1;
 }
 
 /* syz-fuzzer/fuzzer.go:467-489  addInput(): per input, in order. */

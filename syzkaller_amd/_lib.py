@@ -40,6 +40,7 @@ SIGNATURES = {
     "sg_ctx_stream": (c_void_p, [c_void_p]),
     "sg_ctx_timing": (c_int, [c_void_p, c_int]),
     "sg_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), P64]),
+    "sg_ctx_counter": (c_int, [c_void_p, c_char_p, P64]),
     "sg_set_create": (c_int, [c_void_p, POINTER(c_void_p)]),
     "sg_set_destroy": (None, [c_void_p]),
     "sg_set_clear": (c_int, [c_void_p]),
@@ -56,6 +57,12 @@ SIGNATURES = {
     "sg_triage_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64, P64]),
     "sg_triage_batch_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
                                     c_void_p, c_void_p, c_void_p]),
+    "sg_shard_of": (c_int, [c_uint32, c_uint32]),
+    "sg_shard_candidates_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
+                                        c_uint32, c_void_p, c_void_p]),
+    "sg_shard_owners_dev": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "sg_shard_flags_dev": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_uint64, c_uint64, c_void_p]),
+    "sg_set_add_dev": (c_int, [c_void_p, c_void_p, c_uint64]),
     "sg_add_inputs": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t]),
     "sg_accept_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, P32, P64, c_size_t, P8]),
     "sg_merge_poll": (c_int, [c_void_p, c_void_p, P32, P64, c_size_t, P32, P64]),
@@ -72,6 +79,8 @@ SIGNATURES = {
                                    c_void_p]),
     "sg_gen_zipf_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_double, c_uint32, c_uint64, c_uint64, c_uint32,
                                        c_uint32, c_void_p]),
+    "sg_gen_population_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_double, c_double,
+                                             c_uint32, c_uint64, c_uint64, c_uint32, c_uint32, c_void_p]),
     "sg_cover_uncovered": (c_int, [c_void_p, P32, c_size_t, c_uint32, P64, P64, c_size_t, P64, c_size_t, P64, PSZ]),
     "sg_ipc_parse": (c_int, [c_void_p, P32, P64, P64, P32, c_size_t, POINTER(c_int64), P8, POINTER(c_int32), P64, P32,
                              P64, P32]),

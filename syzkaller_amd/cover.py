@@ -75,6 +75,12 @@ class Context:
     def timing(self, enable):
         call("sg_ctx_timing", self.h, 1 if enable else 0)
 
+    def counter(self, name):
+        """sg_ctx_counter: "owner_resets", "owner_floor", "owner_key_space", "max_launch_records"."""
+        v = c_uint64()
+        call("sg_ctx_counter", self.h, name.encode(), byref(v))
+        return v.value
+
     def kernel_time(self, name):
         ms = c_double()
         n = c_uint64()

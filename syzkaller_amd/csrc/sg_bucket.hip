@@ -620,7 +620,63 @@ struct BucketArgs {
   const uint4* blist_q;    // ... and their descriptors
   const uint32_t* nlist;   // device: their number
   uint64_t* dbg;           // diagnostics (k_bucket<true>): per block {start, end, buckets, rounds, 4 phase cycle sums}
+  // candidate emission (sharded triage, sg_shard.hip): instead of flagging
+  // records and setting bits, every distinct candidate s of the batch is
+  // written once, with its first record, as {s, rec_base + record}
+  uint2* pairs;
+  unsigned long long* npairs;
+  uint32_t rec_base;
+  uint32_t nshards;         // pairs are counted per owning shard (shard_of)
+  unsigned long long* shard_cnt;
 };
+
+// Owning shard of a signal in the hash-sharded multi-GPU triage: the murmur3
+// finaliser of s, scaled to [0, nshards).
+__device__ __forceinline__ uint32_t shard_of(uint32_t s, uint32_t nshards) {
+  s ^= s >> 16;
+  s *= 0x85EBCA6Bu;
+  s ^= s >> 13;
+  s *= 0xC2B2AE35u;
+  s ^= s >> 16;
+  return (uint32_t)(((uint64_t)s * nshards) >> 32);
+}
+
+constexpr uint32_t kMaxShards = 64;
+
+// Wave-aggregated append of up to kPer pairs per lane (valid where rec !=
+// kEmpty); each pair is also counted in the block's LDS shard counters.
+template <int kPer>
+__device__ __forceinline__ void emit_pairs(const BucketArgs& a, const uint32_t (&sig)[kPer], const uint32_t (&rec)[kPer],
+                                           uint32_t* shcnt) {
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const int lane = threadIdx.x & 63;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) c += rec[k] != kNone ? 1u : 0u;
+  uint32_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  const uint32_t tot = __shfl(incl, 63);
+  if (tot == 0) return;
+  unsigned long long base = 0;
+  if (lane == 63) base = atomicAdd(a.npairs, (unsigned long long)tot);
+  base = __shfl(base, 63);
+  uint64_t pos = base + incl - c;
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (rec[k] != kNone) {
+      a.pairs[pos++] = make_uint2(sig[k], a.rec_base + rec[k]);
+      atomicAdd(&shcnt[shard_of(sig[k], a.nshards)], 1u);
+    }
+}
+
+__device__ __forceinline__ void flush_shard_counts(const BucketArgs& a, const uint32_t* shcnt) {
+  for (uint32_t i = threadIdx.x; i < a.nshards; i += blockDim.x)
+    if (shcnt[i]) atomicAdd(&a.shard_cnt[i], (unsigned long long)shcnt[i]);
+}
 
 // non-empty flag per bucket (scanned into list positions)
 __global__ void k_bucket_nz(const uint4* __restrict__ bdesc, uint32_t* __restrict__ nz) {
@@ -782,7 +838,7 @@ __device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* 
   return false;  // map (nearly) full: the bucket spills
 }
 
-template <bool kDbg>
+template <bool kDbg, bool kEmit>
 __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
@@ -791,7 +847,10 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
   __shared__ uint32_t sh_fail;         // some insert found the map full: the bucket spills
   __shared__ uint32_t sh_b[2];
   __shared__ uint4 sh_q[2];
+  __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];  // emitted pairs per owning shard
   const int tid = threadIdx.x;
+  if (kEmit)
+    for (uint32_t i = tid; i < kMaxShards; i += kBThreads) shcnt[i] = 0;
   const uint32_t NG = a.NG;
   constexpr uint32_t kRound = kBThreads * kBU;
   // diagnostics (kDbg): block span, buckets, rounds, cycles per phase as wave 0 sees them
@@ -935,6 +994,19 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       }
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
+    } else if (kEmit) {
+      // every distinct candidate of the bucket with its first record
+      uint32_t sig[kHash / kBThreads], rec[kHash / kBThreads];
+#pragma unroll
+      for (int k = 0; k < (int)(kHash / kBThreads); k++) {
+        const uint32_t i = k * kBThreads + tid;
+        const unsigned long long v = ht[i];
+        sig[k] = (b << 16) | (uint32_t)(v >> 32);
+        rec[k] = v != kEmpty64 ? (uint32_t)v : kEmpty;
+        ht[i] = kEmpty64;
+      }
+      emit_pairs(a, sig, rec, shcnt);
+      reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
     } else {
       // a record is queued iff it owns some signal (fuzzer.go:678-690).  A
       // record owns signals in many buckets: its flag is read first and
@@ -985,6 +1057,10 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
 #pragma unroll
     for (int u = 0; u < kBU; u++) x[u] = y[u];
   }
+  if (kEmit) {
+    __syncthreads();
+    flush_shard_counts(a, shcnt);
+  }
   if (kDbg && tid == 0) {
     a.dbg[8 * blockIdx.x] = t_start;
     a.dbg[8 * blockIdx.x + 1] = wall_clock64();
@@ -998,14 +1074,20 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
 
 // Buckets with too many distinct candidates: a direct first-owner table over
 // a quarter of the bucket at a time (16384 signals, 64 KiB of LDS).
+template <bool kEmit>
 __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
   constexpr uint32_t kQ = 16384;
   __shared__ uint32_t owner[kQ];
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
   __shared__ uint32_t gb[kMaxGroups];
+  __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];
   const int tid = threadIdx.x;
   const uint32_t nsp = *a.nspill, NG = a.NG;
+  if (kEmit) {
+    for (uint32_t i = tid; i < kMaxShards; i += kBThreads) shcnt[i] = 0;
+    __syncthreads();
+  }
   for (uint32_t j = blockIdx.x; j < nsp; j += gridDim.x) {
     const uint32_t b = a.spill[j];
     const uint4 q = a.bdesc[b];
@@ -1026,13 +1108,26 @@ __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
         atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
       }
       __syncthreads();
-      for (uint32_t i = tid; i < kQ; i += kBThreads)
-        if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
+      if (kEmit) {
+        constexpr int kPer = kQ / kBThreads;
+        uint32_t sig[kPer], rec[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+          const uint32_t i = k * kBThreads + tid;
+          sig[k] = (b << 16) | (qq * kQ + i);
+          rec[k] = owner[i];
+        }
+        emit_pairs(a, sig, rec, shcnt);
+      } else {
+        for (uint32_t i = tid; i < kQ; i += kBThreads)
+          if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
+      }
       __syncthreads();
     }
-    flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
+    if (!kEmit) flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
     __syncthreads();
   }
+  if (kEmit) flush_shard_counts(a, shcnt);
 }
 
 // ------------------------------------------------------------------ scan ---
@@ -1217,24 +1312,16 @@ struct BucketPlan {
     oLQ = p.add((uint64_t)kNumBuckets * 16);
     oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
   }
+  void rebase(size_t b) {
+    for (size_t* o : {&oTS, &oTR, &oGT, &oH1, &oO1, &oV1, &oNC, &oCB, &oCS, &oCG, &oCF, &oCD, &oDT, &oBD, &oGB, &oH2,
+                      &oO2, &oV2, &oSP, &oTK, &oBN, &oBP, &oLB, &oLQ, &oSC})
+      *o += b;
+  }
 };
 
-// records per launch of the partitioned path (kMaxGroups groups); larger
-// batches run as consecutive record slices.  SG_TRIAGE_MAX_RECS lowers it
-// (tests of the slicing).
-static uint64_t max_launch_records() {
-  uint64_t m = (uint64_t)kMaxGroups * kGroupRecs;
-  if (const char* e = getenv("SG_TRIAGE_MAX_RECS")) {
-    const unsigned long long v = strtoull(e, nullptr, 10);
-    if (v > 0 && v < m) m = v;
-  }
-  return m;
-}
+size_t bucket_plan_bytes(uint64_t n, uint64_t nrec) { return BucketPlan(n, nrec).p.total; }
 
-size_t bucket_ws_bytes(uint64_t n, uint64_t nrec) {
-  const uint64_t m = max_launch_records();
-  return BucketPlan(n, nrec < m ? nrec : m).p.total;
-}
+static_assert(kMaxLaunchRecords == (uint64_t)kMaxGroups * kGroupRecs, "records per partitioned launch");
 
 // Grid of a persistent kernel: every block resident at once (CUs x blocks
 // per CU from the occupancy query), cached per kernel.
@@ -1256,20 +1343,32 @@ static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
 }
 
 // One launch sequence over a batch of <= kMaxGroups groups (rec_new zeroed).
+// With `emit`, the bucket stage writes the distinct candidates instead of
+// flagging records and updating the sets (mwords is then only read).  The
+// launch's scratch starts at workspace offset ws_base (reserved by the caller
+// when ws_base != 0).
 static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
-                             const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
+                             const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new,
+                             const EmitArgs* emit = nullptr, size_t ws_base = 0) {
   if (n == 0) return SG_OK;
   if (nrec == 0) {
     set_error("bucket triage: signal entries without records");
     return SG_EINVAL;
   }
-  const BucketPlan bp(n, nrec);
+  BucketPlan bp(n, nrec);
   if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
     set_error("bucket triage: batch too large");
     return SG_EINVAL;
   }
-  int rc = ws_reserve(ctx, bp.p.total);
+  int rc = ws_base ? SG_OK : ws_reserve(ctx, bp.p.total);
   if (rc) return rc;
+  if (ws_base) {
+    if (ctx->ws_cap < ws_base + bp.p.total) {
+      set_error("bucket triage: workspace not reserved");
+      return SG_EINVAL;
+    }
+    bp.rebase(ws_base);
+  }
   uint32_t* tstart = (uint32_t*)ws_at(ctx, bp.oTS);
   uint32_t* trec = (uint32_t*)ws_at(ctx, bp.oTR);
   uint32_t* gt = (uint32_t*)ws_at(ctx, bp.oGT);
@@ -1318,7 +1417,7 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
   P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, nullptr};
-  const bool dbg = getenv("SG_DEBUG_PART") != nullptr;
+  const bool dbg = ctx->debug_part;
   unsigned long long* p1dbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&p1dbg, 64));
@@ -1374,7 +1473,14 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   ba.nspill = nspill;
   ba.spill = nspill + 1;
   ba.ticket = (uint32_t*)ws_at(ctx, bp.oTK);
-  const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false>, kBThreads);
+  if (emit) {
+    ba.pairs = emit->pairs;
+    ba.npairs = emit->npairs;
+    ba.rec_base = emit->rec_base;
+    ba.nshards = emit->nshards;
+    ba.shard_cnt = emit->shard_cnt;
+  }
+  const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, false>, kBThreads);
   uint64_t* ddbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&ddbg, (size_t)bgrid * 88));
@@ -1398,17 +1504,22 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   ba.nlist = blpos + kNumBuckets;
   {
     ScopedTimer tm(ctx, "bucket_triage");
-    if (dbg)
-      hipLaunchKernelGGL(k_bucket<true>, dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+    if (emit)
+      hipLaunchKernelGGL((k_bucket<false, true>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+    else if (dbg)
+      hipLaunchKernelGGL((k_bucket<true, false>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
     else
-      hipLaunchKernelGGL(k_bucket<false>, dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+      hipLaunchKernelGGL((k_bucket<false, false>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
   }
   {
     ScopedTimer tm(ctx, "bucket_spill");
-    hipLaunchKernelGGL(k_bucket_direct, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
+    if (emit)
+      hipLaunchKernelGGL(k_bucket_direct<true>, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
+    else
+      hipLaunchKernelGGL(k_bucket_direct<false>, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
   }
   SG_HIP(hipGetLastError());
-  if (getenv("SG_DEBUG_PART")) {  // diagnostics: chunk and spill counts (syncs)
+  if (dbg) {  // diagnostics: chunk and spill counts (syncs)
     uint32_t g = 0, sp = 0;
     SG_HIP(hipMemcpyAsync(&g, gcount, 4, hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipMemcpyAsync(&sp, nspill, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -1467,9 +1578,10 @@ __global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t 
 }
 
 // Flags-only triage of a device-resident batch (ctx lock held).  Batches of
-// more than max_launch_records() records run as consecutive record slices:
+// more than ctx->max_launch_recs records run as consecutive record slices:
 // the sequential loop (fuzzer.go:665) cut between two records sees the same
-// maxSignal at every record.
+// maxSignal at every record.  The rebased offsets of a slice live in a
+// grow-only context buffer.
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
                   uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
   if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
@@ -1477,12 +1589,18 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     return SG_EINVAL;
   }
   if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
-  const uint64_t m = max_launch_records();
+  const uint64_t m = ctx->max_launch_recs;
   if (nrec <= m) return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new);
-  uint64_t* roff = nullptr;
-  SG_HIP(hipMalloc(&roff, (m + 1) * 8));
-  int rc = SG_OK;
-  for (uint64_t r0 = 0; r0 < nrec && rc == SG_OK; r0 += m) {
+  if (ctx->slice_off_cap < m + 1) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
+    ctx->slice_off = nullptr;
+    ctx->slice_off_cap = 0;
+    SG_HIP(hipMalloc(&ctx->slice_off, (m + 1) * 8));
+    ctx->slice_off_cap = m + 1;
+  }
+  uint64_t* roff = ctx->slice_off;
+  for (uint64_t r0 = 0; r0 < nrec; r0 += m) {
     const uint64_t r1 = nrec - r0 < m ? nrec : r0 + m;
     uint64_t e[2] = {0, 0};
     SG_HIP(hipMemcpyAsync(&e[0], d_off + r0, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1490,11 +1608,20 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     SG_HIP(hipStreamSynchronize(ctx->stream));
     hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1,
                        e[0], roff);
-    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e[0], roff, e[1] - e[0], r1 - r0, d_rec_new + r0);
+    const int rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e[0], roff, e[1] - e[0], r1 - r0, d_rec_new + r0);
+    if (rc) return rc;
   }
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  SG_HIP(hipFree(roff));
-  return rc;
+  return SG_OK;
+}
+
+int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,
+                uint64_t nrec, const EmitArgs& emit, size_t ws_base) {
+  if (nrec > kMaxLaunchRecords || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("bucket emit: a launch holds <= 2^24 records and < 2^32 - 2^15 entries");
+    return SG_EINVAL;
+  }
+  return bucket_triage_one(ctx, const_cast<uint32_t*>(mwords), nullptr, d_vals, d_off, n, nrec, nullptr, &emit,
+                           ws_base);
 }
 
 }  // namespace sg

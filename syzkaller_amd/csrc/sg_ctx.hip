@@ -81,19 +81,21 @@ int dstage_reserve(sg_ctx* ctx, size_t bytes) {
 }
 
 int owner_keys(sg_ctx* ctx, uint64_t nkeys, uint32_t* key_lo) {
-  if (nkeys >= kOwnerInf) {
-    set_error("batch of %llu keys exceeds the 32-bit first-owner key space", (unsigned long long)nkeys);
+  if (nkeys > ctx->owner_key_space) {
+    set_error("batch of %llu keys exceeds the first-owner key space (%llu)", (unsigned long long)nkeys,
+              (unsigned long long)ctx->owner_key_space);
     return SG_EINVAL;
   }
   if (!ctx->owner) {
     SG_HIP(hipMalloc(&ctx->owner, kOwnerEntries * sizeof(uint32_t)));
     SG_HIP(hipMemsetAsync(ctx->owner, 0xFF, kOwnerEntries * sizeof(uint32_t), ctx->stream));
-    ctx->owner_floor = kOwnerInf;
+    ctx->owner_floor = ctx->owner_key_space;
   }
   if (ctx->owner_floor < nkeys) {
     // Key space exhausted (after ~4G keys): start a fresh generation.
     SG_HIP(hipMemsetAsync(ctx->owner, 0xFF, kOwnerEntries * sizeof(uint32_t), ctx->stream));
-    ctx->owner_floor = kOwnerInf;
+    ctx->owner_floor = ctx->owner_key_space;
+    ctx->owner_resets++;
   }
   ctx->owner_floor -= nkeys;
   *key_lo = (uint32_t)ctx->owner_floor;
@@ -403,6 +405,17 @@ int sg_ctx_create(int device, sg_ctx** out) {
   }
   sg_ctx* c = new sg_ctx();
   c->device = device;
+  // environment switches, read once here (not on the hot path)
+  c->max_launch_recs = kMaxLaunchRecords;
+  if (const char* e = getenv("SG_TRIAGE_MAX_RECS")) {
+    const unsigned long long v = strtoull(e, nullptr, 10);
+    if (v > 0 && v < c->max_launch_recs) c->max_launch_recs = v;
+  }
+  if (const char* e = getenv("SG_OWNER_KEY_SPACE")) {
+    const unsigned long long v = strtoull(e, nullptr, 10);
+    if (v > 0 && v < c->owner_key_space) c->owner_key_space = v;
+  }
+  c->debug_part = getenv("SG_DEBUG_PART") != nullptr;
   int rc = ensure_device(c);
   if (rc) {
     delete c;
@@ -437,6 +450,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);
+  if (ctx->slice_off) hipFree(ctx->slice_off);
   if (ctx->dscal) hipFree(ctx->dscal);
   if (ctx->gen_prob) hipFree(ctx->gen_prob);
   if (ctx->gen_alias) hipFree(ctx->gen_alias);
@@ -484,6 +498,24 @@ int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* laun
   auto it = t.ids.find(name);
   if (ms) *ms = it == t.ids.end() ? 0 : t.ms[it->second];
   if (launches) *launches = it == t.ids.end() ? 0 : t.count[it->second];
+  return SG_OK;
+}
+
+int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
+  if (!ctx || !name || !out) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!strcmp(name, "owner_resets"))
+    *out = ctx->owner_resets;
+  else if (!strcmp(name, "owner_floor"))
+    *out = ctx->owner ? ctx->owner_floor : ctx->owner_key_space;
+  else if (!strcmp(name, "owner_key_space"))
+    *out = ctx->owner_key_space;
+  else if (!strcmp(name, "max_launch_records"))
+    *out = ctx->max_launch_recs;
+  else {
+    set_error("sg_ctx_counter: unknown counter '%s'", name);
+    return SG_EINVAL;
+  }
   return SG_OK;
 }
 

@@ -141,6 +141,31 @@ __global__ void k_gen_traces(uint64_t seed, uint32_t nranks, uint64_t g0, uint64
   }
 }
 
+// Programs drawn from a fixed population, re-executed with flaky coverage:
+// program p of the batch is population member m = pick(trace_seed, p) <
+// npop, whose trace is exactly the one k_gen_traces gives program m under
+// pop_seed; each PC is independently replaced by a fresh Zipf draw with
+// probability noise / 2^32 (interrupts, timing-dependent paths).
+__global__ void k_gen_pop_traces(uint64_t pop_seed, uint64_t trace_seed, uint32_t nranks, uint64_t npop, uint32_t noise,
+                                 uint64_t prog_base, uint64_t nprog, uint64_t per_prog,
+                                 const uint32_t* __restrict__ prob, const uint32_t* __restrict__ alias,
+                                 const uint32_t* __restrict__ perm, uint32_t* __restrict__ out) {
+  const uint64_t n = nprog * per_prog;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t p = prog_base + i / per_prog, j = i % per_prog;
+    const uint64_t m = ((mix64(trace_seed ^ 0xA0761D6478BD642Full) + p) * 0x9E3779B97F4A7C15ull) >> 32;
+    const uint64_t member = (mix64(m) >> 32) * npop >> 32;
+    uint64_t h = mix64(pop_seed + 0x9E3779B97F4A7C15ull * (member * per_prog + j + 1));
+    const uint64_t hn = mix64(trace_seed + 0x9E3779B97F4A7C15ull * (p * per_prog + j + 1));
+    if ((uint32_t)hn < noise) h = mix64(hn ^ 0xD1B54A32D192ED03ull);
+    uint32_t bucket = (uint32_t)(((h >> 32) * (uint64_t)nranks) >> 32);
+    uint32_t frac = (uint32_t)h;
+    uint32_t rank = frac < prob[bucket] ? bucket : alias[bucket];
+    out[i] = 0x81000000u + 16u * perm[rank];
+  }
+}
+
 // Vose alias tables for Zipf(s) over ranks 1..N (rank r has weight r^-s) and a
 // seeded Fisher-Yates permutation rank -> pc slot.  Host-side, deterministic.
 static void build_zipf_tables(uint64_t seed, double s, uint32_t N, std::vector<uint32_t>& prob,
@@ -263,37 +288,72 @@ int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, c
   return SG_OK;
 }
 
+}  // extern "C"
+
+namespace sg {
+// Alias tables and permutation of the Zipf generator, cached per context.
+static int gen_tables(sg_ctx* ctx, uint64_t seed, double zipf_s, uint32_t nranks) {
+  if (ctx->gen_prob && ctx->gen_seed == seed && ctx->gen_s == zipf_s && ctx->gen_nranks == nranks) return SG_OK;
+  std::vector<uint32_t> prob, alias, perm;
+  build_zipf_tables(seed, zipf_s, nranks, prob, alias, perm);
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->gen_prob) {
+    hipFree(ctx->gen_prob);
+    hipFree(ctx->gen_alias);
+    hipFree(ctx->gen_perm);
+    ctx->gen_prob = ctx->gen_alias = ctx->gen_perm = nullptr;
+  }
+  SG_HIP(hipMalloc(&ctx->gen_prob, nranks * 4));
+  SG_HIP(hipMalloc(&ctx->gen_alias, nranks * 4));
+  SG_HIP(hipMalloc(&ctx->gen_perm, nranks * 4));
+  SG_HIP(hipMemcpy(ctx->gen_prob, prob.data(), nranks * 4, hipMemcpyHostToDevice));
+  SG_HIP(hipMemcpy(ctx->gen_alias, alias.data(), nranks * 4, hipMemcpyHostToDevice));
+  SG_HIP(hipMemcpy(ctx->gen_perm, perm.data(), nranks * 4, hipMemcpyHostToDevice));
+  ctx->gen_seed = seed;
+  ctx->gen_s = zipf_s;
+  ctx->gen_nranks = nranks;
+  return SG_OK;
+}
+}  // namespace sg
+
+extern "C" {
+
 int sg_gen_zipf_traces_dev(sg_ctx* ctx, uint64_t seed, uint64_t trace_seed, double zipf_s, uint32_t nranks,
                            uint64_t prog_base, uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs) {
   if (!ctx || !d_pcs || nranks == 0 || nranks > (1u << 24) || !(zipf_s > 0)) return SG_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
-  if (!ctx->gen_prob || ctx->gen_seed != seed || ctx->gen_s != zipf_s || ctx->gen_nranks != nranks) {
-    std::vector<uint32_t> prob, alias, perm;
-    build_zipf_tables(seed, zipf_s, nranks, prob, alias, perm);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    if (ctx->gen_prob) {
-      hipFree(ctx->gen_prob);
-      hipFree(ctx->gen_alias);
-      hipFree(ctx->gen_perm);
-      ctx->gen_prob = ctx->gen_alias = ctx->gen_perm = nullptr;
-    }
-    SG_HIP(hipMalloc(&ctx->gen_prob, nranks * 4));
-    SG_HIP(hipMalloc(&ctx->gen_alias, nranks * 4));
-    SG_HIP(hipMalloc(&ctx->gen_perm, nranks * 4));
-    SG_HIP(hipMemcpy(ctx->gen_prob, prob.data(), nranks * 4, hipMemcpyHostToDevice));
-    SG_HIP(hipMemcpy(ctx->gen_alias, alias.data(), nranks * 4, hipMemcpyHostToDevice));
-    SG_HIP(hipMemcpy(ctx->gen_perm, perm.data(), nranks * 4, hipMemcpyHostToDevice));
-    ctx->gen_seed = seed;
-    ctx->gen_s = zipf_s;
-    ctx->gen_nranks = nranks;
-  }
+  rc = gen_tables(ctx, seed, zipf_s, nranks);
+  if (rc) return rc;
   uint64_t per_prog = (uint64_t)calls * pcs_per_call;
   uint64_t n = nprog * per_prog;
   if (n == 0) return SG_OK;
   hipLaunchKernelGGL(k_gen_traces, dim3(std::min<uint64_t>(div_up(n, 256), 65536)), dim3(256), 0, ctx->stream, trace_seed,
                      nranks, prog_base * per_prog, n, ctx->gen_prob, ctx->gen_alias, ctx->gen_perm, d_pcs);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_gen_population_traces_dev(sg_ctx* ctx, uint64_t universe_seed, uint64_t pop_seed, uint64_t npop,
+                                 uint64_t trace_seed, double noise, double zipf_s, uint32_t nranks, uint64_t prog_base,
+                                 uint64_t nprog, uint32_t calls, uint32_t pcs_per_call, uint32_t* d_pcs) {
+  if (!ctx || !d_pcs || nranks == 0 || nranks > (1u << 24) || !(zipf_s > 0) || npop == 0 || npop > (1ull << 32) ||
+      !(noise >= 0 && noise <= 1))
+    return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  rc = gen_tables(ctx, universe_seed, zipf_s, nranks);
+  if (rc) return rc;
+  const uint64_t per_prog = (uint64_t)calls * pcs_per_call;
+  const uint64_t n = nprog * per_prog;
+  if (n == 0) return SG_OK;
+  const double q = noise * 4294967296.0;
+  const uint32_t thr = q >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)q;
+  hipLaunchKernelGGL(k_gen_pop_traces, dim3(std::min<uint64_t>(div_up(n, 256), 65536)), dim3(256), 0, ctx->stream,
+                     pop_seed, trace_seed, nranks, npop, thr, prog_base, nprog, per_prog, ctx->gen_prob,
+                     ctx->gen_alias, ctx->gen_perm, d_pcs);
   SG_HIP(hipGetLastError());
   return SG_OK;
 }

@@ -21,6 +21,9 @@ constexpr uint64_t kSetBytes = kSetWords * 4;
 // First-owner table: one u32 key per possible signal value = 16 GiB.
 constexpr uint64_t kOwnerEntries = 1ull << 32;
 constexpr uint32_t kOwnerInf = 0xFFFFFFFFu;
+// Records per launch of the partitioned triage (256 groups of 2^16 records);
+// larger batches run as consecutive record slices (sg_bucket.hip).
+constexpr uint64_t kMaxLaunchRecords = 1ull << 24;
 
 // Element tiles of the streaming kernels: 256 threads, one uint4 (4 values)
 // per lane per step, 4 steps per wave -> 4096 values per workgroup tile;
@@ -62,9 +65,20 @@ struct sg_ctx {
   // grow-only device staging for the host entry points' inputs / outputs
   void* dstage = nullptr;
   size_t dstage_cap = 0;
-  // first-owner table and its decreasing key floor
+  // first-owner table and its decreasing key floor; the key space is 2^32 - 1
+  // (SG_OWNER_KEY_SPACE lowers it, so tests reach the generation reset)
   uint32_t* owner = nullptr;
   uint64_t owner_floor = 0;
+  uint64_t owner_key_space = 0xFFFFFFFFull;
+  uint64_t owner_resets = 0;
+  // partitioned triage: records per launch (SG_TRIAGE_MAX_RECS lowers it, for
+  // tests of the record slicing) and diagnostics (SG_DEBUG_PART); the
+  // environment is read once, at context creation
+  uint64_t max_launch_recs = 0;
+  bool debug_part = false;
+  // rebased record offsets of one record slice (grow-only, owned)
+  uint64_t* slice_off = nullptr;
+  size_t slice_off_cap = 0;
   // small device scalars (counters / flags)
   uint64_t* dscal = nullptr;
   // cached Zipf generator tables (alias method + rank->pc permutation)
@@ -147,6 +161,22 @@ int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint6
 // Partitioned flags-only triage (sg_bucket.hip); ctx lock held.
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
                   uint64_t n, uint64_t nrec, uint8_t* d_rec_new);
+// Candidate emission of the partitioned path (sharded triage, sg_shard.hip):
+// each distinct s not in the snapshot, once per launch, as {s, rec_base +
+// first record}, counted per owning shard.
+struct EmitArgs {
+  uint2* pairs;
+  unsigned long long* npairs;
+  uint32_t rec_base;
+  uint32_t nshards;
+  unsigned long long* shard_cnt;
+};
+// Workspace bytes of one partitioned launch over n entries / nrec records.
+size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
+// One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch
+// at ws_base (reserved by the caller).
+int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,
+                uint64_t nrec, const EmitArgs& emit, size_t ws_base);
 
 }  // namespace sg
 

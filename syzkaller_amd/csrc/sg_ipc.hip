@@ -133,6 +133,16 @@ __global__ void k_ipc_walk(IpcArgs a) {
     }
   }
   a.status[p] = st;
+  // A program whose output failed to parse contributes no signal or cover:
+  // execute1 retries it or panics, and never hands its info to the triage
+  // loop (syz-fuzzer/fuzzer.go:752-768).  Its records keep their errno /
+  // fault (the reader's partial state) but get empty CSR slices, so the CSR
+  // is sg_triage_batch's input as is.
+  if (st != kIpcOk)
+    for (uint64_t r = r0; r < r1; r++) {
+      a.sig_cnt[r] = 0;
+      a.cov_cnt[r] = 0;
+    }
 }
 
 // a wave per record: its words from the output region into the CSR

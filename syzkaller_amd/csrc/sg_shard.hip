@@ -1,0 +1,327 @@
+// sg_shard.hip -- one batch's new-signal triage hash-sharded by signal across
+// GPUs (the host protocol is syzkaller_amd/shard.py).
+//
+// Reference: syz-fuzzer/fuzzer.go:645-693, one sequential loop over every
+// call record of the batch.  By the first-owner rule (sg_triage.hip), record
+// r is queued iff some s not in maxSignal has owner(s) = min{r : s in S_r} =
+// r, and maxSignal' = maxSignal ∪ ⋃ S_r.  owner(s) depends only on the
+// records holding s, so the signal space shards cleanly:
+//
+//   candidates  (every rank, its contiguous slice of the batch's records)
+//               the partitioned path (sg_bucket.hip) in emission mode: each
+//               distinct s not in the replicated maxSignal snapshot, once,
+//               with its first record of the slice (global index), grouped
+//               by owning shard shard_of(s) -- only candidates travel;
+//   [RCCL all-to-all of the pairs to their owning shard]
+//   owners      (every rank, the pairs of its shard from all ranks) owner(s)
+//               = min record over them (atomicMin into the first-owner
+//               table), then the owners' bits in a batch-wide record bitset
+//               and each new signal once;
+//   [RCCL all-to-all of the bitset slices back to the records' ranks,
+//    all-gather of the new signals]
+//   flags       (every rank) its records' flags = OR of the received slices;
+//               maxSignal / newSignal ∪= the new signals of every shard.
+#include "sg_internal.h"
+
+namespace sg {
+
+constexpr uint32_t kShardMax = 64;  // == kMaxShards of sg_bucket.hip
+constexpr uint64_t kLaunchEntries = 1ull << 31;  // entries per emitting launch (< the partition's 2^32 cap)
+
+__device__ __forceinline__ uint32_t shard_hash(uint32_t s, uint32_t nshards) {  // == shard_of (sg_bucket.hip)
+  s ^= s >> 16;
+  s *= 0x85EBCA6Bu;
+  s ^= s >> 13;
+  s *= 0xC2B2AE35u;
+  s ^= s >> 16;
+  return (uint32_t)(((uint64_t)s * nshards) >> 32);
+}
+
+__global__ void k_shard_offsets(const unsigned long long* __restrict__ cnt, uint32_t nshards,
+                                uint64_t* __restrict__ off, unsigned long long* __restrict__ cursor) {
+  if (threadIdx.x != 0) return;
+  uint64_t run = 0;
+  for (uint32_t k = 0; k < nshards; k++) {
+    off[k] = run;
+    cursor[k] = run;
+    run += cnt[k];
+  }
+  off[nshards] = run;
+}
+
+// Pairs grouped by owning shard: per round of 1024 pairs a block ranks them
+// per shard in LDS and reserves each shard's run with one global atomic.
+constexpr int kRouteThreads = 256;
+constexpr int kRoutePer = 4;
+__global__ __launch_bounds__(kRouteThreads) void k_shard_route(const uint2* __restrict__ in,
+                                                               const unsigned long long* __restrict__ npairs,
+                                                               uint32_t nshards,
+                                                               unsigned long long* __restrict__ cursor,
+                                                               uint2* __restrict__ out) {
+  __shared__ uint32_t cnt[kShardMax];
+  __shared__ unsigned long long gb[kShardMax];
+  const uint64_t n = *npairs;
+  const int tid = threadIdx.x;
+  constexpr uint64_t kRound = (uint64_t)kRouteThreads * kRoutePer;
+  for (uint64_t base = (uint64_t)blockIdx.x * kRound; base < n; base += (uint64_t)gridDim.x * kRound) {
+    if (tid < (int)kShardMax) cnt[tid] = 0;
+    __syncthreads();
+    uint2 v[kRoutePer];
+    uint32_t sh[kRoutePer], loc[kRoutePer];
+#pragma unroll
+    for (int k = 0; k < kRoutePer; k++) {
+      const uint64_t i = base + (uint64_t)k * kRouteThreads + tid;
+      sh[k] = kShardMax;
+      if (i < n) {
+        v[k] = in[i];
+        sh[k] = shard_hash(v[k].x, nshards);
+        loc[k] = atomicAdd(&cnt[sh[k]], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < (int)nshards && cnt[tid]) gb[tid] = atomicAdd(&cursor[tid], (unsigned long long)cnt[tid]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRoutePer; k++)
+      if (sh[k] < kShardMax) out[gb[sh[k]] + loc[k]] = v[k];
+    __syncthreads();
+  }
+}
+
+// owner(s) = min record over the received pairs (keys key_lo + record, below
+// every key already in the table: sg::owner_keys)
+__global__ void k_shard_claim(const uint2* __restrict__ pairs, uint64_t n, uint32_t* __restrict__ owner,
+                              uint32_t key_lo) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint2 p = pairs[i];
+    const uint32_t key = key_lo + p.y;
+    uint32_t* o = owner + p.x;
+    if (__hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > key) atomicMin(o, key);
+  }
+}
+
+// the owning pair of each s: its record's bit, and s once in the new list
+__global__ void k_shard_resolve(const uint2* __restrict__ pairs, uint64_t n, const uint32_t* __restrict__ owner,
+                                uint32_t key_lo, uint32_t* __restrict__ rec_bits, uint32_t* __restrict__ new_vals,
+                                unsigned long long* __restrict__ nnew) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // whole waves iterate together (the ballot below)
+  const uint64_t n_up = (n + 63) & ~63ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
+    bool own = false;
+    uint2 p = make_uint2(0, 0);
+    if (i < n) {
+      p = pairs[i];
+      own = owner[p.x] == key_lo + p.y;
+    }
+    if (own) atomicOr(&rec_bits[p.y >> 5], 1u << (p.y & 31));
+    const uint64_t m = __ballot(own);
+    if (!m) continue;
+    unsigned long long base = 0;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    if (lane == leader) base = atomicAdd(nnew, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (own) new_vals[base + __popcll(m & lt)] = p.x;
+  }
+}
+
+// rec_new[i] = bit (rec_lo + i) of the OR of nparts bitsets, each holding
+// the words from rec_lo / 32 on
+__global__ void k_shard_flags(const uint32_t* __restrict__ bits, uint32_t nparts, uint64_t wpp, uint64_t rec_lo,
+                              uint64_t nrec, uint8_t* __restrict__ rec_new) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrec) return;
+  const uint64_t r = rec_lo + i, w = (r >> 5) - (rec_lo >> 5);
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < nparts; k++) v |= bits[(uint64_t)k * wpp + w];
+  rec_new[i] = (v >> (r & 31)) & 1u;
+}
+
+__global__ void k_set_add_vals(uint32_t* __restrict__ words, const uint32_t* __restrict__ v, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sgd::set_bit(words, v[i]);
+}
+
+__global__ void k_rebase_off(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = off[i] - base;
+}
+
+static int read_u64(sg_ctx* ctx, const uint64_t* d, uint64_t* h) {
+  SG_HIP(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_shard_of(uint32_t s, uint32_t nshards) {
+  if (nshards == 0) return -1;
+  s ^= s >> 16;
+  s *= 0x85EBCA6Bu;
+  s ^= s >> 13;
+  s *= 0xC2B2AE35u;
+  s ^= s >> 16;
+  return (int)(((uint64_t)s * nshards) >> 32);
+}
+
+int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_vals, const uint64_t* d_rec_off,
+                            uint64_t nvals, uint64_t nrec, uint64_t rec_base, uint32_t nshards, uint32_t* d_pairs,
+                            uint64_t* d_shard_off) {
+  if (!ctx || !snapshot || snapshot->ctx != ctx || !d_rec_off || !d_shard_off || (nvals && (!d_vals || !d_pairs)) ||
+      nshards == 0 || nshards > kShardMax || rec_base + nrec > 0xFFFFFFFFull) {
+    set_error("sg_shard_candidates_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "shard_local");
+  const uint64_t m = ctx->max_launch_recs;
+  const uint64_t max_n = nvals < kLaunchEntries ? nvals : kLaunchEntries;
+  WsPlan p;
+  const size_t o_tmp = p.add(nvals * 8 + 64), o_cnt = p.add(kShardMax * 8 + 8), o_cur = p.add(kShardMax * 8);
+  const size_t o_plan = p.total;
+  rc = ws_reserve(ctx, o_plan + bucket_plan_bytes(max_n ? max_n : 1, nrec < m ? (nrec ? nrec : 1) : m));
+  if (rc) return rc;
+  uint2* tmp = (uint2*)ws_at(ctx, o_tmp);
+  unsigned long long* cnt = (unsigned long long*)ws_at(ctx, o_cnt);
+  unsigned long long* npairs = cnt + kShardMax;
+  unsigned long long* cursor = (unsigned long long*)ws_at(ctx, o_cur);
+  SG_HIP(hipMemsetAsync(cnt, 0, kShardMax * 8 + 8, ctx->stream));
+  const bool single = nrec <= m && nvals < kLaunchEntries;
+  if (nvals && single) {
+    EmitArgs e{tmp, npairs, (uint32_t)rec_base, nshards, cnt};
+    rc = bucket_emit(ctx, snapshot->words, d_vals, d_rec_off, nvals, nrec, e, o_plan);
+    if (rc) return rc;
+  } else if (nvals) {
+    // record slices of <= m records and < 2^31 entries (the 2^32-entry cap
+    // of one partitioned launch holds per slice)
+    if (ctx->slice_off_cap < m + 1) {
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
+      ctx->slice_off = nullptr;
+      ctx->slice_off_cap = 0;
+      SG_HIP(hipMalloc(&ctx->slice_off, (m + 1) * 8));
+      ctx->slice_off_cap = m + 1;
+    }
+    uint64_t e0 = 0;
+    rc = read_u64(ctx, d_rec_off, &e0);
+    if (rc) return rc;
+    for (uint64_t r0 = 0; r0 < nrec;) {
+      uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
+      rc = read_u64(ctx, d_rec_off + r1, &e1);
+      if (rc) return rc;
+      if (e1 - e0 >= kLaunchEntries) {  // largest r1 with entries < 2^31 (a record holds < 2^31)
+        uint64_t lo = r0 + 1, hi = r1;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) / 2;
+          uint64_t em = 0;
+          rc = read_u64(ctx, d_rec_off + mid, &em);
+          if (rc) return rc;
+          if (em - e0 < kLaunchEntries)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        r1 = lo;
+        rc = read_u64(ctx, d_rec_off + r1, &e1);
+        if (rc) return rc;
+        if (e1 - e0 >= kLaunchEntries) {
+          set_error("sg_shard_candidates_dev: a record holds >= 2^31 signal entries");
+          return SG_EINVAL;
+        }
+      }
+      hipLaunchKernelGGL(k_rebase_off, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_rec_off + r0,
+                         r1 - r0 + 1, e0, ctx->slice_off);
+      EmitArgs e{tmp, npairs, (uint32_t)(rec_base + r0), nshards, cnt};
+      rc = bucket_emit(ctx, snapshot->words, d_vals + e0, ctx->slice_off, e1 - e0, r1 - r0, e, o_plan);
+      if (rc) return rc;
+      // the next slice's offsets overwrite slice_off: wait for this one
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      r0 = r1;
+      e0 = e1;
+    }
+  }
+  hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long*)cnt, nshards,
+                     d_shard_off, cursor);
+  if (nvals) {
+    ScopedTimer tr(ctx, "shard_route");
+    hipLaunchKernelGGL(k_shard_route, dim3(std::min<uint64_t>(div_up(nvals, kRouteThreads * kRoutePer), 8192)),
+                       dim3(kRouteThreads), 0, ctx->stream, (const uint2*)tmp, (const unsigned long long*)npairs,
+                       nshards, cursor, (uint2*)d_pairs);
+  }
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_shard_owners_dev(sg_ctx* ctx, const uint32_t* d_pairs, uint64_t npairs, uint64_t nrec_total,
+                        uint32_t* d_rec_bits, uint32_t* d_new_vals, uint64_t* d_nnew) {
+  if (!ctx || !d_rec_bits || !d_nnew || (npairs && (!d_pairs || !d_new_vals)) || nrec_total > 0xFFFFFFFFull) {
+    set_error("sg_shard_owners_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  SG_HIP(hipMemsetAsync(d_rec_bits, 0, ((nrec_total + 31) / 32) * 4, ctx->stream));
+  SG_HIP(hipMemsetAsync(d_nnew, 0, 8, ctx->stream));
+  if (npairs == 0) return SG_OK;
+  uint32_t key_lo = 0;
+  rc = owner_keys(ctx, nrec_total ? nrec_total : 1, &key_lo);
+  if (rc) return rc;
+  const uint32_t grid = std::min<uint64_t>(div_up(npairs, 256), 16384);
+  {
+    ScopedTimer tm(ctx, "shard_owner");
+    hipLaunchKernelGGL(k_shard_claim, dim3(grid), dim3(256), 0, ctx->stream, (const uint2*)d_pairs, npairs,
+                       ctx->owner, key_lo);
+  }
+  {
+    ScopedTimer tm(ctx, "shard_resolve");
+    hipLaunchKernelGGL(k_shard_resolve, dim3(grid), dim3(256), 0, ctx->stream, (const uint2*)d_pairs, npairs,
+                       (const uint32_t*)ctx->owner, key_lo, d_rec_bits, d_new_vals, (unsigned long long*)d_nnew);
+  }
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_shard_flags_dev(sg_ctx* ctx, const uint32_t* d_bits, uint32_t nparts, uint64_t words_per_part, uint64_t rec_lo,
+                       uint64_t nrec, uint8_t* d_rec_new) {
+  if (!ctx || (nrec && (!d_bits || !d_rec_new || nparts == 0)) ||
+      (nrec && ((rec_lo + nrec + 31) >> 5) - (rec_lo >> 5) > words_per_part)) {
+    set_error("sg_shard_flags_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  if (nrec == 0) return SG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "shard_flags");
+  hipLaunchKernelGGL(k_shard_flags, dim3(div_up(nrec, 256)), dim3(256), 0, ctx->stream, d_bits, nparts,
+                     words_per_part, rec_lo, nrec, d_rec_new);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {
+  if (!set || (n && !d_vals)) return SG_EINVAL;
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "set_add");
+  hipLaunchKernelGGL(k_set_add_vals, dim3(std::min<uint64_t>(div_up(n, 256), 16384)), dim3(256), 0, ctx->stream,
+                     set->words, d_vals, n);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+"""One batch's new-signal triage, hash-sharded by signal across GPUs.
+
+Reference: syz-fuzzer/fuzzer.go:645-693 -- ONE sequential loop over every call
+record of the batch (records program-major, call index ascending).  The batch's
+records are split contiguously across the ranks of a process group (one GPU
+each, RCCL over xGMI); every rank holds the same maxSignal snapshot.  Results
+are those of the single sequential loop: record r is queued iff it is the first
+record holding some signal s not in maxSignal (the first-owner rule,
+DESIGN.md §2), and maxSignal' = maxSignal ∪ every record's signal.
+
+Protocol of one step, per rank:
+  1. candidates -- sg_shard_candidates_dev: the rank's distinct s not in the
+     snapshot with their first (global) record, grouped by owning shard
+     sg_shard_of(s, G).  Only candidates travel.
+  2. all-to-all of the pair counts, then of the pairs (RCCL all_to_all_single).
+  3. owners -- sg_shard_owners_dev: owner(s) = min record over the pairs this
+     shard received; the owners' bits in a batch-wide record bitset; each new s
+     once.
+  4. all-to-all of each rank's slice of the record bitset back to it, OR of
+     the G slices into its records' flags (sg_shard_flags_dev; RCCL has no
+     bitwise-OR reduction).
+  5. all-gather of every shard's new signal; maxSignal / newSignal ∪= it
+     (sg_set_add_dev), so the replicated state stays identical on all ranks.
+
+The stage computations are a backend: HipStages (libsyzsig.so) in the
+product; the CPU tests drive the same protocol with a numpy restatement of the
+stages over gloo (tests/test_shard.py).  Collectives run on device tensors
+under RCCL ("nccl"); under gloo they are staged through host memory.
+"""
+import torch
+import torch.distributed as dist
+
+from ._lib import call
+
+
+class Comm:
+    """The collectives of the protocol over a torch.distributed group (or a
+    single rank when torch.distributed is not initialised)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.on else 1
+        self.rank = dist.get_rank(group) if self.on else 0
+        self.host = self.on and dist.get_backend(group) != "nccl"  # gloo: host-staged
+
+    def _stage(self, t):
+        return t.cpu() if self.host and t.is_cuda else t
+
+    def all_gather_i64(self, values):
+        """[values of rank 0, values of rank 1, ...] for a short int64 list."""
+        dev = "cpu" if (self.host or not torch.cuda.is_available()) else "cuda"
+        t = torch.tensor(values, dtype=torch.int64, device=dev)
+        if self.world == 1:
+            return [values]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [x.tolist() for x in out]
+
+    def exchange_counts(self, counts):
+        """counts[k] goes to rank k; returns what every rank sent here."""
+        if self.world == 1:
+            return list(counts)
+        dev = "cpu" if self.host else "cuda"
+        s = torch.tensor(counts, dtype=torch.int64, device=dev)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=self.group)
+        return r.tolist()
+
+    def all_to_all(self, send, send_splits, recv_splits):
+        """all_to_all_single with variable splits (element counts)."""
+        if self.world == 1:
+            return send[: send_splits[0]]
+        dev = send.device
+        recv = torch.empty(sum(recv_splits), dtype=send.dtype, device="cpu" if self.host else dev)
+        dist.all_to_all_single(recv, self._stage(send[: sum(send_splits)]), recv_splits, send_splits, group=self.group)
+        return recv.to(dev) if self.host else recv
+
+    def all_gather_var(self, t, n):
+        """The first n elements of t from every rank, concatenated."""
+        if self.world == 1:
+            return t[:n]
+        counts = [c[0] for c in self.all_gather_i64([n])]
+        m = max(counts)
+        dev = t.device
+        buf = torch.zeros(m, dtype=t.dtype, device="cpu" if self.host else dev)
+        buf[:n] = self._stage(t[:n])
+        out = torch.empty(m * self.world, dtype=t.dtype, device=buf.device)
+        if self.host:
+            parts = list(out.view(self.world, m).unbind(0))
+            dist.all_gather(parts, buf, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, buf, group=self.group)
+        got = torch.cat([out[k * m: k * m + counts[k]] for k in range(self.world)])
+        return got.to(dev) if self.host else got
+
+
+class HipStages:
+    """The stage kernels of libsyzsig.so (include/syzsig.h, sg_shard.hip)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        # stage outputs are read with torch (.tolist / .item): queue the
+        # library's work on torch's current stream
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def candidates(self, snapshot, vals, off, nvals, nrec, rec_base, nshards, pairs):
+        shard_off = torch.empty(nshards + 1, dtype=torch.int64, device="cuda")
+        call("sg_shard_candidates_dev", self.ctx.h, snapshot.h, vals.data_ptr() if nvals else None, off.data_ptr(),
+             nvals, nrec, rec_base, nshards, pairs.data_ptr() if nvals else None, shard_off.data_ptr())
+        return shard_off.tolist()  # the counts are needed on the host for the exchange
+
+    def owners(self, pairs, npairs, nrec_total, rec_bits, new_vals):
+        nnew = torch.empty(1, dtype=torch.int64, device="cuda")
+        call("sg_shard_owners_dev", self.ctx.h, pairs.data_ptr() if npairs else None, npairs, nrec_total,
+             rec_bits.data_ptr(), new_vals.data_ptr() if npairs else None, nnew.data_ptr())
+        return int(nnew.item())
+
+    def flags(self, bits, nparts, words_per_part, rec_lo, nrec, rec_new):
+        if nrec:
+            call("sg_shard_flags_dev", self.ctx.h, bits.data_ptr(), nparts, words_per_part, rec_lo, nrec,
+                 rec_new.data_ptr())
+
+    def add(self, sset, vals, n):
+        if n:
+            call("sg_set_add_dev", sset.h, vals.data_ptr(), n)
+
+
+class ShardedTriage:
+    """fuzzer.go:645-693 over one batch spread across the ranks of `comm`.
+
+    Buffers are allocated once and grown as needed (the pair buffers hold up to
+    one pair per signal entry of the rank's slice)."""
+
+    def __init__(self, stages, comm=None, device="cuda"):
+        self.st = stages
+        self.comm = comm if comm is not None else Comm()
+        self.device = device
+        self._bufs = {}
+        self.last = {}
+
+    def _buf(self, name, n, dtype=torch.int32):
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 1), dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b
+
+    def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new):
+        """Triage records rec_base .. rec_base+nrec-1 of the batch held by this
+        rank (vals / off its CSR slice, off[0] == 0) against maxsig, the
+        replicated snapshot.  rec_new[:nrec] gets their flags; maxsig / newsig
+        (nullable) gain every shard's new signal.  Returns the batch's record
+        count."""
+        c, G = self.comm, self.comm.world
+        ranges = c.all_gather_i64([rec_base, nrec])
+        nrec_total = max(rb + n for rb, n in ranges)
+        # 1. candidates grouped by owning shard
+        pairs = self._buf("pairs", 2 * nvals)
+        shard_off = self.st.candidates(maxsig, vals, off, nvals, nrec, rec_base, G, pairs)
+        send_pairs = [shard_off[k + 1] - shard_off[k] for k in range(G)]
+        # 2. route them to their shards
+        recv_pairs = c.exchange_counts(send_pairs)
+        recv = c.all_to_all(pairs, [2 * x for x in send_pairs], [2 * x for x in recv_pairs])
+        npairs = sum(recv_pairs)
+        # 3. first owners of this shard's signals
+        nwords = (nrec_total + 31) // 32
+        rec_bits = self._buf("rec_bits", nwords)
+        new_vals = self._buf("new_vals", npairs)
+        nnew = self.st.owners(recv, npairs, nrec_total, rec_bits, new_vals)
+        # 4. each rank's slice of the record bitset back to it, OR-ed there
+        w0 = [rb >> 5 for rb, n in ranges]
+        w1 = [((rb + n + 31) >> 5) if n else (rb >> 5) for rb, n in ranges]
+        send_w = [w1[k] - w0[k] for k in range(G)]
+        if G > 1:
+            send = torch.cat([rec_bits[w0[k]:w1[k]] for k in range(G)])
+        else:
+            send = rec_bits[w0[0]:w1[0]]
+        mine = send_w[c.rank]
+        got = c.all_to_all(send, send_w, [mine] * G)
+        self.st.flags(got, G, mine, rec_base, nrec, rec_new)
+        # 5. every shard's new signal into the replicated sets
+        allnew = c.all_gather_var(new_vals, nnew)
+        n_all = int(allnew.numel())
+        self.st.add(maxsig, allnew, n_all)
+        if newsig is not None:
+            self.st.add(newsig, allnew, n_all)
+        self.last = {"pairs_sent": sum(send_pairs), "pairs_received": npairs, "new_signal": n_all,
+                     "nrec_total": nrec_total}
+        return nrec_total
+

@@ -217,10 +217,10 @@ class TwoPaths:
     """The same sets kept twice: one pair driven through the diff-emitting
     claim/resolve path, one through the flags-only partitioned path."""
 
-    def __init__(self, C):
+    def __init__(self, C, ctx=None):
         self.C = C
-        self.d = (C.SignalSet(), C.SignalSet())
-        self.f = (C.SignalSet(), C.SignalSet())
+        self.d = (C.SignalSet(ctx), C.SignalSet(ctx))
+        self.f = (C.SignalSet(ctx), C.SignalSet(ctx))
 
     def add(self, vals):
         self.C.SignalAdd(self.d[0], vals)
@@ -538,7 +538,9 @@ def test_triage_record_slices(C, monkeypatch):
     rng = np.random.default_rng(131)
     for limit, nrec in ((1000, 4321), (100000, 240000), (7, 50)):
         monkeypatch.setenv("SG_TRIAGE_MAX_RECS", str(limit))
-        P = TwoPaths(C)
+        ctx = C.Context(0)  # the switch is read at context creation
+        assert ctx.counter("max_launch_records") == limit
+        P = TwoPaths(C, ctx)
         om, on = O.OSet(), O.OSet()
         lens = rng.integers(0, 40, size=nrec)
         lens[rng.integers(0, nrec, size=nrec // 5)] = 0
@@ -550,7 +552,46 @@ def test_triage_record_slices(C, monkeypatch):
         _check_triage(P, (om, on), vals, off)
         m, n = P.exports()
         assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
+        del P
+        ctx.close()
     monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
+
+
+def test_owner_key_generation_reset(C, monkeypatch):
+    """The first-owner table (sg_ctx.hip owner_keys) hands out decreasing keys
+    and starts a fresh generation (a full reset of the table) when the key
+    space runs out.  The key space is lowered here so that record-keyed
+    triage, element-keyed Poll merges and rank-keyed Minimize cross several
+    resets; every result still equals the oracle's."""
+    monkeypatch.setenv("SG_OWNER_KEY_SPACE", "6000")
+    ctx = C.Context(0)
+    assert ctx.counter("owner_key_space") == 6000
+    rng = np.random.default_rng(151)
+    ms, ns, mm = C.SignalSet(ctx), C.SignalSet(ctx), C.SignalSet(ctx)
+    om, on, omm = O.OSet(), O.OSet(), O.OSet()
+    for it in range(9):
+        nrec = int(rng.integers(1000, 2500))
+        lens = rng.integers(0, 12, size=nrec)
+        vals = rng.integers(0, 1 << 16, size=int(lens.sum())).astype(np.uint32)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        flags, dv, do = C.triage_batch(ms, ns, vals, off)  # claim/resolve: record keys
+        ef, ev, eo = O.triage_batch(om, on, vals, off)
+        assert np.array_equal(flags, ef) and np.array_equal(dv, ev) and np.array_equal(do, eo), it
+        polls = [rng.permutation(np.unique(rng.integers(0, 1 << 17, size=int(rng.integers(0, 900)))).astype(np.uint32))
+                 for _ in range(4)]
+        av, ao = C.to_csr(polls)
+        nv, no = C.merge_poll(mm, av, ao, ctx=ctx)  # element keys
+        ev2, eo2 = O.merge_poll(omm, av, ao)
+        assert np.array_equal(nv, ev2) and np.array_equal(no, eo2), it
+        covs = [C.Canonicalize(rng.integers(0, 3000, size=int(rng.integers(0, 40))).astype(np.uint32), ctx=ctx)
+                for _ in range(700)]
+        cv, co = C.to_csr(covs)
+        assert np.array_equal(C.minimize_csr(cv, co, ctx=ctx), O.minimize(cv, co)), it  # rank keys
+    assert ctx.counter("owner_resets") >= 3
+    assert np.array_equal(ms.export(), om.export()) and np.array_equal(ns.export(), on.export())
+    assert np.array_equal(mm.export(), omm.export())
+    del ms, ns, mm
+    ctx.close()
 
 
 def test_cover_uncovered_radix_edges(C):

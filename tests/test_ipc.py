@@ -98,3 +98,34 @@ def test_ipc_parse_feeds_triage(ctx):
     om, on = O.OSet(), O.OSet()
     eflags, _, _ = O.triage_batch(om, on, sv, so)
     assert np.array_equal(np.asarray(flags), np.asarray(eflags))
+
+
+@pytest.mark.gpu
+def test_ipc_parse_feeds_triage_with_failed_programs(ctx):
+    """A batch with every reader error path planted: the failed programs'
+    records carry no signal in the CSR (execute1 never returns their info,
+    fuzzer.go:752-768), so triaging the CSR as is equals the oracle's
+    sequential loop over the successful programs' records only."""
+    from oracle import pyoracle as O
+    from syzkaller_amd import cover as C
+
+    out, oo, co, nums = K.batch(13, nprog=240, kinds=K.FAULTS, maxsig=800)
+    _, _, status, sv, so, _, _ = C.ipc_parse(out, oo, co, nums, cover=False)
+    assert (status != 0).any() and (status == 0).any()
+    # the oracle's view: the reader's signal of the successful programs only
+    _, _, e_status, e_sig, _ = I.parse_batch(out, oo, co, nums)
+    assert status.tolist() == e_status
+    ok_recs = [r for p in range(len(e_status)) if e_status[p] == 0 for r in range(int(co[p]), int(co[p + 1]))]
+    for p in range(len(e_status)):
+        if e_status[p] != 0:
+            assert all(so[r + 1] == so[r] for r in range(int(co[p]), int(co[p + 1])))
+    m, n = C.SignalSet(), C.SignalSet()
+    flags, _, _ = C.triage_batch(m, n, sv, so)
+    om, on = O.OSet(), O.OSet()
+    ok_sig = [e_sig[r] for r in ok_recs]
+    ov = np.array([x for s in ok_sig for x in s], np.uint32)
+    oo_ = np.concatenate([[0], np.cumsum([len(s) for s in ok_sig])]).astype(np.uint64)
+    eflags, _, _ = O.triage_batch(om, on, ov, oo_)
+    assert np.array_equal(np.asarray(flags)[ok_recs], np.asarray(eflags))
+    assert not np.asarray(flags)[[r for r in range(flags.size) if r not in set(ok_recs)]].any()
+    assert np.array_equal(m.export(), om.export()) and np.array_equal(n.export(), on.export())

@@ -1,0 +1,224 @@
+"""The sharded triage's stage kernels (sg_shard.hip) against their numpy
+restatements, and the whole protocol (syzkaller_amd/shard.py) on the GPU
+against the oracle's sequential loop (syz-fuzzer/fuzzer.go:645-693): one rank,
+and two ranks sharing the one GPU of the test box over gloo (host-staged
+exchanges; RCCL needs one GPU per rank)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pyoracle as O
+from tests.test_shard import NumpyStages, NpSet, shard_of
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(seed, nrec, hi=1 << 22, maxlen=60):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen, size=nrec)
+    lens[rng.integers(0, nrec, size=max(1, nrec // 5))] = 0
+    vals = rng.integers(0, hi, size=int(lens.sum())).astype(np.uint32)
+    vals[rng.integers(0, vals.size, size=vals.size // 3)] = vals[rng.integers(0, vals.size, size=vals.size // 3)]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    return vals, off
+
+
+def _dev(a, dt):
+    return torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()
+
+
+def _pairs_by_shard(pairs, shard_off, g):
+    p = pairs.view(-1, 2)
+    return [p[shard_off[k]:shard_off[k + 1]] for k in range(g)]
+
+
+@pytest.mark.parametrize("g", [1, 3, 8])
+def test_shard_candidates_vs_numpy(ctx, g):
+    from syzkaller_amd.cover import SignalSet
+    from syzkaller_amd.shard import HipStages
+
+    vals, off = _batch(200 + g, 30000)
+    m0 = np.unique(vals[:: 3])
+    snap = SignalSet(ctx)
+    from syzkaller_amd import cover as C
+    C.SignalAdd(snap, m0)
+    st = HipStages(ctx)
+    pairs = torch.empty(2 * vals.size, dtype=torch.int32, device="cuda")
+    so = st.candidates(snap, _dev(vals, np.int32), _dev(off, np.int64), vals.size, off.size - 1, 1000, g, pairs)
+    exp_pairs = torch.zeros(2 * vals.size, dtype=torch.int32)
+    eso = NumpyStages().candidates(NpSet(m0), torch.from_numpy(vals.view(np.int32)),
+                                   torch.from_numpy(off.view(np.int64)), vals.size, off.size - 1, 1000, g, exp_pairs)
+    assert so == eso
+    got = pairs.cpu().numpy().view(np.uint32)
+    exp = exp_pairs.numpy().view(np.uint32)
+    for k in range(g):
+        a = got[2 * so[k]: 2 * so[k + 1]].reshape(-1, 2)
+        b = exp[2 * eso[k]: 2 * eso[k + 1]].reshape(-1, 2)
+        a = a[np.lexsort((a[:, 1], a[:, 0]))]
+        assert np.array_equal(a, b), k
+        assert (shard_of(a[:, 0], g) == k).all()
+    # the snapshot is only read
+    assert np.array_equal(snap.export(), m0)
+
+
+def test_shard_candidates_record_slices(C, monkeypatch):
+    """Record slices of the local stage (a lowered per-launch record limit):
+    a signal may come once per slice; its smallest record is the first one."""
+    from syzkaller_amd.shard import HipStages
+
+    monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
+    ctx2 = C.Context(0)
+    vals, off = _batch(301, 5000, hi=1 << 16)
+    snap = C.SignalSet(ctx2)
+    st = HipStages(ctx2)
+    pairs = torch.empty(2 * vals.size, dtype=torch.int32, device="cuda")
+    so = st.candidates(snap, _dev(vals, np.int32), _dev(off, np.int64), vals.size, off.size - 1, 0, 4, pairs)
+    exp_pairs = torch.zeros(2 * vals.size, dtype=torch.int32)
+    eso = NumpyStages().candidates(NpSet(), torch.from_numpy(vals.view(np.int32)), torch.from_numpy(off.view(np.int64)),
+                                   vals.size, off.size - 1, 0, 4, exp_pairs)
+    got = pairs.cpu().numpy().view(np.uint32)[: 2 * so[-1]].reshape(-1, 2)
+    exp = exp_pairs.numpy().view(np.uint32)[: 2 * eso[-1]].reshape(-1, 2)
+    u, first = np.unique(got[np.lexsort((got[:, 1], got[:, 0]))][:, 0], return_index=True)
+    srt = got[np.lexsort((got[:, 1], got[:, 0]))]
+    assert np.array_equal(srt[first], exp)
+    del snap
+    ctx2.close()
+
+
+@pytest.fixture(scope="module")
+def C(ctx):
+    from syzkaller_amd import cover
+
+    return cover
+
+
+def test_shard_owners_and_flags_vs_numpy(ctx):
+    from syzkaller_amd.shard import HipStages
+
+    rng = np.random.default_rng(7)
+    nrec_total = 100000
+    parts = []
+    for r in range(5):  # five senders: distinct s per sender
+        s = np.unique(rng.integers(0, 1 << 18, size=20000)).astype(np.uint32)
+        rec = rng.integers(0, nrec_total, size=s.size).astype(np.uint32)
+        parts.append(np.stack([s, rec], axis=1))
+    p = np.concatenate(parts).reshape(-1)
+    npairs = p.size // 2
+    st = HipStages(ctx)
+    bits = torch.empty((nrec_total + 31) // 32, dtype=torch.int32, device="cuda")
+    new = torch.empty(npairs, dtype=torch.int32, device="cuda")
+    nnew = st.owners(_dev(p, np.int32), npairs, nrec_total, bits, new)
+    ebits = torch.zeros((nrec_total + 31) // 32, dtype=torch.int32)
+    enew = torch.zeros(npairs, dtype=torch.int32)
+    ennew = NumpyStages().owners(torch.from_numpy(p.view(np.int32)), npairs, nrec_total, ebits, enew)
+    assert nnew == ennew
+    assert np.array_equal(bits.cpu().numpy(), ebits.numpy())
+    assert np.array_equal(np.sort(new[:nnew].cpu().numpy().view(np.uint32)), np.sort(enew[:ennew].numpy().view(np.uint32)))
+    # flags: three parts of one rank's word range, odd record bounds
+    for rec_lo, nrec in ((0, 64), (37, 1000), (96, 5), (12345, 54321)):
+        wpp = ((rec_lo + nrec + 31) >> 5) - (rec_lo >> 5)
+        b = rng.integers(-(1 << 31), (1 << 31) - 1, size=3 * wpp).astype(np.int32)
+        got = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+        st.flags(_dev(b, np.int32), 3, wpp, rec_lo, nrec, got)
+        exp = torch.zeros(nrec, dtype=torch.uint8)
+        NumpyStages().flags(torch.from_numpy(b), 3, wpp, rec_lo, nrec, exp)
+        assert np.array_equal(got.cpu().numpy(), exp.numpy()), (rec_lo, nrec)
+
+
+def _run_protocol(ctx_dev, world, rank, batches, m0):
+    from syzkaller_amd import cover as C
+    from syzkaller_amd.shard import Comm, HipStages, ShardedTriage
+    from tests.test_shard import split
+
+    ctx = C.Context(ctx_dev)
+    tri = ShardedTriage(HipStages(ctx), Comm())
+    ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
+    C.SignalAdd(ms, m0)
+    out = []
+    for seed, nrec in batches:
+        vals, off = _batch(seed, nrec)
+        r0, r1 = split(nrec, world, seed)[rank] if world > 1 else (0, nrec)
+        e0, e1 = int(off[r0]), int(off[r1])
+        v = _dev(vals[e0:e1] if e1 > e0 else np.zeros(1, np.uint32), np.int32)
+        o = _dev((off[r0:r1 + 1] - off[r0]).astype(np.uint64), np.int64)
+        rec_new = torch.zeros(max(r1 - r0, 1), dtype=torch.uint8, device="cuda")
+        tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new)
+        out.append((r0, rec_new[: r1 - r0].cpu().tolist()))
+    res = (out, ms.export().tolist(), ns.export().tolist())
+    del ms, ns, tri
+    ctx.close()
+    return res
+
+
+BATCHES = [(401, 4000), (402, 3000), (403, 0), (404, 5000)]
+M0 = np.unique(np.random.default_rng(400).integers(0, 1 << 22, size=50000)).astype(np.uint32)
+
+
+def _expected():
+    om, on = O.OSet(M0), O.OSet()
+    flags = []
+    for seed, nrec in BATCHES:
+        vals, off = _batch(seed, nrec)
+        flags.append(O.triage_flags_only(om, on, vals, off))
+    return flags, om.export().tolist(), on.export().tolist()
+
+
+def test_sharded_protocol_one_rank_vs_oracle(ctx):
+    out, m, n = _run_protocol(0, 1, 0, BATCHES, M0)
+    ef, em, en = _expected()
+    for b, (r0, fl) in enumerate(out):
+        assert np.array_equal(np.array(fl, np.uint8), ef[b]), b
+        if BATCHES[b][1] > 100:
+            assert 0 < ef[b].sum() < BATCHES[b][1]
+    assert m == em and n == en
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run_protocol(0, world, rank, BATCHES, M0)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_protocol_two_ranks_one_gpu():
+    import torch.multiprocessing as mp
+
+    world = 2
+    port = _free_port()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    procs = [mctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, v = q.get(timeout=280)
+        res[r] = v
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ef, em, en = _expected()
+    for b, (seed, nrec) in enumerate(BATCHES):
+        got = np.zeros(nrec, np.uint8)
+        for r in range(world):
+            r0, fl = res[r][0][b]
+            got[r0:r0 + len(fl)] = fl
+        assert np.array_equal(got, ef[b]), b
+    for r in range(world):
+        assert res[r][1] == em and res[r][2] == en
