@@ -167,6 +167,23 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
  * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */
 int sg_add_inputs(sg_ctx* ctx, sg_set* corpus, sg_set* maxsig, const uint32_t* vals, const uint64_t* off, size_t n);
 
+/* syz-fuzzer/fuzzer.go:521-611 triageInput()'s signal math, over n inputs at
+ * once (the -procs triage goroutines, or a batch of triage candidates).
+ * fuzzer.go:526-532: new_k = Canonicalize(SignalDiff(corpusSignal, S_k)),
+ * every input against the same corpusSignal (only read).  S_k = vals[off[k] ..
+ * off[k+1]); new_vals capacity off[n]; new_off (n+1) gives each new_k. */
+int sg_triage_newsig(sg_ctx* ctx, sg_set* corpus, const uint32_t* vals, const uint64_t* off, size_t n,
+		     uint32_t* new_vals, uint64_t* new_off);
+/* fuzzer.go:567: new_k = Intersection(new_k, Canonicalize(R_k)) for sorted new_k
+ * (new_vals[new_off[k] ..]) and raw re-execution signal R_k (r_vals[r_off[k]
+ * ..]); the result is written at new_k's own start, out_len[k] = its length. */
+int sg_triage_intersect(sg_ctx* ctx, uint32_t* new_vals, const uint64_t* new_off, const uint32_t* r_vals,
+			const uint64_t* r_off, size_t n, uint64_t* out_len);
+/* fuzzer.go:584-587, the minimisation predicate: ok[k] =
+ * len(Intersection(new_k, Canonicalize(R_k))) == len(new_k). */
+int sg_triage_subset(sg_ctx* ctx, const uint32_t* new_vals, const uint64_t* new_off, const uint32_t* r_vals,
+		     const uint64_t* r_off, size_t n, uint8_t* ok);
+
 /* syz-manager/manager.go:907-912 NewInput() signal part, over n RPCs in
  * arrival order: accepted[k] = SignalNew(corpusSignal, S_k) at its turn; on
  * accept corpusSignal ∪= S_k and corpusCover ∪= Cov_k.  cover may be NULL. */
@@ -190,6 +207,35 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
 /* order of cover.Minimize: Go's sort.Sort over minInputArray (Less = longer
  * first, cover.go:157), restated from the Go 1.8/1.9 sort package. */
 int sg_minimize_order(const uint64_t* off, size_t n, uint32_t* order);
+
+/* ---- RPC payloads (pkg/rpctype/rpctype.go:8-63) --------------------------- */
+/* Wire form of a sorted []uint32 (RpcInput.Signal / .Cover are canonical;
+ * ConnectRes.MaxSignal, PollArgs.MaxSignal and PollRes.MaxSignal are set
+ * members): Go's binary.PutUvarint of the first value, then of each successive
+ * difference.  A Go peer decodes it with binary.Uvarint and a running sum.
+ * Batched over n lists: list k is vals[off[k] .. off[k+1]) (non-decreasing,
+ * else SG_EINVAL); its bytes go to out[out_off[k] .. out_off[k+1]).  out_off
+ * (n+1) is always filled; the bytes are copied only when out_off[n] <= cap
+ * (cap = 5 * off[n] always suffices). */
+int sg_delta_encode_batch(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, uint8_t* out, size_t cap,
+			  uint64_t* out_off);
+/* The inverse: list k from in[in_off[k] .. in_off[k+1]) into vals[off[k] ..)
+ * (capacity cap values; in_off[n] always suffices).  SG_EINVAL on a malformed
+ * payload (a list ending inside a value, a value or running sum past 32 bits). */
+int sg_delta_decode_batch(sg_ctx* ctx, const uint8_t* in, const uint64_t* in_off, size_t n, uint32_t* vals, size_t cap,
+			  uint64_t* off);
+/* A set's members (ascending) as one payload: fuzzer.go:358-364 (PollArgs.MaxSignal
+ * from newSignal), manager.go:801-806 / :962 (ConnectRes / PollRes.MaxSignal).
+ * *nbytes = payload size; bytes copied only when it is <= cap. */
+int sg_set_encode(sg_set* set, uint8_t* out, size_t cap, size_t* nbytes);
+/* SignalAdd of a decoded payload (fuzzer.go:146-151, :392-398); *count
+ * (nullable) = values in it. */
+int sg_set_decode_add(sg_set* set, const uint8_t* in, size_t nbytes, uint64_t* count);
+/* tools/syz-execprog/execprog.go:159-177: the sancov file of each of n calls:
+ * u64 0xC0BFFFFFFFFFFF64, then RestorePC(pc, 0xffffffff) (cover.go:23-25) per
+ * cover PC, little-endian.  File k is out[8*(k + cov_off[k]) .. 8*(k+1 +
+ * cov_off[k+1])) (out: 8*(n + cov_off[n]) bytes). */
+int sg_sancov_batch(sg_ctx* ctx, const uint32_t* cov, const uint64_t* cov_off, size_t n, uint8_t* out);
 
 /* ---- sorted-slice algebra (pkg/cover/cover.go:28-117) ---------------------- */
 /* Canonicalize (cover.go:28-40): in place, *nout = canonical length. */

@@ -145,6 +145,40 @@ def signal_diff(s, sig):
     return out[:n].copy()
 
 
+def triage_newsig(corpus, vals, off):
+    """syz-fuzzer/fuzzer.go:526-532 per input: Canonicalize(SignalDiff(corpusSignal, S_k))
+    (cover.go:169-176 then cover.go:28-40), every input against the same corpus."""
+    vals, off = _u32(vals), _u64(off)
+    outs = []
+    for k in range(off.size - 1):
+        a, n = canonicalize(signal_diff(corpus, vals[int(off[k]):int(off[k + 1])]))
+        outs.append(a[:n])
+    return _csr(outs)
+
+
+def triage_intersect(new_vals, new_off, r_vals, r_off):
+    """fuzzer.go:567 per input: Intersection(new_k, Canonicalize(R_k)) (cover.go:72-79)."""
+    outs = []
+    for k in range(new_off.size - 1):
+        r, n = canonicalize(r_vals[int(r_off[k]):int(r_off[k + 1])])
+        outs.append(foreach(INTER, new_vals[int(new_off[k]):int(new_off[k + 1])], r[:n]))
+    return _csr(outs)
+
+
+def triage_subset(new_vals, new_off, r_vals, r_off):
+    """fuzzer.go:584-587 per input: len(Intersection(new_k, Canonicalize(R_k))) == len(new_k)."""
+    iv, io = triage_intersect(new_vals, new_off, r_vals, r_off)
+    return ((io[1:] - io[:-1]) == (_u64(new_off)[1:] - _u64(new_off)[:-1])).astype(np.uint8)
+
+
+def _csr(lists):
+    off = np.zeros(len(lists) + 1, dtype=np.uint64)
+    if lists:
+        off[1:] = np.cumsum([len(x) for x in lists])
+    vals = np.concatenate([_u32(x) for x in lists]) if lists else np.zeros(0, np.uint32)
+    return vals.astype(np.uint32), off
+
+
 def triage_batch(maxset, newset, vals, off):
     vals, off = _u32(vals), _u64(off)
     nrec = off.size - 1

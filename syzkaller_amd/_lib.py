@@ -64,10 +64,18 @@ SIGNATURES = {
     "sg_shard_flags_dev": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_uint64, c_uint64, c_void_p]),
     "sg_set_add_dev": (c_int, [c_void_p, c_void_p, c_uint64]),
     "sg_add_inputs": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t]),
+    "sg_triage_newsig": (c_int, [c_void_p, c_void_p, P32, P64, c_size_t, P32, P64]),
+    "sg_triage_intersect": (c_int, [c_void_p, P32, P64, P32, P64, c_size_t, P64]),
+    "sg_triage_subset": (c_int, [c_void_p, P32, P64, P32, P64, c_size_t, P8]),
     "sg_accept_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, P32, P64, c_size_t, P8]),
     "sg_merge_poll": (c_int, [c_void_p, c_void_p, P32, P64, c_size_t, P32, P64]),
     "sg_minimize": (c_int, [c_void_p, P32, P64, c_size_t, P32, P32, PSZ]),
     "sg_minimize_order": (c_int, [P64, c_size_t, P32]),
+    "sg_delta_encode_batch": (c_int, [c_void_p, P32, P64, c_size_t, P8, c_size_t, P64]),
+    "sg_delta_decode_batch": (c_int, [c_void_p, P8, P64, c_size_t, P32, c_size_t, P64]),
+    "sg_set_encode": (c_int, [c_void_p, P8, c_size_t, PSZ]),
+    "sg_set_decode_add": (c_int, [c_void_p, P8, c_size_t, P64]),
+    "sg_sancov_batch": (c_int, [c_void_p, P32, P64, c_size_t, P8]),
     "sg_canonicalize": (c_int, [c_void_p, P32, c_size_t, PSZ]),
     "sg_canonicalize_batch": (c_int, [c_void_p, P32, P64, c_size_t, P64]),
     "sg_merge": (c_int, [c_void_p, c_int, P32, c_size_t, P32, c_size_t, P32, PSZ]),

@@ -268,6 +268,42 @@ def add_inputs(corpus, maxset, vals, off, ctx=None):
     call("sg_add_inputs", c.h, corpus.h, maxset.h, _p32(vals), _p64(off), off.size - 1)
 
 
+def triage_newsig(corpus, vals, off, ctx=None):
+    """syz-fuzzer/fuzzer.go:526-532 over a batch of triage inputs:
+    new_k = Canonicalize(SignalDiff(corpusSignal, S_k)).  Returns (vals, off)."""
+    vals, off = _u32(vals), _u64(off)
+    n = off.size - 1
+    nv = np.empty(max(vals.size, 1), dtype=U32)
+    no = np.zeros(n + 1, dtype=U64)
+    c = corpus.ctx if ctx is None else ctx
+    call("sg_triage_newsig", c.h, corpus.h, _p32(vals), _p64(off), n, _p32(nv), _p64(no))
+    return nv[: int(no[-1])], no
+
+
+def triage_intersect(new_vals, new_off, r_vals, r_off, ctx=None):
+    """fuzzer.go:567 over a batch: new_k = Intersection(new_k, Canonicalize(R_k)).
+    Returns the packed (vals, off)."""
+    nv, no = _u32(new_vals).copy(), _u64(new_off)
+    rv, ro = _u32(r_vals), _u64(r_off)
+    n = no.size - 1
+    lens = np.zeros(n, dtype=U64)
+    call("sg_triage_intersect", _ctx(ctx).h, _p32(nv), _p64(no), _p32(rv), _p64(ro), n, _p64(lens))
+    out_off = np.concatenate([[0], np.cumsum(lens)]).astype(U64)
+    out = np.concatenate([nv[int(no[k]): int(no[k]) + int(lens[k])] for k in range(n)]) if n else nv[:0]
+    return out.astype(U32), out_off
+
+
+def triage_subset(new_vals, new_off, r_vals, r_off, ctx=None):
+    """fuzzer.go:584-587, the minimisation predicate over a batch:
+    ok[k] = len(Intersection(new_k, Canonicalize(R_k))) == len(new_k)."""
+    nv, no = _u32(new_vals), _u64(new_off)
+    rv, ro = _u32(r_vals), _u64(r_off)
+    n = no.size - 1
+    ok = np.zeros(n, dtype=np.uint8)
+    call("sg_triage_subset", _ctx(ctx).h, _p32(nv), _p64(no), _p32(rv), _p64(ro), n, _p8(ok))
+    return ok
+
+
 def accept_batch(corpus_sig, corpus_cov, sig_vals, sig_off, cov_vals=None, cov_off=None, ctx=None):
     """syz-manager/manager.go:907-912 NewInput acceptance over a batch."""
     sv, so = _u32(sig_vals), _u64(sig_off)
@@ -291,6 +327,55 @@ def merge_poll(mgr_max, a_vals, a_off, ctx=None):
     c = mgr_max.ctx if ctx is None else ctx
     call("sg_merge_poll", c.h, mgr_max.h, _p32(av), _p64(ao), npoll, _p32(nv), _p64(no))
     return nv[: int(no[-1])], no
+
+
+# ---- RPC payloads (pkg/rpctype/rpctype.go:8-63) ------------------------------------
+def delta_encode(vals, off, ctx=None):
+    """Sorted lists -> their delta-varint payloads (bytes, byte offsets)."""
+    vals, off = _u32(vals), _u64(off)
+    n = off.size - 1
+    bo = np.zeros(n + 1, dtype=U64)
+    out = np.empty(max(5 * vals.size, 1), dtype=np.uint8)
+    call("sg_delta_encode_batch", _ctx(ctx).h, _p32(vals), _p64(off), n, _p8(out), out.size, _p64(bo))
+    return out[: int(bo[-1])].copy(), bo
+
+
+def delta_decode(data, data_off, ctx=None):
+    """Payloads -> the sorted lists (vals, off)."""
+    data = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if isinstance(data, (bytes, bytearray))
+                                else np.asarray(data, dtype=np.uint8))
+    do = _u64(data_off)
+    n = do.size - 1
+    vals = np.empty(max(data.size, 1), dtype=U32)
+    off = np.zeros(n + 1, dtype=U64)
+    call("sg_delta_decode_batch", _ctx(ctx).h, _p8(data), _p64(do), n, _p32(vals), vals.size, _p64(off))
+    return vals[: int(off[-1])].copy(), off
+
+
+def set_encode(sset):
+    """The set's members as one payload (PollArgs / ConnectRes / PollRes .MaxSignal)."""
+    nb = c_size_t()
+    call("sg_set_encode", sset.h, None, 0, byref(nb))
+    out = np.empty(max(nb.value, 1), dtype=np.uint8)
+    call("sg_set_encode", sset.h, _p8(out), out.size, byref(nb))
+    return out[: nb.value].tobytes()
+
+
+def set_decode_add(sset, payload):
+    """SignalAdd of a payload (fuzzer.go:146-151, :392-398); returns its value count."""
+    data = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+    cnt = c_uint64()
+    call("sg_set_decode_add", sset.h, _p8(data), data.size, byref(cnt))
+    return cnt.value
+
+
+def sancov(cov_vals, cov_off, ctx=None):
+    """tools/syz-execprog/execprog.go:159-177 sancov files of a batch of calls (list of bytes)."""
+    cv, co = _u32(cov_vals), _u64(cov_off)
+    n = co.size - 1
+    out = np.empty(max(8 * (n + cv.size), 1), dtype=np.uint8)
+    call("sg_sancov_batch", _ctx(ctx).h, _p32(cv), _p64(co), n, _p8(out))
+    return [out[8 * (k + int(co[k])): 8 * (k + 1 + int(co[k + 1]))].tobytes() for k in range(n)]
 
 
 def canonicalize_batch(vals, off, ctx=None):

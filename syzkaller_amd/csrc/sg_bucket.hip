@@ -51,8 +51,16 @@ constexpr int kPThreads = 1024;              // 16 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
-// Entry layouts.  Pass 1: s << 8 | record-in-tile (kRecCap records per tile
-// at most).  Pass 2: (s & 0xFFFF) << 16 | record-in-group.
+// Partition key.  The passes and buckets work on t = key(s), the bytes of
+// s = (b3 b2 b1 b0) reordered as (b2 b1 b3 b0): pass 1 partitions by b2, pass
+// 2 by b1, and a bucket holds the 2^16 signals of one (b2, b1).  The raw top
+// byte of an edge signal is the top byte of hash(prev PC) (pc's own top byte
+// is the kernel-text base, executor.h:393-395), so it concentrates the edges
+// of the hottest PCs in a few slices; bits 8..23 mix both PCs and spread
+// evenly.  A bucket's maxSignal words are 256 runs of 8 words (one run per
+// b3, bucket_word), its LDS slice bit for t is t & 0xFFFF = b3 << 8 | b0.
+// Entry layouts.  Pass 1: t << 8 | record-in-tile (kRecCap records per tile
+// at most).  Pass 2: (t & 0xFFFF) << 16 | record-in-group.
 constexpr uint32_t kRecCap = 256;              // records per pass-1 tile
 constexpr uint32_t kGroupBits = 16;
 constexpr uint32_t kGroupRecs = 1u << kGroupBits;  // records per group
@@ -62,9 +70,21 @@ constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
 constexpr int kBThreads = 512;
 constexpr int kBU = 8;                       // entries per thread per round in the bucket kernel
-constexpr uint32_t kHash = 4096;             // candidate map slots per bucket
-constexpr uint32_t kMaxProbe = 64;           // linear-probe cap before a bucket spills
+constexpr uint32_t kHash = 8192;             // candidate map slots per bucket (32 bits each, see map_insert)
+constexpr uint32_t kMaxProbe = 31;           // linear-probe cap before a bucket spills
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+__host__ __device__ __forceinline__ uint32_t part_key(uint32_t s) {  // (b3 b2 b1 b0) -> (b2 b1 b3 b0)
+  return ((s & 0x00FFFF00u) << 8) | ((s >> 16) & 0xFF00u) | (s & 0xFFu);
+}
+__host__ __device__ __forceinline__ uint32_t part_sig(uint32_t t) {  // inverse of part_key
+  return ((t & 0xFF00u) << 16) | ((t >> 8) & 0x00FFFF00u) | (t & 0xFFu);
+}
+__host__ __device__ __forceinline__ uint32_t p1_digit(uint32_t s) { return (s >> 16) & 0xFFu; }  // part_key(s) >> 24
+// maxSignal word holding bucket b's LDS slice word j (= b3 * 8 + b0 / 32)
+__host__ __device__ __forceinline__ uint64_t bucket_word(uint32_t b, uint32_t j) {
+  return ((uint64_t)(j >> 3) << 19) | ((uint64_t)b << 3) | (j & 7u);
+}
 
 // Blocks sharing an XCD (bid % 8 under round-robin dispatch) get a contiguous
 // run of tiles, so partial lines at the seams of neighbouring tiles' digit
@@ -237,7 +257,7 @@ __global__ __launch_bounds__(kPThreads) void k_p1_hist(const uint32_t* __restric
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPT / kPThreads; k++)
-    if (s0 + k * kPThreads + tid < s1) atomicAdd(&cnt[x[k] >> 24], 1u);
+    if (s0 + k * kPThreads + tid < s1) atomicAdd(&cnt[p1_digit(x[k])], 1u);
   __syncthreads();
   if (tid < 256) hist[(uint64_t)tid * ncols + t] = cnt[tid];
 }
@@ -290,6 +310,10 @@ __device__ __forceinline__ void hist_load(const uint32_t* __restrict__ v, const 
 // a half-wave always hit 32 distinct banks (a shared 256-counter table sees
 // ~3.5-way conflicts per half-wave on random digits).  The copies are summed
 // per digit at the end, each lane starting at a different copy.
+// digit of an input value: pass 1 reads signals (p1_digit), pass 2 pass-1 entries (top byte)
+template <bool kP2>
+__device__ __forceinline__ uint32_t hist_digit(uint32_t x) { return kP2 ? x >> 24 : p1_digit(x); }
+
 template <bool kP2>
 __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restrict__ v,
                                                         const uint32_t* __restrict__ start,
@@ -321,12 +345,12 @@ __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restri
 #pragma unroll
   for (int k = 0; k <= kHistQ; k++)
     if (q0 + k * kPThreads + tid < q1) {
-      atomicAdd(&rc[(r.x[k].x >> 24) * 32 + cp], 1u);
-      atomicAdd(&rc[(r.x[k].y >> 24) * 32 + cp], 1u);
-      atomicAdd(&rc[(r.x[k].z >> 24) * 32 + cp], 1u);
-      atomicAdd(&rc[(r.x[k].w >> 24) * 32 + cp], 1u);
+      atomicAdd(&rc[hist_digit<kP2>(r.x[k].x) * 32 + cp], 1u);
+      atomicAdd(&rc[hist_digit<kP2>(r.x[k].y) * 32 + cp], 1u);
+      atomicAdd(&rc[hist_digit<kP2>(r.x[k].z) * 32 + cp], 1u);
+      atomicAdd(&rc[hist_digit<kP2>(r.x[k].w) * 32 + cp], 1u);
     }
-  if (hist_edge(h, tid) != 0xFFFFFFFFu) atomicAdd(&rc[(r.y >> 24) * 32 + cp], 1u);
+  if (hist_edge(h, tid) != 0xFFFFFFFFu) atomicAdd(&rc[hist_digit<kP2>(r.y) * 32 + cp], 1u);
   __syncthreads();
   if (tid < 256) {
     uint32_t sum = 0;
@@ -516,8 +540,8 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // record in tile
-    dv[k] = sv[k] >> 24;
-    pk[k] = (sv[k] << 8) | r;
+    dv[k] = p1_digit(sv[k]);
+    pk[k] = (part_key(sv[k]) << 8) | r;
   }
   stamp(1);
   uint32_t pos[kSteps];
@@ -718,13 +742,12 @@ __global__ void k_bucket_groups(const uint32_t* __restrict__ goff2, const uint32
 
 __device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
                                                const uint32_t* nbits, int tid, int nthreads) {
-  uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
-  uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords : nullptr;
   for (uint32_t i = tid; i < kBucketWords; i += nthreads) {
     const uint32_t nb = nbits[i];
     if (nb) {
-      mg[i] = mslice[i] | nb;
-      if (ng) ng[i] |= nb;
+      const uint64_t w = bucket_word(b, i);
+      a.mwords[w] = mslice[i] | nb;
+      if (a.nwords) a.nwords[w] |= nb;
     }
   }
 }
@@ -784,12 +807,14 @@ __device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t 
 
 __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, BucketPre& P) {
   static_assert(kBucketWords / kBThreads == 4, "one uint4 of the slice per thread");
-  const uint4 m = reinterpret_cast<const uint4*>(a.mwords + (uint64_t)b * kBucketWords)[threadIdx.x];
+  // LDS slice words 4 tid .. +3: one 16-B half of b3 = tid / 2's run of 8
+  const uint64_t w0 = bucket_word(b, 4 * threadIdx.x);
+  const uint4 m = *reinterpret_cast<const uint4*>(a.mwords + w0);
   P.msw[0] = m.x;
   P.msw[1] = m.y;
   P.msw[2] = m.z;
   P.msw[3] = m.w;
-  const uint4 nw = a.nwords ? reinterpret_cast<const uint4*>(a.nwords + (uint64_t)b * kBucketWords)[threadIdx.x]
+  const uint4 nw = a.nwords ? *reinterpret_cast<const uint4*>(a.nwords + w0)
                             : make_uint4(0, 0, 0, 0);
   P.nsw[0] = nw.x;
   P.nsw[1] = nw.y;
@@ -810,30 +835,51 @@ __device__ __forceinline__ uint32_t list_bucket(const BucketArgs& a, uint32_t t,
   return a.blist_b[t];
 }
 
-constexpr unsigned long long kEmpty64 = ~0ull;
-
 // block-uniform values read from LDS: keep them in scalar registers
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint4 uni(uint4 v) { return make_uint4(uni(v.x), uni(v.y), uni(v.z), uni(v.w)); }
 
-__device__ __forceinline__ uint32_t slot_of(uint32_t sl) { return (sl * 2654435761u) >> 20; }  // 12 bits
+// The candidate map: kHash = 8192 slots of 32 bits, linear probing.  The
+// bucket's 16-bit signal sl goes through a bijection y = sl * kMapMul (mod
+// 2^16): home slot = y >> 3, tag = y & 7.  A slot holds
+//   tag << 29 | displacement << 24 | record        (record < 2^24 = kMaxGroups << 16)
+// so the slot index and its top byte give back sl, and one 32-bit atomicMin
+// lowers the record of an equal key.  Displacements stay <= kMaxProbe - 1 =
+// 30, so no entry equals kEmpty (displacement field 31).
+constexpr uint32_t kMapMul = 0x6F4Bu;  // odd: invertible mod 2^16
+constexpr uint32_t inv16(uint32_t c) {
+  uint32_t x = c;  // Newton: each step doubles the correct low bits (c * c == 1 mod 8 for odd c)
+  for (int i = 0; i < 4; i++) x = (x * (2u - c * x)) & 0xFFFFu;
+  return x;
+}
+constexpr uint32_t kMapInv = inv16(kMapMul);
+static_assert(((kMapMul * kMapInv) & 0xFFFFu) == 1u, "kMapInv");
+static_assert(kHash == 8192 && kMaxProbe <= 31, "13-bit slots, 5-bit displacements");
+static_assert((uint64_t)kMaxGroups << kGroupBits <= (1u << 24), "records fit 24 bits");
+constexpr uint32_t kRecMask = 0xFFFFFFu;
 
-// Map slot = signal (high word) | record (low word).  A first insert is one
-// CAS; a repeat of a signal lowers the record with a u64 min (equal high words).
-__device__ __forceinline__ bool hash_insert64(unsigned long long* ht, uint32_t* nbits, uint32_t sl, uint32_t rec) {
-  const unsigned long long mine = ((unsigned long long)sl << 32) | rec;
-  uint32_t h = slot_of(sl);
-  for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
-    const unsigned long long old = atomicCAS(&ht[h], kEmpty64, mine);
-    if (old == kEmpty64) {
+__device__ __forceinline__ uint32_t map_signal(uint32_t slot, uint32_t v) {  // sl of an occupied slot
+  const uint32_t home = (slot - ((v >> 24) & 31u)) & (kHash - 1);
+  return (((home << 3) | (v >> 29)) * kMapInv) & 0xFFFFu;
+}
+
+// A first insert is one CAS; a repeat of a signal lowers the record with a
+// 32-bit min (equal key bits above the record).
+__device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t* nbits, uint32_t sl, uint32_t rec) {
+  const uint32_t y = (sl * kMapMul) & 0xFFFFu;
+  const uint32_t home = y >> 3, tag = y & 7u;
+  for (uint32_t disp = 0; disp < kMaxProbe; disp++) {
+    const uint32_t mine = (tag << 29) | (disp << 24) | rec;
+    uint32_t* slot = &ht[(home + disp) & (kHash - 1)];
+    const uint32_t old = atomicCAS(slot, kEmpty, mine);
+    if (old == kEmpty) {
       atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
       return true;
     }
-    if ((uint32_t)(old >> 32) == sl) {
-      if ((uint32_t)old > rec) atomicMin(&ht[h], mine);
+    if ((old >> 24) == (mine >> 24)) {
+      if ((old & kRecMask) > rec) atomicMin(slot, mine);
       return true;
     }
-    h = (h + 1) & (kHash - 1);
   }
   return false;  // map (nearly) full: the bucket spills
 }
@@ -842,7 +888,7 @@ template <bool kDbg, bool kEmit>
 __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  __shared__ unsigned long long ht[kHash];
+  __shared__ uint32_t ht[kHash];
   __shared__ alignas(16) uint32_t gb[kMaxGroups];  // the bucket's group boundaries (kEmpty past NG)
   __shared__ uint32_t sh_fail;         // some insert found the map full: the bucket spills
   __shared__ uint32_t sh_b[2];
@@ -858,7 +904,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
   uint64_t n_buckets = 0, n_rounds = 0;
   uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};  // install, rounds, -, flush | rounds: test, inserts, -
   uint64_t tk = kDbg ? clock64() : 0;
-  for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
+  for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty;
   for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
   if (tid == 0) sh_fail = 0;
   // list entries: blockIdx and gridDim + blockIdx first, then tickets from
@@ -960,7 +1006,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
             g++;
             nb = g + 1 < NG ? gb[g + 1] : kEmpty;
           }
-          if (!hash_insert64(ht, nbits, xu >> 16, entry_record(g, xu))) {
+          if (!map_insert(ht, nbits, xu >> 16, entry_record(g, xu))) {
             ok = false;
             // the others stop inserting (the bucket is redone)
             __hip_atomic_store(&sh_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -992,57 +1038,68 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         a.spill[atomicAdd(a.nspill, 1u)] = b;
         sh_fail = 0;
       }
-      for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty64;
+      for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
     } else if (kEmit) {
       // every distinct candidate of the bucket with its first record
-      uint32_t sig[kHash / kBThreads], rec[kHash / kBThreads];
+      constexpr int kPer = kHash / kBThreads / 2;
 #pragma unroll
-      for (int k = 0; k < (int)(kHash / kBThreads); k++) {
-        const uint32_t i = k * kBThreads + tid;
-        const unsigned long long v = ht[i];
-        sig[k] = (b << 16) | (uint32_t)(v >> 32);
-        rec[k] = v != kEmpty64 ? (uint32_t)v : kEmpty;
-        ht[i] = kEmpty64;
+      for (int half = 0; half < 2; half++) {
+        uint32_t sig[kPer], rec[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+          const uint32_t i = (half * kPer + k) * kBThreads + tid;
+          const uint32_t v = ht[i];
+          sig[k] = part_sig((b << 16) | map_signal(i, v));
+          rec[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
+          ht[i] = kEmpty;
+        }
+        emit_pairs(a, sig, rec, shcnt);
       }
-      emit_pairs(a, sig, rec, shcnt);
       reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
     } else {
       // a record is queued iff it owns some signal (fuzzer.go:678-690).  A
       // record owns signals in many buckets: its flag is read first and
       // written only while still clear, so its line is not dirtied (and
       // written back) once per bucket
-      uint32_t own[kHash / kBThreads];
-      uint8_t seen[kHash / kBThreads];
+      constexpr int kOwn = kHash / kBThreads / 2;  // slots per thread, in two halves
+      uint32_t own[kOwn];
+      uint8_t seen[kOwn];
 #pragma unroll
-      for (int k = 0; k < (int)(kHash / kBThreads); k++) {
-        const uint32_t i = k * kBThreads + tid;
-        const unsigned long long v = ht[i];
-        own[k] = v != kEmpty64 ? (uint32_t)v : kEmpty;
-        ht[i] = kEmpty64;
-      }
+      for (int half = 0; half < 2; half++) {
 #pragma unroll
-      for (int k = 0; k < (int)(kHash / kBThreads); k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
-      // (the flag reads are in flight while the slice's words go out)
-      // words 4 tid .. +3: this block is their only writer
-      uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords + 4 * tid;
-      uint32_t* ng = a.nwords ? a.nwords + (uint64_t)b * kBucketWords + 4 * tid : nullptr;
-      const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
-      if (nb4.x | nb4.y | nb4.z | nb4.w) {
-        const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
-        const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
-        const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
+        for (int k = 0; k < kOwn; k++) {
+          const uint32_t i = (half * kOwn + k) * kBThreads + tid;
+          const uint32_t v = ht[i];
+          own[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
+          ht[i] = kEmpty;
+        }
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (nb[j]) {
-            mg[j] = mw[j] | nb[j];
-            if (ng) ng[j] = nw[j] | nb[j];
+        for (int k = 0; k < kOwn; k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
+        if (half == 0) {
+          // (the first half's flag reads are in flight while the slice's words go out)
+          // words 4 tid .. +3: this block is their only writer
+          const uint64_t w0 = bucket_word(b, 4 * tid);
+          uint32_t* mg = a.mwords + w0;
+          uint32_t* ng = a.nwords ? a.nwords + w0 : nullptr;
+          const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
+          if (nb4.x | nb4.y | nb4.z | nb4.w) {
+            const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
+            const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
+            const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (nb[j]) {
+                mg[j] = mw[j] | nb[j];
+                if (ng) ng[j] = nw[j] | nb[j];
+              }
+            reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
           }
-        reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
-      }
+        }
 #pragma unroll
-      for (int k = 0; k < (int)(kHash / kBThreads); k++)
-        if (!seen[k]) a.rec_new[own[k]] = 1;
+        for (int k = 0; k < kOwn; k++)
+          if (!seen[k]) a.rec_new[own[k]] = 1;
+      }
     }
     __syncthreads();  // sh_b[0] / sh_q[0] are written
     if (kDbg) {
@@ -1091,9 +1148,8 @@ __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
   for (uint32_t j = blockIdx.x; j < nsp; j += gridDim.x) {
     const uint32_t b = a.spill[j];
     const uint4 q = a.bdesc[b];
-    const uint32_t* mg = a.mwords + (uint64_t)b * kBucketWords;
     for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
-      mslice[i] = mg[i];
+      mslice[i] = a.mwords[bucket_word(b, i)];
       nbits[i] = 0;
     }
     for (uint32_t i = tid; i < NG; i += kBThreads) gb[i] = a.gbnd[(uint64_t)b * NG + i];
@@ -1114,7 +1170,7 @@ __global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
           const uint32_t i = k * kBThreads + tid;
-          sig[k] = (b << 16) | (qq * kQ + i);
+          sig[k] = part_sig((b << 16) | (qq * kQ + i));
           rec[k] = owner[i];
         }
         emit_pairs(a, sig, rec, shcnt);

@@ -641,6 +641,37 @@ int sg_set_count(sg_set* set, uint64_t* out) {
   return set_tile_bases(set, &bases, out);
 }
 
+}  // extern "C"
+
+namespace sg {
+// The members of `set`, ascending, into device memory d_out (capacity cap);
+// *total = count (ctx lock held; syncs).
+int set_export_dev(sg_set* set, uint32_t* d_out, uint64_t cap, uint64_t* total) {
+  sg_ctx* ctx = set->ctx;
+  uint64_t* bases;
+  int rc = set_tile_bases(set, &bases, total);
+  if (rc) return rc;
+  const uint64_t m = *total < cap ? *total : cap;
+  if (m == 0) return SG_OK;
+  hipLaunchKernelGGL(k_set_export, dim3((uint32_t)(kSetWords / kTile)), dim3(kBlock), 0, ctx->stream, set->words,
+                     bases, d_out, m);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+// SignalAdd of n device-resident values (ctx lock held, stream-ordered).
+int set_add_dev_locked(sg_set* set, const uint32_t* d_vals, uint64_t n) {
+  if (n == 0) return SG_OK;
+  ScopedTimer tm(set->ctx, "set_add");
+  hipLaunchKernelGGL(k_set_add, dim3(std::min<uint64_t>(div_up(n, 256), 8192)), dim3(256), 0, set->ctx->stream,
+                     set->words, d_vals, n);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+}  // namespace sg
+
+extern "C" {
+
 int sg_set_export(sg_set* set, uint32_t* out, size_t cap, size_t* n) {
   if (!set || !n || (cap && !out)) return SG_EINVAL;
   sg_ctx* ctx = set->ctx;

@@ -32,14 +32,37 @@ __device__ __forceinline__ uint32_t exec_hash(uint32_t a) {  // executor.h:497-5
   return a;
 }
 
+// The speculative pass, per edge j of the batch (lanes start..nvalid-1), all
+// deciding against the table as it stands:
+//   decision slot d_j: the slot holding sig (dup), the first empty slot
+//   (insert), or sig % 8192 (overwrite, all four taken); writers = inserts
+//   and overwrites, each writing d_j.
+// A write by an earlier edge i changes edge j's outcome only if it lands on
+// d_j: the window slots before d_j are taken and stay taken (an insert only
+// fills an empty slot, an overwrite keeps a slot taken), and the slots after
+// d_j are not looked at (or, for an overwrite, stay taken).  An earlier writer
+// with the same sig always writes d_j too (same window, same table).  So with
+// m = the first earlier writer on d_j:
+//   sig_m == sig_j  -> edge j is a duplicate (sequentially it finds sig at d_j)
+//   sig_m != sig_j  -> edge j is undecided (it decides again next pass).
+// Any later writer on d_j with another sig is itself undecided, so it cannot
+// commit before j.  The first writer per slot is found with an LDS atomicMin
+// of lane ids into kMarkSize marks indexed by d & (kMarkSize-1); a mark whose
+// lane wrote a different slot (aliasing) makes the lane undecided too.  The
+// decided prefix commits (its writers hit distinct slots); each pass commits
+// at least one edge.
+constexpr uint32_t kMarkSize = 2048;  // 8 KiB: table + marks = 40 KiB, 4 programs per CU
+
 __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__ pcs,
                                                     const uint64_t* __restrict__ call_off,
                                                     const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
                                                     uint32_t* __restrict__ cnt) {
   __shared__ uint32_t table[kDedupSize];
+  __shared__ uint32_t mark[kMarkSize];
   const int lane = threadIdx.x;
   const uint64_t p = blockIdx.x;
   for (uint32_t i = lane; i < kDedupSize; i += 64) table[i] = 0;
+  for (uint32_t i = lane; i < kMarkSize; i += 64) mark[i] = 64u;
   __syncthreads();
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const uint64_t c0 = prog_off[p], c1 = prog_off[p + 1];
@@ -62,13 +85,7 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
       const uint32_t sig = pc ^ hprev;  // executor.h:393-395
       const int nvalid = (int)((e - j) < 64 ? (e - j) : 64);
       carry = __shfl(h, nvalid - 1);
-      // The 64 edges' dedup decisions, speculatively in parallel: every
-      // lane from `start` decides against the table as it stands (its four
-      // probe slots), and the decisions stand up to the first lane whose
-      // probe window holds a slot that an earlier undecided lane writes.
-      // Those are committed (their writes hit distinct slots); the rest
-      // decide again.  Each pass commits at least one edge; a pass usually
-      // commits a few dozen (8192 slots, 4-slot windows).
+      // The 64 edges' dedup decisions, speculatively in parallel (see above).
       uint64_t keep = 0;
       for (int start = 0; start < nvalid;) {
         const bool act = lane >= start && lane < nvalid;
@@ -78,27 +95,46 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
         // executor.h:509-525: probe (s+q) % 8192 for q = 0..3 in order; a
         // slot equal to s means duplicate, an empty slot takes s, and when
         // all four are taken slot s % 8192 is overwritten.
-        int q = 4;
+        uint32_t q = 0;
         bool dup = false;
 #pragma unroll
         for (int k = 3; k >= 0; k--)
           if (t[k] == sig || t[k] == 0u) {
-            q = k;
+            q = (uint32_t)k;
             dup = t[k] == sig;
           }
-        const uint32_t w = !act || dup ? 0xFFFFFFFFu : ((sig + (uint32_t)(q < 4 ? q : 0)) & (kDedupSize - 1));
-        // only the pass's writers can dirty a later edge: walk them (most
-        // edges of a trace are repeats, so writers are few)
-        bool dirty = false;
-        for (uint64_t wm = __ballot(w != 0xFFFFFFFFu); wm; wm &= wm - 1) {
-          const int i = __ffsll((unsigned long long)wm) - 1;
-          const uint32_t wi = __builtin_amdgcn_readlane(w, i);
-          dirty |= lane > i && ((wi - sig) & (kDedupSize - 1)) < 4u;
+        const uint32_t d = (sig + q) & (kDedupSize - 1);
+        const bool wr = act && !dup;
+        const uint64_t wm = __ballot(wr);
+        int f = nvalid;
+        bool bdup = false;
+        if (wm) {
+          bool earlier;
+          if (!(wm & (wm - 1))) {  // one writer: compare against it directly
+            const int i = __ffsll((unsigned long long)wm) - 1;
+            const uint32_t di = __builtin_amdgcn_readlane(d, i), si = __builtin_amdgcn_readlane(sig, i);
+            earlier = act && lane > i && d == di;
+            bdup = earlier && sig == si;
+          } else {  // each lane's first earlier writer on its slot, through the marks
+            if (wr)
+              __hip_atomic_fetch_min(&mark[d & (kMarkSize - 1)], (uint32_t)lane, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t m = act ? mark[d & (kMarkSize - 1)] : 64u;
+            const int src = m < 64u ? (int)m : lane;
+            const uint32_t dm = __shfl(d, src), sm = __shfl(sig, src);
+            earlier = act && m < (uint32_t)lane;
+            bdup = earlier && dm == d && sm == sig;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (wr) mark[d & (kMarkSize - 1)] = 64u;
+          }
+          const uint64_t um = __ballot(earlier && !bdup);
+          f = um ? __ffsll((unsigned long long)um) - 1 : nvalid;
         }
-        const uint64_t dm = __ballot(act && dirty);
-        const int f = dm ? __ffsll((unsigned long long)dm) - 1 : nvalid;
-        const bool commit = lane >= start && lane < f && !dup;
-        if (commit) table[w] = sig;
+        const bool commit = wr && !bdup && lane < f;
+        if (commit) table[d] = sig;
         keep |= __ballot(commit);
         start = f;
       }

@@ -146,6 +146,11 @@ inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) /
 int scan_counts(sg_ctx* ctx, const uint32_t* d_in, uint64_t* d_out, uint64_t n, size_t ws_used);
 size_t scan_ws_bytes(uint64_t n);
 
+// Members of a set, ascending, into device memory (sg_ctx.hip; ctx lock held).
+int set_export_dev(sg_set* set, uint32_t* d_out, uint64_t cap, uint64_t* total);
+// SignalAdd of device-resident values (sg_ctx.hip; ctx lock held, stream-ordered).
+int set_add_dev_locked(sg_set* set, const uint32_t* d_vals, uint64_t n);
+
 // Shared first-owner pipeline (sg_triage.hip).
 struct OwnerJob {
   const uint32_t* vals;   // device

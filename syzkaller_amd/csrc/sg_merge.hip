@@ -534,7 +534,7 @@ __global__ void k_unique_write(CanonArgs a) {
 }
 
 // ---- host orchestration ----------------------------------------------------------
-static int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg, uint64_t* out_len) {
+int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg, uint64_t* out_len) {
   // off: host offsets (nseg+1); d_vals: device values (sorted+uniqued in place)
   uint64_t n = off[nseg];
   std::vector<SortChunk> chunks;

@@ -1,0 +1,405 @@
+// sg_rpc.hip -- RPC payload forms of signal and cover.
+//
+// Reference: pkg/rpctype/rpctype.go:8-63.  The fuzzer and the manager ship
+// signal as []uint32 (gob: a varint per element, up to 5 bytes each for
+// 32-bit edge signal): RpcInput.Signal / .Cover (canonical, ascending),
+// ConnectRes.MaxSignal, PollArgs.MaxSignal (the fuzzer's drained newSignal,
+// fuzzer.go:358-364) and PollRes.MaxSignal (manager.go:949-962).
+//
+// Wire form here: each sorted list as Go's binary.PutUvarint of its first
+// value, then of each successive difference (LEB128: 7 bits per byte, high
+// bit = more bytes follow).  A Go peer decodes it with binary.Uvarint and a
+// running sum.  Encoding and decoding run on the GPU straight from / into a
+// signal set's bitmap:
+//   encode  lengths of the deltas' varints -> exclusive scan -> byte writes;
+//   decode  a byte ends a value iff its high bit is clear; the terminators'
+//           scan numbers the values, each terminator decodes its (<= 5-byte)
+//           run, and a scan of the deltas restores the values.
+// The sancov dump of tools/syz-execprog/execprog.go:159-177 (magic
+// 0xC0BFFFFFFFFFFF64, then RestorePC(pc, 0xffffffff) per cover PC, all u64
+// little-endian) is the interchange form for offline cover tooling.
+#include "sg_internal.h"
+
+#include <algorithm>
+
+namespace sg {
+namespace {
+
+constexpr uint64_t kSancovMagic = 0xC0BFFFFFFFFFFF64ull;  // execprog.go:166
+
+__device__ __forceinline__ uint32_t varint_len(uint32_t d) {
+  return d < (1u << 7) ? 1u : d < (1u << 14) ? 2u : d < (1u << 21) ? 3u : d < (1u << 28) ? 4u : 5u;
+}
+
+// list k of the CSR holding global element i (off non-decreasing, off[0] = 0)
+__device__ __forceinline__ uint64_t list_of(const uint64_t* off, uint64_t n, uint64_t i) {
+  uint64_t lo = 0, hi = n - 1;  // last k with off[k] <= i
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+// delta of element i within its list (the first one: itself); err on a descent
+__device__ __forceinline__ uint32_t elem_delta(const uint32_t* v, const uint64_t* off, uint64_t n, uint64_t i,
+                                               uint32_t* err) {
+  const uint64_t k = list_of(off, n, i);
+  const uint32_t x = v[i];
+  if (i == off[k]) return x;
+  const uint32_t p = v[i - 1];
+  if (x < p) *err = 1;
+  return x - p;
+}
+
+__global__ void k_enc_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
+                          uint32_t* __restrict__ len, uint32_t* __restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride)
+    len[i] = varint_len(elem_delta(v, off, n, i, err));
+}
+
+__global__ void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
+                            const uint64_t* __restrict__ pos, uint8_t* __restrict__ out, uint32_t* __restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+    uint32_t d = elem_delta(v, off, n, i, err);
+    uint8_t* o = out + pos[i];
+    while (d >= 0x80u) {  // binary.PutUvarint
+      *o++ = (uint8_t)(d | 0x80u);
+      d >>= 7;
+    }
+    *o = (uint8_t)d;
+  }
+}
+
+// byte offsets of the lists: out_off[k] = pos[off[k]]
+__global__ void k_list_pos(const uint64_t* __restrict__ off, uint64_t n, const uint64_t* __restrict__ pos,
+                           uint64_t* __restrict__ out_off) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k <= n) out_off[k] = pos[off[k]];
+}
+
+__global__ void k_dec_term(const uint8_t* __restrict__ in, uint64_t nb, uint32_t* __restrict__ term) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride)
+    term[j] = (in[j] & 0x80u) ? 0u : 1u;
+}
+
+// Each terminator decodes its run (back to the previous terminator or the
+// list's first byte); a run must be <= 5 bytes and fit 32 bits, and a list
+// must end on a terminator.
+__global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n, uint64_t nb,
+                           const uint64_t* __restrict__ vidx, uint32_t* __restrict__ delta, uint32_t* __restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
+    const uint64_t k = list_of(in_off, n, j);
+    const uint64_t b = in_off[k];
+    const uint8_t c = in[j];
+    if (c & 0x80u) {
+      if (j + 1 == in_off[k + 1]) *err = 1;  // the list ends inside a value
+      continue;
+    }
+    uint64_t s = j;
+    while (s > b && (in[s - 1] & 0x80u)) {
+      s--;
+      if (j - s >= 5) break;
+    }
+    if (j - s >= 5 || (j - s == 4 && c > 0x0Fu)) {  // more than 32 bits
+      *err = 1;
+      continue;
+    }
+    uint32_t d = 0;
+    for (uint64_t q = s; q <= j; q++) d |= (uint32_t)(in[q] & 0x7Fu) << (7 * (q - s));
+    delta[vidx[j]] = d;
+  }
+}
+
+// values of each list: running sums of its deltas (u64 scan), range-checked
+__global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t* __restrict__ excl,
+                             const uint64_t* __restrict__ voff, uint64_t n, uint64_t N, uint32_t* __restrict__ out,
+                             uint32_t* __restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+    const uint64_t k = list_of(voff, n, i);
+    const uint64_t v = excl[i] + delta[i] - excl[voff[k]];
+    if (v > 0xFFFFFFFFull) *err = 1;
+    out[i] = (uint32_t)v;
+  }
+}
+
+__global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
+                         uint64_t* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N + n; i += stride) {
+    if (i < n) {
+      out[i + off[i]] = kSancovMagic;  // file i's header (execprog.go:166)
+    } else {
+      const uint64_t e = i - n, k = list_of(off, n, e);
+      out[k + 1 + e] = (0xFFFFFFFFull << 32) + cov[e];  // RestorePC(pc, 0xffffffff), cover.go:23-25
+    }
+  }
+}
+
+inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::min<uint64_t>(div_up(n ? n : 1, 256), 16384); }
+
+bool offsets_ok(const uint64_t* off, size_t n) {
+  if (off[0] != 0) return false;
+  for (size_t k = 0; k < n; k++)
+    if (off[k + 1] < off[k]) return false;
+  return true;
+}
+
+// Encode the n lists at device d_v / d_off (N = elements) into device bytes;
+// h_out_off (host, n+1) gets the byte offsets.  dstage holds d_v / d_off; the
+// scratch and output live in ws from `base`.  Returns the byte buffer.
+int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t n, uint64_t N, uint64_t* h_out_off,
+               uint8_t** d_bytes) {
+  WsPlan p;
+  const size_t o_len = p.add(N * 4), o_pos = p.add((N + 1) * 8), o_lo = p.add((n + 1) * 8), o_err = p.add(8),
+               o_out = p.add(N * 5 + 8);
+  const size_t scan_off = p.total;
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(N));
+  if (rc) return rc;
+  uint32_t* len = (uint32_t*)ws_at(ctx, o_len);
+  uint64_t* pos = (uint64_t*)ws_at(ctx, o_pos);
+  uint64_t* lo = (uint64_t*)ws_at(ctx, o_lo);
+  uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
+  uint8_t* out = (uint8_t*)ws_at(ctx, o_out);
+  SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "rpc_encode");
+    if (N)
+      hipLaunchKernelGGL(k_enc_len, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, n, N, len, err);
+    rc = scan_counts(ctx, len, pos, N, scan_off);
+    if (rc) return rc;
+    if (N)
+      hipLaunchKernelGGL(k_enc_write, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, n, N, pos, out, err);
+    hipLaunchKernelGGL(k_list_pos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_off, n, pos, lo);
+  }
+  SG_HIP(hipGetLastError());
+  uint32_t herr = 0;
+  SG_HIP(hipMemcpyAsync(h_out_off, lo, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (herr) {
+    set_error("sg_delta_encode: a list is not sorted (non-decreasing)");
+    return SG_EINVAL;
+  }
+  *d_bytes = out;
+  return SG_OK;
+}
+
+// Decode n lists of device bytes d_in / d_in_off (nb bytes) into device values
+// (capacity cap); h_off (host, n+1) gets the value offsets.  Scratch in ws.
+int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n, uint64_t nb, uint32_t* d_vals,
+               uint64_t cap, uint64_t* h_off, uint64_t* d_voff) {
+  WsPlan p;
+  const size_t o_t = p.add(nb * 4), o_vi = p.add((nb + 1) * 8), o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8),
+               o_err = p.add(8);
+  const size_t scan_off = p.total;
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nb));
+  if (rc) return rc;
+  uint32_t* term = (uint32_t*)ws_at(ctx, o_t);
+  uint64_t* vidx = (uint64_t*)ws_at(ctx, o_vi);
+  uint32_t* delta = (uint32_t*)ws_at(ctx, o_d);
+  uint64_t* excl = (uint64_t*)ws_at(ctx, o_x);
+  uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
+  SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+  ScopedTimer tm(ctx, "rpc_decode");
+  if (nb) hipLaunchKernelGGL(k_dec_term, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, nb, term);
+  rc = scan_counts(ctx, term, vidx, nb, scan_off);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_list_pos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vidx, d_voff);
+  SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  const uint64_t N = h_off[n];
+  if (N > cap) {
+    set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
+    return SG_EINVAL;
+  }
+  if (nb) hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, d_in_off, n, nb, vidx,
+                             delta, err);
+  rc = scan_counts(ctx, delta, excl, N, scan_off);
+  if (rc) return rc;
+  if (N)
+    hipLaunchKernelGGL(k_dec_values, dim3(grid_for(N)), dim3(256), 0, ctx->stream, delta, excl, d_voff, n, N, d_vals,
+                       err);
+  SG_HIP(hipGetLastError());
+  uint32_t herr = 0;
+  SG_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (herr) {
+    set_error("sg_delta_decode: malformed payload (unterminated value, value over 32 bits, or sum over 32 bits)");
+    return SG_EINVAL;
+  }
+  return SG_OK;
+}
+
+}  // namespace
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_delta_encode_batch(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, uint8_t* out, size_t cap,
+                          uint64_t* out_off) {
+  if (!ctx || !off || !out_off || !offsets_ok(off, n) || (off[n] && !vals) || (cap && !out)) {
+    set_error("sg_delta_encode_batch: invalid argument");
+    return SG_EINVAL;
+  }
+  const uint64_t N = off[n];
+  if (n == 0 || N == 0) {
+    for (size_t k = 0; k <= n; k++) out_off[k] = 0;
+    return SG_OK;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  const size_t b_v = (N * 4 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_v + (n + 1) * 8);
+  if (rc) return rc;
+  uint32_t* dv = (uint32_t*)ctx->dstage;
+  uint64_t* doff = (uint64_t*)((char*)ctx->dstage + b_v);
+  SG_HIP(hipMemcpyAsync(dv, vals, N * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  uint8_t* bytes = nullptr;
+  rc = encode_dev(ctx, dv, doff, n, N, out_off, &bytes);
+  if (rc) return rc;
+  if (out_off[n] <= cap) {
+    SG_HIP(hipMemcpyAsync(out, bytes, out_off[n], hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return SG_OK;
+}
+
+int sg_delta_decode_batch(sg_ctx* ctx, const uint8_t* in, const uint64_t* in_off, size_t n, uint32_t* vals, size_t cap,
+                          uint64_t* off) {
+  if (!ctx || !in_off || !off || !offsets_ok(in_off, n) || (in_off[n] && !in) || (cap && !vals)) {
+    set_error("sg_delta_decode_batch: invalid argument");
+    return SG_EINVAL;
+  }
+  const uint64_t nb = in_off[n];
+  if (n == 0 || nb == 0) {
+    for (size_t k = 0; k <= n; k++) off[k] = 0;
+    return SG_OK;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  // every byte can end a value: nb values at most
+  const size_t b_b = (nb + 255) & ~size_t(255), b_o = ((n + 1) * 8 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_b + 2 * b_o + nb * 4 + 4);
+  if (rc) return rc;
+  uint8_t* din = (uint8_t*)ctx->dstage;
+  uint64_t* dio = (uint64_t*)((char*)ctx->dstage + b_b);
+  uint64_t* dvo = (uint64_t*)((char*)ctx->dstage + b_b + b_o);
+  uint32_t* dv = (uint32_t*)((char*)ctx->dstage + b_b + 2 * b_o);
+  SG_HIP(hipMemcpyAsync(din, in, nb, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dio, in_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  rc = decode_dev(ctx, din, dio, n, nb, dv, nb, off, dvo);
+  if (rc) return rc;
+  if (off[n] > cap) {
+    set_error("sg_delta_decode_batch: %llu values, capacity %zu", (unsigned long long)off[n], cap);
+    return SG_EINVAL;
+  }
+  if (off[n]) SG_HIP(hipMemcpyAsync(vals, dv, off[n] * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+int sg_set_encode(sg_set* set, uint8_t* out, size_t cap, size_t* nbytes) {
+  if (!set || !nbytes || (cap && !out)) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  uint64_t total = 0;
+  {  // count first: the members go to dstage
+    rc = set_export_dev(set, nullptr, 0, &total);
+    if (rc) return rc;
+  }
+  *nbytes = 0;
+  if (total == 0) return SG_OK;
+  const size_t b_v = (total * 4 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_v + 16);
+  if (rc) return rc;
+  uint32_t* dv = (uint32_t*)ctx->dstage;
+  uint64_t* doff = (uint64_t*)((char*)ctx->dstage + b_v);
+  rc = set_export_dev(set, dv, total, &total);
+  if (rc) return rc;
+  const uint64_t hoff[2] = {0, total};
+  SG_HIP(hipMemcpyAsync(doff, hoff, 16, hipMemcpyHostToDevice, ctx->stream));
+  uint64_t bo[2] = {0, 0};
+  uint8_t* bytes = nullptr;
+  rc = encode_dev(ctx, dv, doff, 1, total, bo, &bytes);
+  if (rc) return rc;
+  *nbytes = bo[1];
+  if (bo[1] <= cap) {
+    SG_HIP(hipMemcpyAsync(out, bytes, bo[1], hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return SG_OK;
+}
+
+int sg_set_decode_add(sg_set* set, const uint8_t* in, size_t nbytes, uint64_t* count) {
+  if (!set || (nbytes && !in)) return SG_EINVAL;
+  if (count) *count = 0;
+  if (nbytes == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  const size_t b_b = (nbytes + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_b + 512 + nbytes * 4 + 4);
+  if (rc) return rc;
+  uint8_t* din = (uint8_t*)ctx->dstage;
+  uint64_t* dio = (uint64_t*)((char*)ctx->dstage + b_b);
+  uint64_t* dvo = dio + 32;
+  uint32_t* dv = (uint32_t*)((char*)ctx->dstage + b_b + 512);
+  const uint64_t hio[2] = {0, nbytes};
+  SG_HIP(hipMemcpyAsync(din, in, nbytes, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dio, hio, 16, hipMemcpyHostToDevice, ctx->stream));
+  uint64_t hoff[2] = {0, 0};
+  rc = decode_dev(ctx, din, dio, 1, nbytes, dv, nbytes, hoff, dvo);
+  if (rc) return rc;
+  rc = set_add_dev_locked(set, dv, hoff[1]);  // fuzzer.go:392-398 / :146-151 (SignalAdd of the payload)
+  if (rc) return rc;
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (count) *count = hoff[1];
+  return SG_OK;
+}
+
+int sg_sancov_batch(sg_ctx* ctx, const uint32_t* cov, const uint64_t* cov_off, size_t n, uint8_t* out) {
+  if (!ctx || !cov_off || !offsets_ok(cov_off, n) || (cov_off[n] && !cov) || (n && !out)) {
+    set_error("sg_sancov_batch: invalid argument");
+    return SG_EINVAL;
+  }
+  if (n == 0) return SG_OK;
+  const uint64_t N = cov_off[n];
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  const size_t b_v = (N * 4 + 255) & ~size_t(255), b_o = ((n + 1) * 8 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_v + b_o + (N + n) * 8);
+  if (rc) return rc;
+  uint32_t* dv = (uint32_t*)ctx->dstage;
+  uint64_t* doff = (uint64_t*)((char*)ctx->dstage + b_v);
+  uint64_t* dout = (uint64_t*)((char*)ctx->dstage + b_v + b_o);
+  if (N) SG_HIP(hipMemcpyAsync(dv, cov, N * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(doff, cov_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "sancov");
+    hipLaunchKernelGGL(k_sancov, dim3(grid_for(N + n)), dim3(256), 0, ctx->stream, dv, doff, (uint64_t)n, N, dout);
+  }
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out, dout, (N + n) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""Full-size C2 parity (BASELINE.json configs[1]: 64Ki programs x 16 calls x
+1024 PCs): one whole batch through the product's device path
+(sg_triage_batch_dev, the partitioned kernels the bench times) against the
+oracle's sequential loop (oracle/sigoracle.c, restating
+syz-fuzzer/fuzzer.go:645-693) on the same batch, bit-exact in the per-record
+flags and in both sets afterwards.
+
+The batch is the fuzzer's steady state (bench.py "steady"): programs drawn
+from a fixed population with flaky coverage, against maxSignal = the
+population's signal, so the flags are mixed (the fresh-Zipf C2 batch flags
+every record: each one carries some never-seen edge)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+UNIVERSE_SEED = 0x5A17C0DE
+POP_SEED = 0x9091A7E5
+
+
+def _signal(call, ctx, trace, nprog, calls, pcs):
+    ncalls, npcs = nprog * calls, nprog * calls * pcs
+    call_off = torch.arange(0, npcs + 1, pcs, dtype=torch.int64, device="cuda")
+    prog_off = torch.arange(0, ncalls + 1, calls, dtype=torch.int64, device="cuda")
+    sig = torch.empty(npcs, dtype=torch.int32, device="cuda")
+    off = torch.empty(ncalls + 1, dtype=torch.int64, device="cuda")
+    call("sg_exec_signal_dev", ctx.h, trace.data_ptr(), call_off.data_ptr(), prog_off.data_ptr(), nprog, ncalls, npcs,
+         sig.data_ptr(), off.data_ptr())
+    torch.cuda.synchronize()
+    n = int(off[-1].item())
+    return sig[:n], off
+
+
+@pytest.mark.timeout(600)
+def test_c2_full_batch_steady_state_vs_oracle(ctx):
+    from syzkaller_amd._lib import call
+    from syzkaller_amd.cover import SignalSet
+
+    nprog, calls, pcs, npop = 65536, 16, 1024, 2048
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    trace = torch.empty(nprog * calls * pcs, dtype=torch.int32, device="cuda")
+    # maxSignal = every population member's signal
+    call("sg_gen_zipf_traces_dev", ctx.h, UNIVERSE_SEED, POP_SEED, 1.1, 1 << 20, 0, npop, calls, pcs, trace.data_ptr())
+    msig, moff = _signal(call, ctx, trace, npop, calls, pcs)
+    m0 = np.unique(msig.cpu().numpy().view(np.uint32))
+    # the batch: population programs re-executed with flaky coverage
+    call("sg_gen_population_traces_dev", ctx.h, UNIVERSE_SEED, POP_SEED, npop, 5_001, 2e-4, 1.1, 1 << 20, 0, nprog,
+         calls, pcs, trace.data_ptr())
+    sig, off = _signal(call, ctx, trace, nprog, calls, pcs)
+    del trace
+    nvals, nrec = sig.numel(), off.numel() - 1
+    assert nrec == nprog * calls and nvals > 800_000_000  # the C2 shape
+    ms, ns = SignalSet(ctx), SignalSet(ctx)
+    call("sg_set_add_dev", ms.h, torch.from_numpy(m0.view(np.int32)).cuda().data_ptr(), m0.size)
+    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
+         None, None)
+    torch.cuda.synchronize()
+    got = rec_new.cpu().numpy()
+    # the oracle's sequential loop over the same batch
+    om, on = O.OSet(m0), O.OSet()
+    exp = O.triage_flags_only(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
+    frac = float(exp.mean())
+    assert 0.05 < frac < 0.95, frac  # mixed flags: the attribution is really tested
+    assert np.array_equal(got, exp)
+    assert np.array_equal(ns.export(), on.export())
+    assert np.array_equal(ms.export(), om.export())
+    ns.close()
+    ms.close()
+    call("sg_ctx_reset_stream", ctx.h)

@@ -17,6 +17,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _batch(seed, nrec, hi=1 << 22, maxlen=60):
+    if nrec == 0:
+        return np.zeros(0, np.uint32), np.zeros(1, np.uint64)
     rng = np.random.default_rng(seed)
     lens = rng.integers(0, maxlen, size=nrec)
     lens[rng.integers(0, nrec, size=max(1, nrec // 5))] = 0
@@ -81,9 +83,11 @@ def test_shard_candidates_record_slices(C, monkeypatch):
                                    vals.size, off.size - 1, 0, 4, exp_pairs)
     got = pairs.cpu().numpy().view(np.uint32)[: 2 * so[-1]].reshape(-1, 2)
     exp = exp_pairs.numpy().view(np.uint32)[: 2 * eso[-1]].reshape(-1, 2)
-    u, first = np.unique(got[np.lexsort((got[:, 1], got[:, 0]))][:, 0], return_index=True)
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]  # the restatement's pairs are grouped by shard
     srt = got[np.lexsort((got[:, 1], got[:, 0]))]
+    u, first = np.unique(srt[:, 0], return_index=True)
     assert np.array_equal(srt[first], exp)
+    assert (shard_of(got[:, 0], 4) == np.repeat(np.arange(4), np.diff(so))).all()  # grouped by owning shard
     del snap
     ctx2.close()
 
