@@ -95,7 +95,11 @@ int sg_set_new(sg_set* set, const uint32_t* sig, size_t n, int* out);
 /* pkg/cover/cover.go:169-176  SignalDiff(base, signal): members of sig not in
  * base, in order, duplicates kept.  out capacity n; *nout = count. */
 int sg_set_diff(sg_set* set, const uint32_t* sig, size_t n, uint32_t* out, size_t* nout);
-/* Device bitmap (2^27 uint32 words) for collectives (OR-reduce across ranks). */
+/* Device bitmap (2^27 uint32 words) for collectives (OR-reduce across ranks).
+ * Layout: signal s = bytes (b3 b2 b1 b0) is bit p = (b2 b1 b3 b0) (bit p & 31
+ * of word p >> 5), a fixed permutation of whole words that keeps each (b2, b1)
+ * block of 2^16 signals contiguous (the triage's buckets).  Element-wise ops
+ * (OR, copy, count) do not depend on it. */
 void* sg_set_device_words(sg_set* set);
 /* Wrap caller-owned device memory (2^27 uint32 words, e.g. a torch tensor)
  * as a set without copying; sg_set_destroy then frees only the handle. */
@@ -236,6 +240,8 @@ int sg_set_decode_add(sg_set* set, const uint8_t* in, size_t nbytes, uint64_t* c
  * cover PC, little-endian.  File k is out[8*(k + cov_off[k]) .. 8*(k+1 +
  * cov_off[k+1])) (out: 8*(n + cov_off[n]) bytes). */
 int sg_sancov_batch(sg_ctx* ctx, const uint32_t* cov, const uint64_t* cov_off, size_t n, uint8_t* out);
+/* (execprog.go:162-164 writes no file for a call without cover: such a call's
+ * slice here is the 8-byte header alone.) */
 
 /* ---- sorted-slice algebra (pkg/cover/cover.go:28-117) ---------------------- */
 /* Canonicalize (cover.go:28-40): in place, *nout = canonical length. */

@@ -171,6 +171,59 @@ def triage_subset(new_vals, new_off, r_vals, r_off):
     return ((io[1:] - io[:-1]) == (_u64(new_off)[1:] - _u64(new_off)[:-1])).astype(np.uint8)
 
 
+def put_uvarint(x):
+    """Go encoding/binary PutUvarint (LEB128)."""
+    out = bytearray()
+    while x >= 0x80:
+        out.append((x & 0x7F) | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+def delta_encode(lst):
+    """The RPC payload of a sorted []uint32 (pkg/rpctype/rpctype.go:8-63 fields):
+    PutUvarint of the first value, then of each successive difference."""
+    out, prev = bytearray(), 0
+    for v in lst:
+        v = int(v)
+        assert v >= prev, "sorted input"
+        out += put_uvarint(v - prev)
+        prev = v
+    return bytes(out)
+
+
+def delta_decode(data):
+    """binary.Uvarint + running sum; ValueError on a malformed payload."""
+    vals, x, shift, prev = [], 0, 0, 0
+    for i, c in enumerate(data):
+        x |= (c & 0x7F) << shift
+        if c & 0x80:
+            shift += 7
+            if shift >= 35:
+                raise ValueError("value over 32 bits")
+            continue
+        if x > 0xFFFFFFFF:
+            raise ValueError("value over 32 bits")
+        prev += x
+        if prev > 0xFFFFFFFF:
+            raise ValueError("sum over 32 bits")
+        vals.append(prev)
+        x, shift = 0, 0
+    if shift:
+        raise ValueError("payload ends inside a value")
+    return vals
+
+
+def sancov(cov):
+    """tools/syz-execprog/execprog.go:165-168: u64 LE 0xC0BFFFFFFFFFFF64, then
+    cover.RestorePC(pc, 0xffffffff) (cover.go:23-25) per PC."""
+    import struct
+
+    return struct.pack("<Q", 0xC0BFFFFFFFFFFF64) + b"".join(struct.pack("<Q", (0xFFFFFFFF << 32) + int(pc))
+                                                           for pc in cov)
+
+
 def _csr(lists):
     off = np.zeros(len(lists) + 1, dtype=np.uint64)
     if lists:

@@ -51,14 +51,11 @@ constexpr int kPThreads = 1024;              // 16 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
-// Partition key.  The passes and buckets work on t = key(s), the bytes of
-// s = (b3 b2 b1 b0) reordered as (b2 b1 b3 b0): pass 1 partitions by b2, pass
-// 2 by b1, and a bucket holds the 2^16 signals of one (b2, b1).  The raw top
-// byte of an edge signal is the top byte of hash(prev PC) (pc's own top byte
-// is the kernel-text base, executor.h:393-395), so it concentrates the edges
-// of the hottest PCs in a few slices; bits 8..23 mix both PCs and spread
-// evenly.  A bucket's maxSignal words are 256 runs of 8 words (one run per
-// b3, bucket_word), its LDS slice bit for t is t & 0xFFFF = b3 << 8 | b0.
+// Partition key.  The passes and buckets work on t = set_pos(s), the
+// position of s in a set's bitmap (sg_internal.h): bytes (b2 b1 b3 b0) of
+// s = (b3 b2 b1 b0).  Pass 1 partitions by b2, pass 2 by b1, and a bucket
+// holds the 2^16 signals of one (b2, b1): bitmap words [b << 11, +2048), its
+// LDS slice bit for t is t & 0xFFFF.
 // Entry layouts.  Pass 1: t << 8 | record-in-tile (kRecCap records per tile
 // at most).  Pass 2: (t & 0xFFFF) << 16 | record-in-group.
 constexpr uint32_t kRecCap = 256;              // records per pass-1 tile
@@ -74,16 +71,12 @@ constexpr uint32_t kHash = 8192;             // candidate map slots per bucket (
 constexpr uint32_t kMaxProbe = 31;           // linear-probe cap before a bucket spills
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-__host__ __device__ __forceinline__ uint32_t part_key(uint32_t s) {  // (b3 b2 b1 b0) -> (b2 b1 b3 b0)
-  return ((s & 0x00FFFF00u) << 8) | ((s >> 16) & 0xFF00u) | (s & 0xFFu);
-}
-__host__ __device__ __forceinline__ uint32_t part_sig(uint32_t t) {  // inverse of part_key
-  return ((t & 0xFF00u) << 16) | ((t >> 8) & 0x00FFFF00u) | (t & 0xFFu);
-}
+__host__ __device__ __forceinline__ uint32_t part_key(uint32_t s) { return sgd::set_pos(s); }
+__host__ __device__ __forceinline__ uint32_t part_sig(uint32_t t) { return sgd::set_sig(t); }
 __host__ __device__ __forceinline__ uint32_t p1_digit(uint32_t s) { return (s >> 16) & 0xFFu; }  // part_key(s) >> 24
-// maxSignal word holding bucket b's LDS slice word j (= b3 * 8 + b0 / 32)
+// maxSignal word holding bucket b's LDS slice word j
 __host__ __device__ __forceinline__ uint64_t bucket_word(uint32_t b, uint32_t j) {
-  return ((uint64_t)(j >> 3) << 19) | ((uint64_t)b << 3) | (j & 7u);
+  return ((uint64_t)b << 11) | j;
 }
 
 // Blocks sharing an XCD (bid % 8 under round-robin dispatch) get a contiguous
@@ -807,7 +800,7 @@ __device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t 
 
 __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, BucketPre& P) {
   static_assert(kBucketWords / kBThreads == 4, "one uint4 of the slice per thread");
-  // LDS slice words 4 tid .. +3: one 16-B half of b3 = tid / 2's run of 8
+  // LDS slice words 4 tid .. +3
   const uint64_t w0 = bucket_word(b, 4 * threadIdx.x);
   const uint4 m = *reinterpret_cast<const uint4*>(a.mwords + w0);
   P.msw[0] = m.x;

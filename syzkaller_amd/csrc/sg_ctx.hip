@@ -316,11 +316,12 @@ __global__ void k_count_missing(const uint32_t* __restrict__ words, const uint32
 __global__ __launch_bounds__(kBlock) void k_set_tile_pop(const uint32_t* __restrict__ words,
                                                          uint32_t* __restrict__ tile_cnt) {
   __shared__ uint32_t red[kBlock / 64];
-  const uint4* w4 = reinterpret_cast<const uint4*>(words) + (uint64_t)blockIdx.x * (kTile / 4);
+  // tiles of 4096 words in signal order (sgd::set_word), as the export walks them
   uint32_t c = 0;
 #pragma unroll
   for (int j = 0; j < kTile / 4 / kBlock; j++) {
-    uint4 v = w4[j * kBlock + threadIdx.x];
+    const uint32_t ws = (uint32_t)blockIdx.x * kTile + (j * kBlock + threadIdx.x) * 4;
+    const uint4 v = *reinterpret_cast<const uint4*>(words + sgd::set_word(ws));
     c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
@@ -338,12 +339,14 @@ __global__ __launch_bounds__(kBlock) void k_set_export(const uint32_t* __restric
   uint64_t w0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * 16;
   uint64_t tb = tile_base[blockIdx.x];
   if (tile_base[blockIdx.x + 1] == tb) return;  // empty tile (block-uniform)
-  const uint4* w4 = reinterpret_cast<const uint4*>(words + w0);
+  // signal-order words w0 .. w0+15: two runs of 8 consecutive bitmap words
+  const uint4* r0 = reinterpret_cast<const uint4*>(words + sgd::set_word((uint32_t)w0));
+  const uint4* r1 = reinterpret_cast<const uint4*>(words + sgd::set_word((uint32_t)w0 + 8));
   uint32_t w[16];
   uint32_t c = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    uint4 v = w4[j];
+    uint4 v = j < 2 ? r0[j] : r1[j - 2];
     w[4 * j] = v.x;
     w[4 * j + 1] = v.y;
     w[4 * j + 2] = v.z;

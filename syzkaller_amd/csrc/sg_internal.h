@@ -188,11 +188,29 @@ int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, con
 // ---- device helpers -------------------------------------------------------
 namespace sgd {
 
+// Layout of a set's 2^32-bit bitmap: signal s = bytes (b3 b2 b1 b0) is bit
+// set_pos(s) = (b2 b1 b3 b0).  The low 5 bits are s's own, so this is a fixed
+// permutation of 32-bit words; 8 consecutive words (256 signals, one b0 range)
+// stay together.  It makes the 2^16 signals of one (b2, b1) -- the partitioned
+// triage's bucket (sg_bucket.hip) -- one contiguous 8 KiB slice: the raw top
+// byte of an edge signal is the top byte of hash(prev PC) and would pile the
+// edges of the hottest PCs into a few buckets.  Export walks the words in s
+// order (sg_ctx.hip), so members still come out ascending.
+__host__ __device__ __forceinline__ uint32_t set_pos(uint32_t s) {
+  return ((s & 0x00FFFF00u) << 8) | ((s >> 16) & 0xFF00u) | (s & 0xFFu);
+}
+__host__ __device__ __forceinline__ uint32_t set_sig(uint32_t p) {  // inverse of set_pos
+  return ((p & 0xFF00u) << 16) | ((p >> 8) & 0x00FFFF00u) | (p & 0xFFu);
+}
+// word of the bitmap holding s-order word ws (= s >> 5)
+__host__ __device__ __forceinline__ uint32_t set_word(uint32_t ws) {
+  return (((ws >> 3) & 0xFFFFu) << 11) | ((ws >> 19) << 3) | (ws & 7u);
+}
 __device__ __forceinline__ bool test_bit(const uint32_t* words, uint32_t s) {
-  return (words[s >> 5] >> (s & 31)) & 1u;
+  return (words[set_pos(s) >> 5] >> (s & 31)) & 1u;
 }
 __device__ __forceinline__ void set_bit(uint32_t* words, uint32_t s) {
-  atomicOr(&words[s >> 5], 1u << (s & 31));
+  atomicOr(&words[set_pos(s) >> 5], 1u << (s & 31));
 }
 
 // largest r in [lo, hi] with off[r] <= i (off non-decreasing), searched in

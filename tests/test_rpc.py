@@ -1,0 +1,110 @@
+"""RPC payload forms (pkg/rpctype/rpctype.go:8-63) and
+the sancov dump (tools/syz-execprog/execprog.go:159-177): the oracle against
+Go's encoding rules (CPU), the product's encoders / decoders against the
+oracle bit-exactly and round-tripping the []uint32 form (GPU)."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+
+def test_uvarint_matches_go_encoding():
+    # binary.PutUvarint reference points (LEB128)
+    assert O.put_uvarint(0) == b"\x00"
+    assert O.put_uvarint(127) == b"\x7f"
+    assert O.put_uvarint(128) == b"\x80\x01"
+    assert O.put_uvarint(300) == b"\xac\x02"
+    assert O.put_uvarint(0xFFFFFFFF) == b"\xff\xff\xff\xff\x0f"
+    rng = np.random.default_rng(41)
+    for _ in range(50):
+        v = np.unique(rng.integers(0, 1 << 32, size=int(rng.integers(0, 500)), dtype=np.uint64)).astype(np.uint32)
+        assert O.delta_decode(O.delta_encode(v)) == [int(x) for x in v]
+    for bad in (b"\x80", b"\xff\xff\xff\xff\x1f", b"\xff\xff\xff\xff\x0f\x01"):
+        with pytest.raises(ValueError):
+            O.delta_decode(bad)
+
+
+def test_sancov_layout():
+    b = O.sancov([0x81000010, 5])
+    assert b[:8] == bytes.fromhex("64ffffffffffbfc0")
+    assert b[8:16] == (0xFFFFFFFF81000010).to_bytes(8, "little")
+    assert len(b) == 24
+
+
+def _lists(rng, n):
+    out = []
+    for k in range(n):
+        m = int(rng.integers(0, 3000)) if k % 9 else 0
+        if k % 3 == 0:   # edge signal: spread over 32 bits
+            v = rng.integers(0, 1 << 32, size=m, dtype=np.uint64)
+        else:            # cover: clustered kernel-text PCs, duplicates (multisets sort fine)
+            v = 0x81000000 + 16 * rng.integers(0, 1 << 16, size=m)
+        v = np.sort(v).astype(np.uint32)
+        if k == 5 and m:
+            v[-1] = 0xFFFFFFFF
+        out.append(v)
+    return out
+
+
+@pytest.mark.gpu
+def test_delta_batch_vs_oracle(ctx):
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(42)
+    lists = _lists(rng, 200)
+    vals, off = C.to_csr(lists)
+    data, doff = C.delta_encode(vals, off, ctx=ctx)
+    for k, v in enumerate(lists):
+        assert data[int(doff[k]):int(doff[k + 1])].tobytes() == O.delta_encode(v), k
+    gv, go = C.delta_decode(data, doff, ctx=ctx)
+    assert np.array_equal(go, off) and np.array_equal(gv, vals)
+    # not sorted -> rejected
+    from syzkaller_amd._lib import SyzSigError
+    with pytest.raises(SyzSigError):
+        C.delta_encode(np.array([5, 3], np.uint32), np.array([0, 2], np.uint64), ctx=ctx)
+    # malformed payloads -> rejected
+    for bad in (b"\x05\x80", b"\xff\xff\xff\xff\x1f", b"\xff\xff\xff\xff\x0f\x01", b"\xff\xff\xff\xff\xff\x01"):
+        with pytest.raises(SyzSigError):
+            C.delta_decode(bad, np.array([0, len(bad)], np.uint64), ctx=ctx)
+    # a list may not end inside a value even when the next one would complete it
+    with pytest.raises(SyzSigError):
+        C.delta_decode(b"\x81\x01", np.array([0, 1, 2], np.uint64), ctx=ctx)
+
+
+@pytest.mark.gpu
+def test_set_payload_round_trip(ctx):
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(43)
+    m = np.unique(rng.integers(0, 1 << 32, size=300000, dtype=np.uint64)).astype(np.uint32)
+    m = np.concatenate([m, np.array([0, 0xFFFFFFFF], np.uint32)])
+    s = C.SignalSet(ctx)
+    C.SignalAdd(s, m)
+    payload = C.set_encode(s)
+    exp = np.unique(m)
+    assert payload == O.delta_encode(exp)
+    assert len(payload) < 4 * exp.size  # smaller than the []uint32 form
+    t = C.SignalSet(ctx)
+    C.SignalAdd(t, np.array([7, 8, 9], np.uint32))
+    assert C.set_decode_add(t, payload) == exp.size  # SignalAdd of the payload
+    assert np.array_equal(t.export(), np.union1d(exp, [7, 8, 9]).astype(np.uint32))
+    e = C.SignalSet(ctx)
+    assert C.set_encode(e) == b""
+    assert C.set_decode_add(e, b"") == 0 and len(e) == 0
+    for x in (s, t, e):
+        x.close()
+
+
+@pytest.mark.gpu
+def test_sancov_batch_vs_oracle(ctx):
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(44)
+    covs = [(0x81000000 + 16 * rng.integers(0, 1 << 20, size=int(rng.integers(0, 500)))).astype(np.uint32)
+            for _ in range(64)]
+    covs[3] = np.zeros(0, np.uint32)
+    vals, off = C.to_csr(covs)
+    files = C.sancov(vals, off, ctx=ctx)
+    assert len(files) == len(covs)
+    for k, c in enumerate(covs):
+        assert files[k] == O.sancov(c), k
