@@ -16,7 +16,9 @@ point (PCIe staging included), and the oracle on a bounded sample:
       calls x 1024 PCs.
   ipc executor output ingest (pkg/ipc/ipc_linux.go:168-307): 16Ki program
       output regions x 16 calls x 1024 signal words.
-Usage: python bench_rows.py [c1 c4 c5 a0 ipc]
+  f2  the manager's cover.Union folds (syz-manager/html.go:84/:94/:306): a
+      50k-input corpus by syscall and over everything.
+Usage: python bench_rows.py [c1 c4 c5 a0 ipc f2]
 """
 import json
 import os
@@ -68,10 +70,14 @@ def row_c1(ctx, rng):
         ctx.timing(False)
         dev_ms = sum(kt.values())
         n_out = sum(o.size for o in out)
-        # Union reads both lists of every pair; Difference only has to read
-        # cov0 (its count in cov1 is a search), so cov1 is not charged to it
-        n_in = int(a.size + (1000 * corpus.size if op == 2 else 0))
+        # One byte model for both ops: every trace and every output element
+        # once, and the corpus signal once per launch (all 1000 pairs share it;
+        # it stays cache-resident).  SURVEY §8(d)'s literal C1 formula charges
+        # the corpus to every pair, an upper bound that exceeds HBM peak when
+        # the corpus is not re-read (reported beside it).
+        n_in = int(a.size + corpus.size)
         algo = 4 * (n_in + n_out)
+        algo_per_pair = 4 * (a.size + 1000 * corpus.size + n_out)
         # oracle on a sample of 20 pairs
         t1 = time.perf_counter()
         for k in range(20):
@@ -80,6 +86,8 @@ def row_c1(ctx, rng):
         res[name] = {"pairs": 1000, "elements_in": n_in, "elements_out": n_out, "device_ms": dev_ms,
                      "kernels_ms": kt, "wall_ms_host_api": wall * 1e3,
                      "device_GBs_algo": algo / (dev_ms / 1e3) / 1e9, "frac_hbm": algo / (dev_ms / 1e3) / 1e9 / HBM,
+                     "byte_model": "4*(sum|a| + |corpus| + sum|out|), corpus once per launch",
+                     "survey_formula_GBs": algo_per_pair / (dev_ms / 1e3) / 1e9,
                      "cpu_oracle_ms_est_1000_pairs": cpu_s * 1e3, "parity_sample_20": True}
     return {"row": "c1 pkg/cover merge ops", **res}
 
@@ -111,6 +119,10 @@ def row_c4(ctx, rng):
 
 
 def row_c5(ctx, rng):
+    """100M query PCs against 5M call sites in 50k functions.  The queries
+    cover 10% of the functions, each of those on about half of its call sites
+    (random per function), so uncoveredPcsInFuncs (syz-manager/cover.go:257-307)
+    both marks whole covered functions' sites and removes the covered ones."""
     from oracle import pyoracle as O
 
     nsym, nsites, nq = 50_000, 5_000_000, 100_000_000
@@ -119,8 +131,13 @@ def row_c5(ctx, rng):
     starts = base + np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
     ends = starts + sizes
     per = (sizes // 16).astype(np.int64)
-    sites = np.concatenate([s + 5 + 16 * np.arange(k, dtype=np.uint64) for s, k in zip(starts, per)])[:nsites]
-    q = (rng.choice(sites[: nsites // 2], size=nq) + 5 - (np.uint64(0xffffffff) << np.uint64(32))).astype(np.uint32)
+    fn = np.repeat(np.arange(nsym), per)
+    sites = np.concatenate([s + 5 + 16 * np.arange(k, dtype=np.uint64) for s, k in zip(starts, per)])
+    sites, fn = sites[: nsites], fn[: nsites]
+    touched = rng.random(nsym) < 0.10
+    pool = sites[touched[fn] & (rng.random(sites.size) < 0.5)]
+    q = (rng.choice(pool, size=nq) + 5 - (np.uint64(0xffffffff) << np.uint64(32))).astype(np.uint32)
+    C.cover_uncovered(q[:1000], 0xffffffff, starts, ends, sites, ctx=ctx)  # warm
     ctx.timing(True)
     t0 = time.perf_counter()
     got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites, ctx=ctx)
@@ -135,10 +152,55 @@ def row_c5(ctx, rng):
     algo = 16 * nq
     dev = sum(v for v in kt.values() if v)
     return {"row": "c5 cover report", "queries": nq, "sites": int(sites.size), "symbols": nsym,
+            "functions_touched": int(touched.sum()), "query_pool_sites": int(pool.size),
             "uncovered": int(got.size), "kernels_ms": kt, "device_ms": dev,
             "device_ms_query_kernel": kt.get("report_query"), "wall_ms_host_api": wall * 1e3,
             "query_GBs_algo": algo / (kt["report_query"] / 1e3) / 1e9 if kt.get("report_query") else None,
+            "frac_hbm_query": algo / (kt["report_query"] / 1e3) / 1e9 / HBM if kt.get("report_query") else None,
+            "frac_hbm_all": algo / (dev / 1e3) / 1e9 / HBM,
             "parity_2M_prefix": bool(np.array_equal(got_s, ref)), "cpu_oracle_s_2M": cpu, "cpu_cores": 1}
+
+
+def row_f2(ctx, rng):
+    """syz-manager/html.go:84/:94/:306 cover.Union folds over a 50k-input corpus
+    (lognormal cover sizes, median 1k, over 2M kernel-text PCs), grouped by 4000
+    syscalls and over everything."""
+    from oracle import pyoracle as O
+
+    n, ncalls = 50_000, 4000
+    lens = np.clip(np.exp(rng.normal(np.log(1000), 0.8, size=n)), 1, 16384).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    raw = zipf_vals(rng, int(off[-1]), s=1.05, nranks=1 << 21)
+    covs = [np.unique(raw[int(off[k]):int(off[k + 1])]) for k in range(n)]  # executor-deduped cover
+    vals, off = C.to_csr(covs)
+    calls = rng.integers(0, ncalls, size=n).astype(np.uint32)
+    res = {}
+    for name, grp, ng in [("per_call_html84", calls, ncalls), ("all_html306", None, 1)]:
+        C.union_fold(vals[:10], np.array([0, 10], np.uint64), ctx=ctx)  # warm
+        ctx.timing(True)
+        t0 = time.perf_counter()
+        fv, fo = C.union_fold(vals, off, grp, ng, ctx=ctx)
+        wall = time.perf_counter() - t0
+        kt = ktime(ctx, ["union_fold", "merge_small", "merge_keep", "merge_scatter", "scan"])
+        ctx.timing(False)
+        dev = kt.get("union_fold", 0.0)
+        algo = 4 * (vals.size + fv.size)  # every input element read once, every fold element written once
+        # the oracle's left fold (the reference's O(inputs x |cov|) loop) on a sample
+        m = 2000
+        sv, so = C.to_csr(covs[:m])
+        gs = calls[:m] if grp is not None else None
+        t1 = time.perf_counter()
+        ev, eo = O.union_fold(sv, so, gs, ng)
+        cpu = time.perf_counter() - t1
+        pv, po = C.union_fold(sv, so, gs, ng, ctx=ctx)
+        parity = bool(np.array_equal(pv, ev) and np.array_equal(po, eo))
+        res[name] = {"inputs": n, "groups": ng, "elements_in": int(vals.size), "elements_out": int(fv.size),
+                     "device_ms": dev, "wall_ms_host_api": wall * 1e3, "kernels_ms": kt,
+                     "device_GBs_algo": algo / (dev / 1e3) / 1e9 if dev else None,
+                     "frac_hbm": algo / (dev / 1e3) / 1e9 / HBM if dev else None,
+                     "byte_model": "4*(elements_in + elements_out)", "parity": parity,
+                     "cpu_oracle_s_sample": cpu, "cpu_sample": f"first {m} inputs (parity on them)"}
+    return {"row": "f2 manager cover aggregation (Union folds)", **res}
 
 
 def row_a0(ctx, rng):
@@ -212,7 +274,7 @@ def main():
     import torch
 
     torch.cuda.set_device(0)
-    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc"]
+    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc", "f2"]
     ctx = C.Context(0)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(2026)

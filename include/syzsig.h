@@ -266,6 +266,16 @@ int sg_merge_batch(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const
 		   const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
 		   const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
 		   uint64_t* out_len);
+/* The manager's cover.Union folds (cov = Union(cov, inp.Cover) over inputs:
+ * syz-manager/html.go:84 grouped by syscall, :94, :184, :306, and the
+ * same-hash merge manager.go:916-917): for each group g < ngroups, the Union
+ * (cover.go:63-70) of the sorted lists k with group[k] == g (group NULL: one
+ * group of all n lists) -- every value with its largest count over those
+ * lists, ascending, 0xFFFFFFFF dropped.  List k is vals[off[k] .. off[k+1]).
+ * Group g's fold goes to out_vals[out_off[g] .. out_off[g+1]) (out_off:
+ * ngroups+1; capacity cap >= off[n] always suffices). */
+int sg_union_fold(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, const uint32_t* group,
+		  size_t ngroups, uint32_t* out_vals, size_t cap, uint64_t* out_off);
 /* HasDifference (cover.go:106-117): *out = 1 iff a has an element (multiset,
  * no sentinel special case) not matched in b. */
 int sg_has_difference(sg_ctx* ctx, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, int* out);

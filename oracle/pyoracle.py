@@ -171,6 +171,17 @@ def triage_subset(new_vals, new_off, r_vals, r_off):
     return ((io[1:] - io[:-1]) == (_u64(new_off)[1:] - _u64(new_off)[:-1])).astype(np.uint8)
 
 
+def union_fold(vals, off, group=None, ngroups=1):
+    """syz-manager/html.go:84/:94/:184/:306: cov = cover.Union(cov, inp.Cover)
+    over the inputs of each group, in input order (cover.go:63-70 via foreach)."""
+    vals, off = _u32(vals), _u64(off)
+    covs = [np.zeros(0, np.uint32) for _ in range(ngroups)]
+    for k in range(off.size - 1):
+        g = int(group[k]) if group is not None else 0
+        covs[g] = foreach(UNION, covs[g], vals[int(off[k]):int(off[k + 1])])
+    return _csr(covs)
+
+
 def put_uvarint(x):
     """Go encoding/binary PutUvarint (LEB128)."""
     out = bytearray()

@@ -200,6 +200,20 @@ def Intersection(cov0, cov1, ctx=None):
     return _merge(_lib.OP_INTERSECT, cov0, cov1, ctx)
 
 
+def union_fold(vals, off, group=None, ngroups=1, ctx=None):
+    """The manager's cover.Union folds (syz-manager/html.go:84/:94/:184/:306,
+    manager.go:916-917) for every group at once.  Returns (vals, off) with one
+    fold per group."""
+    vals, off = _u32(vals), _u64(off)
+    n = off.size - 1
+    g = _u32(group) if group is not None else None
+    out = np.empty(max(vals.size, 1), dtype=U32)
+    oo = np.zeros(ngroups + 1, dtype=U64)
+    call("sg_union_fold", _ctx(ctx).h, _p32(vals), _p64(off), n, _p32(g) if g is not None else None, ngroups,
+         _p32(out), out.size, _p64(oo))
+    return out[: int(oo[-1])].copy(), oo
+
+
 def HasDifference(cov0, cov1, ctx=None):
     a, b = _u32(cov0), _u32(cov1)
     out = c_int()

@@ -1026,7 +1026,13 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       ph[1] += t - tk;
       tk = t;
     }
-    if (__syncthreads_or(!ok)) {  // map full: redo with the direct table (no global writes yet)
+    const bool spill = __syncthreads_or(!ok);
+    if (kDbg) {  // the wait for the block's slowest wave
+      const uint64_t t = clock64();
+      ph[2] += t - tk;
+      tk = t;
+    }
+    if (spill) {  // map full: redo with the direct table (no global writes yet)
       if (tid == 0) {
         a.spill[atomicAdd(a.nspill, 1u)] = b;
         sh_fail = 0;
@@ -1094,10 +1100,15 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
           if (!seen[k]) a.rec_new[own[k]] = 1;
       }
     }
-    __syncthreads();  // sh_b[0] / sh_q[0] are written
     if (kDbg) {
       const uint64_t t = clock64();
       ph[3] += t - tk;
+      tk = t;
+    }
+    __syncthreads();  // sh_b[0] / sh_q[0] are written
+    if (kDbg) {
+      const uint64_t t = clock64();
+      ph[6] += t - tk;
       tk = t;
     }
     b = b1;
@@ -1119,6 +1130,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
     for (int j = 0; j < 4; j++) a.dbg[8 * blockIdx.x + 4 + j] = ph[j];
     a.dbg[8 * gridDim.x + 3 * blockIdx.x] = ph[4];
     a.dbg[8 * gridDim.x + 3 * blockIdx.x + 1] = ph[5];
+    a.dbg[8 * gridDim.x + 3 * blockIdx.x + 2] = ph[6];
   }
 }
 
@@ -1580,10 +1592,11 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
     std::vector<uint64_t> hd((size_t)bgrid * 11);
     SG_HIP(hipMemcpy(bd.data(), bdesc, bd.size() * 16, hipMemcpyDeviceToHost));
     SG_HIP(hipMemcpy(hd.data(), ddbg, hd.size() * 8, hipMemcpyDeviceToHost));
-    double qa = 0, qb = 0;
+    double qa = 0, qb = 0, qc = 0;
     for (uint32_t i = 0; i < bgrid; i++) {
       qa += hd[8 * bgrid + 3 * i];
       qb += hd[8 * bgrid + 3 * i + 1];
+      qc += hd[8 * bgrid + 3 * i + 2];
     }
     SG_HIP(hipFree(ddbg));
     std::vector<uint32_t> sz(kNumBuckets);
@@ -1606,11 +1619,9 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
       nrd += hd[8 * i + 3];
       for (int j = 0; j < 4; j++) phs[j] += hd[8 * i + 4 + j];
     }
-    fprintf(stderr, "sg bucket phases (Mcycles/block): install %.2f queue %.2f dense %.2f flush %.2f; per bucket %.0f"
-            " cycles, per round queue %.0f dense %.0f\n", phs[0] / bgrid / 1e6, phs[1] / bgrid / 1e6,
-            phs[2] / bgrid / 1e6, phs[3] / bgrid / 1e6, (phs[0] + phs[3]) / nbk, phs[1] / nrd, phs[2] / nrd);
-    fprintf(stderr, "sg bucket queue phase per round: to test done %.0f, to enqueue done %.0f cycles (cumulative)\n",
-            qa / nrd, qb / nrd);
+    fprintf(stderr, "sg bucket per bucket (cycles, wave 0): install %.0f | rounds: test %.0f insert %.0f tail %.0f | "
+            "end barrier %.0f flush %.0f final barrier %.0f | rounds/bucket %.2f\n", phs[0] / nbk, qa / nbk, qb / nbk,
+            phs[1] / nbk, phs[2] / nbk, phs[3] / nbk, qc / nbk, nrd / nbk);
     std::sort(dur.begin(), dur.end());
     fprintf(stderr,
             "sg bucket: sizes max=%u p99=%u median=%u rounds=%llu | blocks=%u span=%.1fus dur min=%.1f med=%.1f "

@@ -622,17 +622,16 @@ int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_
   return SG_OK;
 }
 
-static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
-                     const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
-                     const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
-                     uint64_t* out_len) {
+// Batched merge of device-resident lists: pair k is da[a_beg[k] .. +a_len[k])
+// op db[b_beg[k] .. +b_len[k]) into dout[out_beg[k] ..) (capacity a_len[k] +
+// b_len[k]).  The pair descriptors are host arrays (their lengths size the
+// launches); out_len (host) gets the result lengths.  da / db / dout must not
+// live in the workspace.  Syncs.
+int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint32_t* dout, const uint64_t* a_beg,
+              const uint64_t* a_len, const uint64_t* b_beg, const uint64_t* b_len, const uint64_t* out_beg,
+              size_t npair, uint64_t* out_len) {
   std::vector<uint64_t> aoff(npair + 1, 0), boff(npair + 1, 0);
   for (size_t k = 0; k < npair; k++) {
-    if (a_beg[k] + a_len[k] > a_total || b_beg[k] + b_len[k] > b_total ||
-        out_beg[k] + a_len[k] + b_len[k] > out_total) {
-      set_error("sg_merge_batch: pair %zu out of bounds", k);
-      return SG_EINVAL;
-    }
     aoff[k + 1] = aoff[k] + a_len[k];
     boff[k + 1] = boff[k] + b_len[k];
   }
@@ -642,23 +641,17 @@ static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, con
   uint64_t na = aoff[npair], nb = bside ? boff[npair] : 0;
   uint64_t nca = ((na + kTile - 1) / kTile) * kChunksPerTile, ncb = ((nb + kTile - 1) / kTile) * kChunksPerTile;
   WsPlan p;
-  size_t o_a = p.add(a_total * 4), o_b = p.add(b_total * 4), o_out = p.add(out_total * 4);
   size_t o_meta = p.add((npair * 2 + (npair + 1)) * 8 * 2 + npair * 8 * 2);
   size_t o_m0 = p.add(nca * 32), o_m1 = p.add(ncb * 32), o_c0 = p.add(nca * 4), o_c1 = p.add(ncb * 4),
          o_s0 = p.add((nca + 1) * 8), o_s1 = p.add((ncb + 1) * 8);
   size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(std::max(nca, ncb)));
   if (rc) return rc;
-  uint32_t* da = (uint32_t*)ws_at(ctx, o_a);
-  uint32_t* db = (uint32_t*)ws_at(ctx, o_b);
-  uint32_t* dout = (uint32_t*)ws_at(ctx, o_out);
   uint64_t* meta = (uint64_t*)ws_at(ctx, o_meta);
   // meta layout: a_beg a_len aoff b_beg b_len boff out_beg out_len
   uint64_t *m_abeg = meta, *m_alen = m_abeg + npair, *m_aoff = m_alen + npair, *m_bbeg = m_aoff + npair + 1,
            *m_blen = m_bbeg + npair, *m_boff = m_blen + npair, *m_obeg = m_boff + npair + 1,
            *m_olen = m_obeg + npair;
-  if (a_total) SG_HIP(hipMemcpyAsync(da, a, a_total * 4, hipMemcpyHostToDevice, ctx->stream));
-  if (b_total) SG_HIP(hipMemcpyAsync(db, b, b_total * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_abeg, a_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_alen, a_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_aoff, aoff.data(), (npair + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -672,58 +665,74 @@ static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, con
       ScopedTimer tm(ctx, "merge_small");
       hipLaunchKernelGGL(k_merge_small, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
     }
-    SG_HIP(hipGetLastError());
-    SG_HIP(hipMemcpyAsync(out_len, m_olen, npair * 8, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    for (size_t k = 0; k < npair; k++)
-      if (out_len[k])
-        SG_HIP(hipMemcpyAsync(out + out_beg[k], dout + out_beg[k], out_len[k] * 4, hipMemcpyDeviceToHost,
-                              ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    return SG_OK;
+  } else {
+    MergeArgs m{};
+    m.op = op;
+    m.a = {da, m_abeg, m_alen, m_aoff};
+    m.b = {db, m_bbeg, m_blen, m_boff};
+    m.npair = npair;
+    m.mask[0] = (uint64_t*)ws_at(ctx, o_m0);
+    m.mask[1] = (uint64_t*)ws_at(ctx, o_m1);
+    m.cnt[0] = (uint32_t*)ws_at(ctx, o_c0);
+    m.cnt[1] = (uint32_t*)ws_at(ctx, o_c1);
+    m.base[0] = (uint64_t*)ws_at(ctx, o_s0);
+    m.base[1] = (uint64_t*)ws_at(ctx, o_s1);
+    m.nchunks[0] = nca;
+    m.nchunks[1] = ncb;
+    m.out = dout;
+    m.out_beg = m_obeg;
+    m.out_len = m_olen;
+    {
+      ScopedTimer tm(ctx, "merge_keep");
+      if (nca) hipLaunchKernelGGL(k_merge_keep<0>, dim3(div_up(nca, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
+      if (ncb) hipLaunchKernelGGL(k_merge_keep<1>, dim3(div_up(ncb, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
+    }
+    if (nca) {
+      rc = scan_counts(ctx, m.cnt[0], m.base[0], nca, scan_off);
+      if (rc) return rc;
+    }
+    if (ncb) {
+      rc = scan_counts(ctx, m.cnt[1], m.base[1], ncb, scan_off);
+      if (rc) return rc;
+    }
+    {
+      ScopedTimer tm(ctx, "merge_scatter");
+      if (na)
+        hipLaunchKernelGGL(k_merge_scatter<0>, dim3((uint32_t)std::min<uint64_t>(div_up(na, 256), 16384)), dim3(256),
+                           0, ctx->stream, m);
+      if (nb)
+        hipLaunchKernelGGL(k_merge_scatter<1>, dim3((uint32_t)std::min<uint64_t>(div_up(nb, 256), 16384)), dim3(256),
+                           0, ctx->stream, m);
+    }
+    hipLaunchKernelGGL(k_merge_len, dim3(div_up(npair, 256)), dim3(256), 0, ctx->stream, m);
   }
-  MergeArgs m{};
-  m.op = op;
-  m.a = {da, m_abeg, m_alen, m_aoff};
-  m.b = {db, m_bbeg, m_blen, m_boff};
-  m.npair = npair;
-  m.mask[0] = (uint64_t*)ws_at(ctx, o_m0);
-  m.mask[1] = (uint64_t*)ws_at(ctx, o_m1);
-  m.cnt[0] = (uint32_t*)ws_at(ctx, o_c0);
-  m.cnt[1] = (uint32_t*)ws_at(ctx, o_c1);
-  m.base[0] = (uint64_t*)ws_at(ctx, o_s0);
-  m.base[1] = (uint64_t*)ws_at(ctx, o_s1);
-  m.nchunks[0] = nca;
-  m.nchunks[1] = ncb;
-  m.out = dout;
-  m.out_beg = m_obeg;
-  m.out_len = m_olen;
-  {
-    ScopedTimer tm(ctx, "merge_keep");
-    if (nca) hipLaunchKernelGGL(k_merge_keep<0>, dim3(div_up(nca, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
-    if (ncb) hipLaunchKernelGGL(k_merge_keep<1>, dim3(div_up(ncb, kBlock / 64)), dim3(kBlock), 0, ctx->stream, m);
-  }
-  if (nca) {
-    rc = scan_counts(ctx, m.cnt[0], m.base[0], nca, scan_off);
-    if (rc) return rc;
-  }
-  if (ncb) {
-    rc = scan_counts(ctx, m.cnt[1], m.base[1], ncb, scan_off);
-    if (rc) return rc;
-  }
-  {
-    ScopedTimer tm(ctx, "merge_scatter");
-    if (na)
-      hipLaunchKernelGGL(k_merge_scatter<0>, dim3((uint32_t)std::min<uint64_t>(div_up(na, 256), 16384)), dim3(256), 0,
-                         ctx->stream, m);
-    if (nb)
-      hipLaunchKernelGGL(k_merge_scatter<1>, dim3((uint32_t)std::min<uint64_t>(div_up(nb, 256), 16384)), dim3(256), 0,
-                         ctx->stream, m);
-  }
-  hipLaunchKernelGGL(k_merge_len, dim3(div_up(npair, 256)), dim3(256), 0, ctx->stream, m);
   SG_HIP(hipGetLastError());
   SG_HIP(hipMemcpyAsync(out_len, m_olen, npair * 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+static int merge_run(sg_ctx* ctx, int op, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+                     const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+                     const uint64_t* b_len, size_t npair, uint32_t* out, size_t out_total, const uint64_t* out_beg,
+                     uint64_t* out_len) {
+  for (size_t k = 0; k < npair; k++) {
+    if (a_beg[k] + a_len[k] > a_total || b_beg[k] + b_len[k] > b_total ||
+        out_beg[k] + a_len[k] + b_len[k] > out_total) {
+      set_error("sg_merge_batch: pair %zu out of bounds", k);
+      return SG_EINVAL;
+    }
+  }
+  const size_t b_a = (a_total * 4 + 255) & ~size_t(255), b_b = (b_total * 4 + 255) & ~size_t(255);
+  int rc = dstage_reserve(ctx, b_a + b_b + out_total * 4 + 256);
+  if (rc) return rc;
+  uint32_t* da = (uint32_t*)ctx->dstage;
+  uint32_t* db = (uint32_t*)((char*)ctx->dstage + b_a);
+  uint32_t* dout = (uint32_t*)((char*)ctx->dstage + b_a + b_b);
+  if (a_total) SG_HIP(hipMemcpyAsync(da, a, a_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (b_total) SG_HIP(hipMemcpyAsync(db, b, b_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  rc = merge_dev(ctx, op, da, db, dout, a_beg, a_len, b_beg, b_len, out_beg, npair, out_len);
+  if (rc) return rc;
   // copy back only each pair's result range
   for (size_t k = 0; k < npair; k++)
     if (out_len[k])

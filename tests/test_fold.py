@@ -1,0 +1,67 @@
+"""The manager's cover.Union folds (SURVEY.md §8(f) row 2:
+syz-manager/html.go:84/:94/:184/:306, manager.go:916-917) as one batched
+k-way tree of Unions (sg_union_fold) against the oracle's left fold of
+cover.go:63-70, bit-exact: multiset max-count semantics, 0xFFFFFFFF dropped."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from tests import refmodel as R
+
+
+def _corpus(rng, n, universe, maxlen, multiset=False):
+    covs = []
+    for k in range(n):
+        m = int(rng.integers(0, maxlen)) if k % 11 else 0
+        v = np.sort(rng.choice(universe, size=m, replace=multiset)).astype(np.uint32)
+        if k % 13 == 1 and m:
+            v[-1] = 0xFFFFFFFF  # cover.go:97 drops it in every Union
+        covs.append(v)
+    return covs
+
+
+def test_oracle_fold_vs_counts():
+    rng = np.random.default_rng(51)
+    uni = (0x81000000 + 16 * np.arange(5000)).astype(np.uint32)
+    for multiset in (False, True):
+        covs = _corpus(rng, 40, uni, 300, multiset)
+        vals, off = O._csr(covs)
+        fv, fo = O.union_fold(vals, off)
+        acc = []
+        for c in covs:
+            acc = R.foreach_counts(2, acc, [int(x) for x in c])
+        assert list(fv) == acc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("multiset", [False, True])
+def test_union_fold_vs_oracle(ctx, multiset):
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(52 + multiset)
+    uni = (0x81000000 + 16 * np.arange(1 << 16)).astype(np.uint32)
+    # html.go:84 (grouped by call), :306 (everything)
+    covs = _corpus(rng, 3000, uni, 2000, multiset)
+    vals, off = C.to_csr(covs)
+    calls = rng.integers(0, 37, size=len(covs)).astype(np.uint32)
+    calls[:5] = 36  # a group with several lists up front
+    gv, go = C.union_fold(vals, off, calls, 40, ctx=ctx)  # groups 37..39 stay empty
+    ev, eo = O.union_fold(vals, off, calls, 40)
+    assert np.array_equal(go, eo) and np.array_equal(gv, ev)
+    gv, go = C.union_fold(vals, off, ctx=ctx)
+    ev, eo = O.union_fold(vals, off)
+    assert np.array_equal(go, eo) and np.array_equal(gv, ev)
+    # html.go:94: the per-call covers folded again
+    gv2, go2 = C.union_fold(*C.union_fold(vals, off, calls, 40, ctx=ctx), ctx=ctx)
+    assert np.array_equal(gv2, ev)
+    # manager.go:916-917: Union of two
+    a, b = covs[3], covs[4]
+    gv, go = C.union_fold(*C.to_csr([a, b]), ctx=ctx)
+    assert np.array_equal(gv, O.foreach(O.UNION, a, b))
+    # a single list: Union(nil, c) -- the sentinel goes
+    c = np.array([5, 7, 7, 0xFFFFFFFF], np.uint32)
+    gv, _ = C.union_fold(*C.to_csr([c]), ctx=ctx)
+    assert list(gv) == [5, 7, 7]
+    # nothing at all
+    gv, go = C.union_fold(np.zeros(0, np.uint32), np.zeros(3, np.uint64), ctx=ctx)
+    assert gv.size == 0 and not go.any()

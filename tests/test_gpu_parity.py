@@ -623,3 +623,20 @@ def test_cover_uncovered_radix_edges(C):
     got = C.cover_uncovered(q, 0, s3, e3, p3)
     exp = O.cover_uncovered(q, 0, s3, e3, p3)
     assert np.array_equal(got, exp)
+
+
+def test_cover_uncovered_partial_functions(C):
+    """A non-degenerate report (C5's shape, scaled down): 10% of the functions
+    are touched, each on about half of its call sites, so the result holds
+    every untouched site of every touched function (syz-manager/cover.go:288-299
+    marks the function's whole range, then the covered PCs leave it)."""
+    rng = np.random.default_rng(142)
+    starts, ends, sites = _symtab(rng, 20000)
+    fn = np.searchsorted(starts, sites, side="right") - 1
+    touched = rng.random(starts.size) < 0.10
+    pool = sites[touched[fn] & (rng.random(sites.size) < 0.5)]
+    q = (rng.choice(pool, size=2_000_000) + np.uint64(5) - (np.uint64(0xffffffff) << np.uint64(32))).astype(np.uint32)
+    got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+    exp = O.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+    assert np.array_equal(got, exp)
+    assert exp.size > 0.2 * pool.size  # about half of the touched functions' sites stay uncovered
