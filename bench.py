@@ -325,6 +325,7 @@ def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world):
         dist.barrier()
     torch.cuda.synchronize()
     ctx.timing(True)
+    call("sg_ctx_marker", ctx.h, 0, 1)  # the timed region, for kernel traces (scripts/trace_summary.py)
     t0 = time.perf_counter()
     for b in batches:
         tm.mark()
@@ -333,6 +334,7 @@ def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world):
         triage(ctx, maxsig, newsig, b, rec_new)
         tm.mark()
         tm.ev.append(None)  # step separator
+    call("sg_ctx_marker", ctx.h, 1, 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

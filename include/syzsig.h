@@ -74,6 +74,9 @@ int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* laun
  * SG_TRIAGE_MAX_RECS (test knobs that lower the key space / the records per
  * partitioned launch) are read once, by sg_ctx_create. */
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
+/* Profiling aid: a one-thread kernel (k_mark_begin, or k_mark_end when end !=
+ * 0) on the context's stream, so a kernel trace can cut out a region. */
+int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag);
 
 /* ---- signal sets: replace map[uint32]struct{} ---------------------------- */
 /* maxSignal / corpusSignal / newSignal (syz-fuzzer/fuzzer.go:65-68) and

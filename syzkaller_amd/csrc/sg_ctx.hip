@@ -504,6 +504,33 @@ int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* laun
   return SG_OK;
 }
 
+}  // extern "C"
+
+namespace sg {
+// one-thread kernels that only mark a point of the stream in kernel traces
+__global__ void k_mark_begin(uint32_t* sink, uint32_t tag) {
+  if (tag == 0xFFFFFFFFu) *sink = tag;  // never taken: keeps the launch from being elided
+}
+__global__ void k_mark_end(uint32_t* sink, uint32_t tag) {
+  if (tag == 0xFFFFFFFFu) *sink = tag;
+}
+}  // namespace sg
+
+extern "C" {
+
+int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag) {
+  if (!ctx || tag == 0xFFFFFFFFu) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  if (end)
+    hipLaunchKernelGGL(k_mark_end, dim3(1), dim3(1), 0, ctx->stream, (uint32_t*)ctx->dscal, tag);
+  else
+    hipLaunchKernelGGL(k_mark_begin, dim3(1), dim3(1), 0, ctx->stream, (uint32_t*)ctx->dscal, tag);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
   if (!ctx || !name || !out) return SG_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
