@@ -66,7 +66,7 @@ static_assert(kGroupRecs % kRecCap == 0, "group boundaries must be tile cuts");
 constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
 constexpr int kBThreads = 512;
-constexpr int kBU = 8;                       // entries per thread per round in the bucket kernel
+constexpr int kBU = 4;                       // entries per thread per round in the bucket kernel
 constexpr uint32_t kHash = 8192;             // candidate map slots per bucket (32 bits each, see map_insert)
 constexpr uint32_t kMaxProbe = 31;           // linear-probe cap before a bucket spills
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -858,10 +858,11 @@ __device__ __forceinline__ uint32_t map_signal(uint32_t slot, uint32_t v) {  // 
 
 // A first insert is one CAS; a repeat of a signal lowers the record with a
 // 32-bit min (equal key bits above the record).
-__device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t* nbits, uint32_t sl, uint32_t rec) {
+__device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t* nbits, uint32_t sl, uint32_t rec,
+                                           uint32_t disp0 = 0) {
   const uint32_t y = (sl * kMapMul) & 0xFFFFu;
   const uint32_t home = y >> 3, tag = y & 7u;
-  for (uint32_t disp = 0; disp < kMaxProbe; disp++) {
+  for (uint32_t disp = disp0; disp < kMaxProbe; disp++) {
     const uint32_t mine = (tag << 29) | (disp << 24) | rec;
     uint32_t* slot = &ht[(home + disp) & (kHash - 1)];
     const uint32_t old = atomicCAS(slot, kEmpty, mine);
@@ -946,6 +947,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       pend_t = pend_b < kNumBuckets ? 2 * gridDim.x + atomicAdd(a.ticket, 1u) : kEmpty;
     }
     __syncthreads();
+    const uint32_t gbl = NG <= 64 ? gb[threadIdx.x & 63] : kEmpty;  // boundary of group lane (kEmpty past NG)
     if (kDbg) {
       const uint64_t t = clock64();
       ph[0] += t - tk;
@@ -984,28 +986,91 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         tk = t;
       }
       // (a relaxed atomic read: a volatile one would wait for every load in flight)
-      if (cm && __hip_atomic_load(&sh_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
-        // the record of each candidate: its group, found once per thread
-        // and stepped forward (entries are in group order)
-        uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
-        uint32_t nb = g + 1 < NG ? gb[g + 1] : kEmpty;  // next boundary
-        do {
-          const int u = __builtin_ctz(cm);
-          cm &= cm - 1;
-          uint32_t xu = x[0];
+      // each entry's group (its record is group << 16 | the entry's low half;
+      // entries are in group order).  Up to 64 groups the bucket's
+      // boundaries sit one per lane (gbl): the groups before the wave's
+      // first position are counted with a ballot, and the (rare) boundaries
+      // inside the wave's kBU * 64 positions are stepped over uniformly.
+      uint32_t gu[kBU];
+      if (NG <= 64) {
+        const uint32_t pw = base + (threadIdx.x & ~63u) * kBU;
+        // group of p = (boundaries <= p) - 1; positions before the first
+        // boundary are outside the bucket (never candidates): clamped to 0
+        const uint32_t nle = (uint32_t)__popcll(__ballot(gbl <= pw));
 #pragma unroll
-          for (int k = 1; k < kBU; k++) xu = k == u ? x[k] : xu;
-          while (nb <= p0 + u) {
-            g++;
-            nb = g + 1 < NG ? gb[g + 1] : kEmpty;
+        for (int u = 0; u < kBU; u++) gu[u] = nle;
+        for (uint64_t c = __ballot(gbl > pw && gbl < pw + 64 * kBU); c; c &= c - 1) {
+          const uint32_t bk = __builtin_amdgcn_readlane(gbl, __ffsll((unsigned long long)c) - 1);
+#pragma unroll
+          for (int u = 0; u < kBU; u++) gu[u] += p0 + u >= bk ? 1u : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kBU; u++) gu[u] = gu[u] ? gu[u] - 1 : 0u;
+      }
+      if (cm && __hip_atomic_load(&sh_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+        if (NG > 64) {  // the groups by search, stepped forward
+          uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
+          uint32_t nb = g + 1 < NG ? gb[g + 1] : kEmpty;  // next boundary
+#pragma unroll
+          for (int u = 0; u < kBU; u++) {
+            if ((cm >> u) & 1u)
+              while (nb <= p0 + u) {
+                g++;
+                nb = g + 1 < NG ? gb[g + 1] : kEmpty;
+              }
+            gu[u] = g;
           }
-          if (!map_insert(ht, nbits, xu >> 16, entry_record(g, xu))) {
+        }
+        // first probes of the thread's candidates in flight together, four
+        // at a time (straight-line, predicated): most land on an empty slot
+        // or on their own key; the rest take the probing loop below
+        uint32_t slow = 0;
+#pragma unroll
+        for (int h = 0; h < kBU; h += 4) {
+          uint32_t mine[4], old[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int u = h + j;
+            mine[j] = kEmpty;
+            old[j] = kEmpty;
+            if ((cm >> u) & 1u) {
+              const uint32_t y = ((x[u] >> 16) * kMapMul) & 0xFFFFu;
+              mine[j] = ((y & 7u) << 29) | entry_record(gu[u], x[u]);
+              old[j] = atomicCAS(&ht[y >> 3], kEmpty, mine[j]);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int u = h + j;
+            if ((cm >> u) & 1u) {
+              const uint32_t sl = x[u] >> 16;
+              if (old[j] == kEmpty) {
+                atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+              } else if ((old[j] >> 24) == (mine[j] >> 24)) {
+                if ((old[j] & kRecMask) > (mine[j] & kRecMask))
+                  atomicMin(&ht[((sl * kMapMul) & 0xFFFFu) >> 3], mine[j]);
+              } else {
+                slow |= 1u << u;
+              }
+            }
+          }
+        }
+        while (slow) {  // collisions: probe on from displacement 1
+          const int u = __builtin_ctz(slow);
+          slow &= slow - 1;
+          uint32_t xu = x[0], gk = gu[0];
+#pragma unroll
+          for (int k = 1; k < kBU; k++) {
+            xu = k == u ? x[k] : xu;
+            gk = k == u ? gu[k] : gk;
+          }
+          if (!map_insert(ht, nbits, xu >> 16, entry_record(gk, xu), 1)) {
             ok = false;
             // the others stop inserting (the bucket is redone)
             __hip_atomic_store(&sh_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             break;
           }
-        } while (cm);
+        }
       }
       if (kDbg) {
         const uint64_t t = clock64();
@@ -1061,44 +1126,41 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       // record owns signals in many buckets: its flag is read first and
       // written only while still clear, so its line is not dirtied (and
       // written back) once per bucket
-      constexpr int kOwn = kHash / kBThreads / 2;  // slots per thread, in two halves
+      constexpr int kOwn = kHash / kBThreads;  // slots per thread
       uint32_t own[kOwn];
       uint8_t seen[kOwn];
 #pragma unroll
-      for (int half = 0; half < 2; half++) {
-#pragma unroll
-        for (int k = 0; k < kOwn; k++) {
-          const uint32_t i = (half * kOwn + k) * kBThreads + tid;
-          const uint32_t v = ht[i];
-          own[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
-          ht[i] = kEmpty;
-        }
-#pragma unroll
-        for (int k = 0; k < kOwn; k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
-        if (half == 0) {
-          // (the first half's flag reads are in flight while the slice's words go out)
-          // words 4 tid .. +3: this block is their only writer
-          const uint64_t w0 = bucket_word(b, 4 * tid);
-          uint32_t* mg = a.mwords + w0;
-          uint32_t* ng = a.nwords ? a.nwords + w0 : nullptr;
-          const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
-          if (nb4.x | nb4.y | nb4.z | nb4.w) {
-            const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
-            const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
-            const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              if (nb[j]) {
-                mg[j] = mw[j] | nb[j];
-                if (ng) ng[j] = nw[j] | nb[j];
-              }
-            reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kOwn; k++)
-          if (!seen[k]) a.rec_new[own[k]] = 1;
+      for (int k = 0; k < kOwn; k++) {
+        const uint32_t i = k * kBThreads + tid;
+        const uint32_t v = ht[i];
+        own[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
+        ht[i] = kEmpty;
       }
+      // all the flag reads in flight together, while the slice's words go out
+#pragma unroll
+      for (int k = 0; k < kOwn; k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
+      {
+        // words 4 tid .. +3: this block is their only writer
+        const uint64_t w0 = bucket_word(b, 4 * tid);
+        uint32_t* mg = a.mwords + w0;
+        uint32_t* ng = a.nwords ? a.nwords + w0 : nullptr;
+        const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
+        if (nb4.x | nb4.y | nb4.z | nb4.w) {
+          const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
+          const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
+          const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (nb[j]) {
+              mg[j] = mw[j] | nb[j];
+              if (ng) ng[j] = nw[j] | nb[j];
+            }
+          reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kOwn; k++)
+        if (!seen[k]) a.rec_new[own[k]] = 1;
     }
     if (kDbg) {
       const uint64_t t = clock64();
