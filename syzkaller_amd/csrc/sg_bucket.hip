@@ -1122,23 +1122,9 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
       }
       reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
     } else {
-      // a record is queued iff it owns some signal (fuzzer.go:678-690).  A
-      // record owns signals in many buckets: its flag is read first and
-      // written only while still clear, so its line is not dirtied (and
-      // written back) once per bucket
+      // a record is queued iff it owns some signal (fuzzer.go:678-690): its
+      // flag is set (a record owns signals in many buckets; all set 1)
       constexpr int kOwn = kHash / kBThreads;  // slots per thread
-      uint32_t own[kOwn];
-      uint8_t seen[kOwn];
-#pragma unroll
-      for (int k = 0; k < kOwn; k++) {
-        const uint32_t i = k * kBThreads + tid;
-        const uint32_t v = ht[i];
-        own[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
-        ht[i] = kEmpty;
-      }
-      // all the flag reads in flight together, while the slice's words go out
-#pragma unroll
-      for (int k = 0; k < kOwn; k++) seen[k] = own[k] != kEmpty ? a.rec_new[own[k]] : 1;
       {
         // words 4 tid .. +3: this block is their only writer
         const uint64_t w0 = bucket_word(b, 4 * tid);
@@ -1159,8 +1145,12 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         }
       }
 #pragma unroll
-      for (int k = 0; k < kOwn; k++)
-        if (!seen[k]) a.rec_new[own[k]] = 1;
+      for (int k = 0; k < kOwn; k++) {
+        const uint32_t i = k * kBThreads + tid;
+        const uint32_t v = ht[i];
+        ht[i] = kEmpty;
+        if (v != kEmpty) a.rec_new[v & kRecMask] = 1;
+      }
     }
     if (kDbg) {
       const uint64_t t = clock64();
