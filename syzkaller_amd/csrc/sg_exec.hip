@@ -8,12 +8,12 @@
 //
 // The dedup decisions are inherently sequential within a program (each
 // insert can change later lookups), so one wave owns one program and its
-// 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 64
+// 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 128
 // edges at a time in parallel (pc ^ hash(prev pc) needs only a neighbour
-// shuffle) and decides their dedup speculatively: all 64 probe the table at
-// once, and the decisions are kept up to the first edge whose probe window
-// an earlier edge of the batch writes into (then the rest probe again);
-// kept edges are written with one coalesced compaction store per 64 PCs.
+// shift) and decides their dedup speculatively: all of them probe the table at
+// once, and the decisions are kept up to the first edge whose decision slot an
+// earlier writer of the window takes (then the rest probe again); kept edges
+// are written with coalesced compaction stores.
 #include "sg_internal.h"
 
 #include <cmath>
@@ -32,8 +32,9 @@ __device__ __forceinline__ uint32_t exec_hash(uint32_t a) {  // executor.h:497-5
   return a;
 }
 
-// The speculative pass, per edge j of the batch (lanes start..nvalid-1), all
-// deciding against the table as it stands:
+// The speculative pass, per edge j of the window (positions start..nvalid-1
+// of up to 128 edges: lane l holds positions l and 64 + l), all deciding
+// against the table as it stands:
 //   decision slot d_j: the slot holding sig (dup), the first empty slot
 //   (insert), or sig % 8192 (overwrite, all four taken); writers = inserts
 //   and overwrites, each writing d_j.
@@ -46,100 +47,160 @@ __device__ __forceinline__ uint32_t exec_hash(uint32_t a) {  // executor.h:497-5
 //   sig_m == sig_j  -> edge j is a duplicate (sequentially it finds sig at d_j)
 //   sig_m != sig_j  -> edge j is undecided (it decides again next pass).
 // Any later writer on d_j with another sig is itself undecided, so it cannot
-// commit before j.  The first writer per slot is found with an LDS atomicMin
-// of lane ids into kMarkSize marks indexed by d & (kMarkSize-1); a mark whose
-// lane wrote a different slot (aliasing) makes the lane undecided too.  The
-// decided prefix commits (its writers hit distinct slots); each pass commits
-// at least one edge.
-constexpr uint32_t kMarkSize = 2048;  // 8 KiB: table + marks = 40 KiB, 4 programs per CU
+// commit before j.  The first writer per slot comes from two small mark
+// tables (bucket d & 511 and bucket d >> 4): each writer posts
+// position << 45 | d << 32 | sig there with a 64-bit LDS atomicMin, so a
+// bucket's mark is its first writer together with that writer's slot and
+// signal.  If either of j's buckets has no writer before j, no earlier writer
+// is on d_j; otherwise a bucket mark on exactly d_j is the first writer on d_j
+// (every writer on d_j is in both buckets); if both marks are on other slots
+// (aliasing in both tables) edge j is conservatively undecided.  The decided
+// prefix commits (its writers hit distinct slots); each pass commits at least
+// one edge.
+constexpr uint32_t kMarkN = 512;       // per mark table: 2 x 512 x 8 B = 8 KiB; table + marks = 40 KiB, 4 programs per CU
+constexpr unsigned long long kNoMark = ~0ull;
+
+// (every lane probes: an inactive lane's result is not used, and unpredicated
+// LDS reads keep the probe free of exec-mask branches)
+__device__ __forceinline__ void probe(const uint32_t* table, uint32_t sig, uint32_t& d, bool& dup) {
+  uint32_t t[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) t[q] = table[(sig + (uint32_t)q) & (kDedupSize - 1)];
+  // executor.h:509-525: probe (s+q) % 8192 for q = 0..3 in order; a slot
+  // equal to s means duplicate, an empty slot takes s, and when all four are
+  // taken slot s % 8192 is overwritten.
+  uint32_t q = 0;
+  dup = false;
+#pragma unroll
+  for (int k = 3; k >= 0; k--)
+    if (t[k] == sig || t[k] == 0u) {
+      q = (uint32_t)k;
+      dup = t[k] == sig;
+    }
+  d = (sig + q) & (kDedupSize - 1);
+}
+
+// position pos (act) against its two bucket marks: bdup / undecided
+__device__ __forceinline__ void resolve(unsigned long long ma, unsigned long long mb, uint32_t pos, uint32_t d,
+                                        uint32_t sig, bool act, bool& bdup, bool& dirty) {
+  bdup = dirty = false;
+  if (!act || (uint32_t)(ma >> 45) >= pos || (uint32_t)(mb >> 45) >= pos) return;  // no earlier writer on d
+  if ((uint32_t)(ma >> 32 & 0x1FFFu) == d)
+    bdup = (uint32_t)ma == sig;
+  else if ((uint32_t)(mb >> 32 & 0x1FFFu) == d)
+    bdup = (uint32_t)mb == sig;
+  dirty = !bdup;
+}
+
+__device__ __forceinline__ unsigned long long mark_val(uint32_t pos, uint32_t d, uint32_t sig) {
+  return ((unsigned long long)pos << 45) | ((unsigned long long)d << 32) | sig;
+}
 
 __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__ pcs,
                                                     const uint64_t* __restrict__ call_off,
                                                     const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
                                                     uint32_t* __restrict__ cnt) {
   __shared__ uint32_t table[kDedupSize];
-  __shared__ uint32_t mark[kMarkSize];
+  __shared__ unsigned long long markA[kMarkN], markB[kMarkN];
   const int lane = threadIdx.x;
+  const uint32_t pos0 = (uint32_t)lane, pos1 = 64u + (uint32_t)lane;
   const uint64_t p = blockIdx.x;
   for (uint32_t i = lane; i < kDedupSize; i += 64) table[i] = 0;
-  for (uint32_t i = lane; i < kMarkSize; i += 64) mark[i] = 64u;
+  for (uint32_t i = lane; i < kMarkN; i += 64) markA[i] = markB[i] = kNoMark;
   __syncthreads();
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const uint64_t c0 = prog_off[p], c1 = prog_off[p + 1];
-  // the program's calls are contiguous in the trace: the next 64 PCs are
-  // always in flight (the next batch of this call, or the next call's first)
+  // the program's calls are contiguous in the trace: the next 128 PCs are
+  // always in flight (the next window of this call, or the next call's first)
   const uint64_t pend = call_off[c1];
-  uint32_t npc = call_off[c0] + lane < pend ? pcs[call_off[c0] + lane] : 0u;
+  uint64_t w0 = call_off[c0];
+  uint32_t npc0 = w0 + pos0 < pend ? pcs[w0 + pos0] : 0u, npc1 = w0 + pos1 < pend ? pcs[w0 + pos1] : 0u;
   for (uint64_t c = c0; c < c1; c++) {
     const uint64_t b = call_off[c], e = call_off[c + 1];
     uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
     uint64_t outpos = b;
-    for (uint64_t j = b; j < e; j += 64) {
-      const bool valid = j + lane < e;
-      const uint32_t pc = valid ? npc : 0u;
-      const uint64_t nj = j + 64 < e ? j + 64 : e;
-      npc = nj + lane < pend ? pcs[nj + lane] : 0u;
-      const uint32_t h = exec_hash(pc);
-      uint32_t hprev = __shfl_up(h, 1);
-      if (lane == 0) hprev = carry;
-      const uint32_t sig = pc ^ hprev;  // executor.h:393-395
-      const int nvalid = (int)((e - j) < 64 ? (e - j) : 64);
-      carry = __shfl(h, nvalid - 1);
-      // The 64 edges' dedup decisions, speculatively in parallel (see above).
-      uint64_t keep = 0;
+    for (uint64_t j = b; j < e; j += 128) {
+      const int nvalid = (int)((e - j) < 128 ? (e - j) : 128);
+      const uint32_t pc0 = pos0 < (uint32_t)nvalid ? npc0 : 0u, pc1 = pos1 < (uint32_t)nvalid ? npc1 : 0u;
+      // (unpredicated loads at clamped addresses: with no branch around them the
+      // wait for them lands where they are used, a window later, not here)
+      const uint64_t nj = j + 128 < e ? j + 128 : e;
+      const uint32_t l0 = pcs[nj + pos0 < pend ? nj + pos0 : pend - 1];
+      const uint32_t l1 = pcs[nj + pos1 < pend ? nj + pos1 : pend - 1];
+      npc0 = nj + pos0 < pend ? l0 : 0u;
+      npc1 = nj + pos1 < pend ? l1 : 0u;
+      const uint32_t h0 = exec_hash(pc0), h1 = exec_hash(pc1);
+      // the previous PC's hash: the position before's (a DPP wave shift; lane 0
+      // of the first half takes the carry, of the second half lane 63's)
+      const uint32_t hp0 =
+          (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)h0, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+      const uint32_t hp1 = (uint32_t)__builtin_amdgcn_update_dpp((int)__builtin_amdgcn_readlane(h0, 63), (int)h1, 0x138,
+                                                                 0xF, 0xF, false);
+      const uint32_t sig0 = pc0 ^ hp0, sig1 = pc1 ^ hp1;  // executor.h:393-395
+      carry = nvalid > 64 ? __builtin_amdgcn_readlane(h1, nvalid - 65) : __builtin_amdgcn_readlane(h0, nvalid - 1);
+      uint64_t keep0 = 0, keep1 = 0;
       for (int start = 0; start < nvalid;) {
-        const bool act = lane >= start && lane < nvalid;
-        uint32_t t[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) t[q] = act ? table[(sig + (uint32_t)q) & (kDedupSize - 1)] : 1u;
-        // executor.h:509-525: probe (s+q) % 8192 for q = 0..3 in order; a
-        // slot equal to s means duplicate, an empty slot takes s, and when
-        // all four are taken slot s % 8192 is overwritten.
-        uint32_t q = 0;
-        bool dup = false;
-#pragma unroll
-        for (int k = 3; k >= 0; k--)
-          if (t[k] == sig || t[k] == 0u) {
-            q = (uint32_t)k;
-            dup = t[k] == sig;
-          }
-        const uint32_t d = (sig + q) & (kDedupSize - 1);
-        const bool wr = act && !dup;
-        const uint64_t wm = __ballot(wr);
+        const bool act0 = (int)pos0 >= start && (int)pos0 < nvalid, act1 = (int)pos1 >= start && (int)pos1 < nvalid;
+        uint32_t d0, d1;
+        bool dup0, dup1;
+        probe(table, sig0, d0, dup0);
+        probe(table, sig1, d1, dup1);
+        const bool wr0 = act0 && !dup0, wr1 = act1 && !dup1;
+        const uint64_t wm0 = __ballot(wr0), wm1 = __ballot(wr1);
         int f = nvalid;
-        bool bdup = false;
-        if (wm) {
-          bool earlier;
-          if (!(wm & (wm - 1))) {  // one writer: compare against it directly
-            const int i = __ffsll((unsigned long long)wm) - 1;
-            const uint32_t di = __builtin_amdgcn_readlane(d, i), si = __builtin_amdgcn_readlane(sig, i);
-            earlier = act && lane > i && d == di;
-            bdup = earlier && sig == si;
-          } else {  // each lane's first earlier writer on its slot, through the marks
-            if (wr)
-              __hip_atomic_fetch_min(&mark[d & (kMarkSize - 1)], (uint32_t)lane, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool bd0 = false, bd1 = false;
+        if (wm0 | wm1) {
+          bool dt0, dt1;
+          if (__popcll(wm0) + __popcll(wm1) == 1) {  // one writer: compare against it directly
+            const uint32_t i = wm0 ? (uint32_t)(__ffsll((unsigned long long)wm0) - 1)
+                                   : 64u + (uint32_t)(__ffsll((unsigned long long)wm1) - 1);
+            const uint32_t di = i < 64 ? __builtin_amdgcn_readlane(d0, i) : __builtin_amdgcn_readlane(d1, i - 64);
+            const uint32_t si = i < 64 ? __builtin_amdgcn_readlane(sig0, i) : __builtin_amdgcn_readlane(sig1, i - 64);
+            const bool e0 = act0 && pos0 > i && d0 == di, e1 = act1 && pos1 > i && d1 == di;
+            bd0 = e0 && sig0 == si;
+            bd1 = e1 && sig1 == si;
+            dt0 = e0 && !bd0;
+            dt1 = e1 && !bd1;
+          } else {
+            if (wr0) {
+              const unsigned long long v = mark_val(pos0, d0, sig0);
+              __hip_atomic_fetch_min(&markA[d0 & (kMarkN - 1)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_min(&markB[d0 >> 4], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (wr1) {
+              const unsigned long long v = mark_val(pos1, d1, sig1);
+              __hip_atomic_fetch_min(&markA[d1 & (kMarkN - 1)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_min(&markB[d1 >> 4], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
-            const uint32_t m = act ? mark[d & (kMarkSize - 1)] : 64u;
-            const int src = m < 64u ? (int)m : lane;
-            const uint32_t dm = __shfl(d, src), sm = __shfl(sig, src);
-            earlier = act && m < (uint32_t)lane;
-            bdup = earlier && dm == d && sm == sig;
+            const unsigned long long a0 = markA[d0 & (kMarkN - 1)], b0 = markB[d0 >> 4];
+            const unsigned long long a1 = markA[d1 & (kMarkN - 1)], b1 = markB[d1 >> 4];
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             __builtin_amdgcn_wave_barrier();
-            if (wr) mark[d & (kMarkSize - 1)] = 64u;
+            if (wr0) markA[d0 & (kMarkN - 1)] = markB[d0 >> 4] = kNoMark;
+            if (wr1) markA[d1 & (kMarkN - 1)] = markB[d1 >> 4] = kNoMark;
+            resolve(a0, b0, pos0, d0, sig0, act0, bd0, dt0);
+            resolve(a1, b1, pos1, d1, sig1, act1, bd1, dt1);
           }
-          const uint64_t um = __ballot(earlier && !bdup);
-          f = um ? __ffsll((unsigned long long)um) - 1 : nvalid;
+          const uint64_t um0 = __ballot(dt0), um1 = __ballot(dt1);
+          f = um0 ? __ffsll((unsigned long long)um0) - 1 : (um1 ? 64 + __ffsll((unsigned long long)um1) - 1 : nvalid);
         }
-        const bool commit = wr && !bdup && lane < f;
-        if (commit) table[d] = sig;
-        keep |= __ballot(commit);
+        const bool cm0 = wr0 && !bd0 && (int)pos0 < f, cm1 = wr1 && !bd1 && (int)pos1 < f;
+        if (cm0) table[d0] = sig0;
+        if (cm1) table[d1] = sig1;
+        keep0 |= __ballot(cm0);
+        keep1 |= __ballot(cm1);
         start = f;
       }
-      if ((keep >> lane) & 1ull) tmp[outpos + __popcll(keep & lt)] = sig;
-      outpos += __popcll(keep);
+      // the next window's PCs are needed from here on: waiting for them before
+      // the (exec-masked, so branched-around) stores keeps the wait off the
+      // next window's critical path
+      asm volatile("" ::"v"(npc0), "v"(npc1));
+      if ((keep0 >> lane) & 1ull) tmp[outpos + __popcll(keep0 & lt)] = sig0;
+      outpos += __popcll(keep0);
+      if ((keep1 >> lane) & 1ull) tmp[outpos + __popcll(keep1 & lt)] = sig1;
+      outpos += __popcll(keep1);
     }
     if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
   }
