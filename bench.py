@@ -184,6 +184,8 @@ def pmc_bytes_per_step(kernels):
         if k in per and per[k].get("hbm_bytes_per_launch") is not None:
             tot += per[k]["hbm_bytes_per_launch"]
             seen.append(k)
+        elif k not in ("scan", "bucket_spill"):  # a summary of another kernel set: stale
+            return None, None
     return (tot if seen else None), d.get("tag")
 
 
