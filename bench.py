@@ -14,6 +14,9 @@ Workloads (BASELINE.json configs):
      16M-entry maxSignal bitmap.  The 16M-entry state is restored before every
      step (the restore copy is inside the timed region), so every timed step
      runs against the stated maxSignal.  Each step triages a fresh batch.
+  from traces (N=1, reported under "from_traces"): C2 end to end -- the timed
+     step also runs the executor signal kernels over the batch's raw PC traces
+     (resident in HBM), then triages what they produce.
   steady (N=1, reported under "steady_state"): the fuzzer's low-novelty steady
      state -- programs drawn from a fixed population of --npop programs,
      re-executed with flaky coverage (each PC replaced by a fresh draw with
@@ -414,9 +417,67 @@ def run_c2(ctx, args, cfg, rank):
         res["cpu"] = cpu_baseline(m0_values, timed[0], calls, gpu_flags0, args.cpu_budget, args.cpu_threads)
     del batches, timed
     torch.cuda.empty_cache()
+    if args.from_traces:
+        res["from_traces"] = run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new,
+                                             min(args.steps, 4))
     if args.steady:
         res["steady"] = run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new)
     return res
+
+
+def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
+    """End to end from executor traces: each timed step runs the executor-exact
+    signal kernels (A0, executor.h:389-401 + :497-526) over the batch's raw PC
+    traces, resident in HBM, and triages the signal it produced (C2's seeds,
+    so the triage work is the timed C2 batches')."""
+    calls = cfg["calls"]
+    traces, offs = [], []
+    for k in range(steps):
+        call("sg_gen_zipf_traces_dev", ctx.h, UNIVERSE_SEED, 1_000 + args.warmup + k, cfg["zipf_s"], cfg["ranks"], 0,
+             cfg["programs"], cfg["calls"], cfg["pcs_per_call"], g.trace.data_ptr())
+        traces.append(g.trace.clone())
+        offs.append(torch.empty(g.ncalls + 1, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    ev = []
+
+    def mark():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.append(e)
+
+    def step(tr, so):
+        call("sg_set_copy", maxsig.h, m0set.h)
+        mark()
+        call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
+             cfg["programs"], g.ncalls, g.npcs, g.sig.data_ptr(), so.data_ptr())
+        mark()
+        n = int(so[-1].item())  # the signal count, for the triage launch (8 bytes to the host)
+        call("sg_triage_batch_dev", ctx.h, maxsig.h, newsig.h, g.sig.data_ptr(), so.data_ptr(), n, g.ncalls,
+             rec_new.data_ptr(), None, None)
+        mark()
+        return n
+
+    step(traces[0], offs[0])  # warm-up
+    torch.cuda.synchronize()
+    ev.clear()
+    ctx.timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    units = sum(step(tr, so) for tr, so in zip(traces, offs))
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernels = kernel_table(ctx, ["exec_signal", "exec_compact"] + STEP_KERNELS, steps)
+    ctx.timing(False)
+    ex = [ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 3)]
+    tri = [ev[i + 1].elapsed_time(ev[i + 2]) for i in range(0, len(ev), 3)]
+    del traces, offs
+    torch.cuda.empty_cache()
+    return {"workload": "C2 from traces: the timed step is executor signal (exec_signal + exec_compact over "
+                        f"{g.npcs} resident raw PCs) + triage of the {units / steps:.0f} signal entries it yields, "
+                        "maxSignal restored before every step",
+            "value": g.npcs * steps / wall, "unit": "raw PCs/s", "signal_per_s": units / wall,
+            "ms_per_step": wall * 1e3 / steps, "steps": steps, "exec_ms_events": float(np.mean(ex)),
+            "triage_ms_events": float(np.mean(tri)), "kernels": kernels}
 
 
 def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
@@ -482,6 +543,7 @@ def main():
     ap.add_argument("--npop", type=int, default=2048, help="steady state: population size")
     ap.add_argument("--noise", type=float, default=2e-4, help="steady state: per-PC flaky-coverage probability")
     ap.add_argument("--no-steady", dest="steady", action="store_false")
+    ap.add_argument("--no-from-traces", dest="from_traces", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of single-thread CPU baseline work")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-cores CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
@@ -550,6 +612,7 @@ def main():
             "kernels": r["kernels"],
             "accounting": acct,
             "steady_state": r.get("steady"),
+            "from_traces": r.get("from_traces"),
             "path": "partitioned (flags + set updates)",
             "gen_s": r["gen_s"],
         }
