@@ -371,7 +371,7 @@ def test_triage_partition_geometry(C):
     vals = (0x5A000000 | rng.integers(0, 1 << 24, size=n)).astype(np.uint64)
     lens = np.diff(np.concatenate([[0], np.sort(rng.integers(0, n, size=2999)), [n]]))
     run(vals, lens)
-    # a bucket with ~20k distinct candidates (overflows the 4096-slot map), repeated
+    # a bucket with ~20k distinct candidates (overflows the 8192-slot map), repeated
     base = 0x3C7A0000
     vals = base + rng.permutation(65536)[:20000].astype(np.uint64)
     vals = np.concatenate([vals, vals[::-1], rng.integers(0, 1 << 32, size=5000, dtype=np.uint64)])
