@@ -66,7 +66,11 @@ constexpr uint32_t kMaxGroups = 256;           // groups per launch (larger batc
 static_assert(kGroupRecs % kRecCap == 0, "group boundaries must be tile cuts");
 constexpr uint32_t kNumBuckets = 1u << 16;   // (top byte, second byte) of s
 constexpr uint32_t kBucketWords = 2048;      // 2^16 signals
-constexpr int kBThreads = 512;
+#ifndef SG_BTHREADS
+#define SG_BTHREADS 512
+#endif
+constexpr int kBThreads = SG_BTHREADS;     // bucket-kernel workgroup
+constexpr int kBWaves = kBThreads == 512 ? 6 : 8;  // waves per SIMD it is built for
 constexpr int kBU = 4;                       // entries per thread per round in the bucket kernel
 constexpr uint32_t kHash = 8192;             // candidate map slots per bucket (32 bits each, see map_insert)
 constexpr uint32_t kMaxProbe = 31;           // linear-probe cap before a bucket spills
@@ -734,18 +738,6 @@ __global__ void k_bucket_groups(const uint32_t* __restrict__ goff2, const uint32
   gbnd[i] = goff2[(uint64_t)(b & 255) * *gcount + cbase[(b >> 8) * NG + g]];
 }
 
-__device__ __forceinline__ void flush_new_bits(const BucketArgs& a, uint32_t b, const uint32_t* mslice,
-                                               const uint32_t* nbits, int tid, int nthreads) {
-  for (uint32_t i = tid; i < kBucketWords; i += nthreads) {
-    const uint32_t nb = nbits[i];
-    if (nb) {
-      const uint64_t w = bucket_word(b, i);
-      a.mwords[w] = mslice[i] | nb;
-      if (a.nwords) a.nwords[w] |= nb;
-    }
-  }
-}
-
 // group of bucket position p >= gb[0]: last g < NG with gb[g] <= p
 __device__ __forceinline__ uint32_t group_of(const uint32_t* gb, uint32_t NG, uint32_t p) {
   uint32_t lo = 0, hi = NG;
@@ -774,6 +766,8 @@ __device__ __forceinline__ uint32_t entry_record(uint32_t g, uint32_t x) { retur
 // maxSignal slice and group boundaries.  The ticket after that is fetched a
 // bucket ahead, so no dependent load is exposed.
 constexpr uint32_t kGroupWords = (kMaxGroups + kBThreads - 1) / kBThreads;  // group boundaries per thread
+constexpr int kWPT = kBucketWords / kBThreads;  // LDS slice words per thread
+typedef uint32_t wvec __attribute__((ext_vector_type(kWPT)));
 struct BucketPre {  // a bucket's first loads, held in registers
   uint32_t msw[kBucketWords / kBThreads];
   uint32_t nsw[kBucketWords / kBThreads];  // newSignal words (only this block writes them)
@@ -806,20 +800,16 @@ __device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t 
 }
 
 __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, BucketPre& P) {
-  static_assert(kBucketWords / kBThreads == 4, "one uint4 of the slice per thread");
-  // LDS slice words 4 tid .. +3
-  const uint64_t w0 = bucket_word(b, 4 * threadIdx.x);
-  const uint4 m = *reinterpret_cast<const uint4*>(a.mwords + w0);
-  P.msw[0] = m.x;
-  P.msw[1] = m.y;
-  P.msw[2] = m.z;
-  P.msw[3] = m.w;
-  const uint4 nw = a.nwords ? *reinterpret_cast<const uint4*>(a.nwords + w0)
-                            : make_uint4(0, 0, 0, 0);
-  P.nsw[0] = nw.x;
-  P.nsw[1] = nw.y;
-  P.nsw[2] = nw.z;
-  P.nsw[3] = nw.w;
+  // LDS slice words kWPT tid .. + kWPT - 1
+  const uint64_t w0 = bucket_word(b, kWPT * threadIdx.x);
+  const wvec m = *reinterpret_cast<const wvec*>(a.mwords + w0);
+  wvec nw = {};
+  if (a.nwords) nw = *reinterpret_cast<const wvec*>(a.nwords + w0);
+#pragma unroll
+  for (int j = 0; j < kWPT; j++) {
+    P.msw[j] = m[j];
+    P.nsw[j] = nw[j];
+  }
   const uint32_t* gr = a.gbnd + (uint64_t)b * a.NG;
 #pragma unroll
   for (int j = 0; j < (int)kGroupWords; j++) {
@@ -886,7 +876,7 @@ __device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t* nbits, uint32
 }
 
 template <bool kDbg, bool kEmit>
-__global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_bucket(BucketArgs a) {
+__global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWaves))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
   __shared__ uint32_t ht[kHash];
@@ -939,8 +929,15 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
   while (b < kNumBuckets) {
     const uint32_t lo = q.x, hi = q.y;
     __syncthreads();  // the previous bucket is done with the LDS
-    reinterpret_cast<uint4*>(mslice)[tid] = make_uint4(P.msw[0], P.msw[1], P.msw[2], P.msw[3]);
-    const uint4 ns = make_uint4(P.nsw[0], P.nsw[1], P.nsw[2], P.nsw[3]);  // words 4 tid .. +3
+    {
+      wvec mv;
+#pragma unroll
+      for (int j = 0; j < kWPT; j++) mv[j] = P.msw[j];
+      reinterpret_cast<wvec*>(mslice)[tid] = mv;
+    }
+    uint32_t ns[kWPT];  // newSignal words kWPT tid .. + kWPT - 1
+#pragma unroll
+    for (int j = 0; j < kWPT; j++) ns[j] = P.nsw[j];
 #pragma unroll
     for (int j = 0; j < (int)kGroupWords; j++) {
       const uint32_t i = j * kBThreads + tid;
@@ -1127,28 +1124,29 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
         }
         emit_pairs(a, sig, rec, shcnt);
       }
-      reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<wvec*>(nbits)[tid] = wvec{};
     } else {
       // a record is queued iff it owns some signal (fuzzer.go:678-690): its
       // flag is set (a record owns signals in many buckets; all set 1)
       constexpr int kOwn = kHash / kBThreads;  // slots per thread
       {
-        // words 4 tid .. +3: this block is their only writer
-        const uint64_t w0 = bucket_word(b, 4 * tid);
+        // words kWPT tid ..: this block is their only writer
+        const uint64_t w0 = bucket_word(b, kWPT * tid);
         uint32_t* mg = a.mwords + w0;
         uint32_t* ng = a.nwords ? a.nwords + w0 : nullptr;
-        const uint4 nb4 = reinterpret_cast<const uint4*>(nbits)[tid];
-        if (nb4.x | nb4.y | nb4.z | nb4.w) {
-          const uint4 m4 = reinterpret_cast<const uint4*>(mslice)[tid];
-          const uint32_t nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, mw[4] = {m4.x, m4.y, m4.z, m4.w};
-          const uint32_t nw[4] = {ns.x, ns.y, ns.z, ns.w};
+        const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
+        uint32_t any = 0;
 #pragma unroll
-          for (int j = 0; j < 4; j++)
+        for (int j = 0; j < kWPT; j++) any |= nb[j];
+        if (any) {
+          const wvec mw = reinterpret_cast<const wvec*>(mslice)[tid];
+#pragma unroll
+          for (int j = 0; j < kWPT; j++)
             if (nb[j]) {
               mg[j] = mw[j] | nb[j];
-              if (ng) ng[j] = nw[j] | nb[j];
+              if (ng) ng[j] = ns[j] | nb[j];
             }
-          reinterpret_cast<uint4*>(nbits)[tid] = make_uint4(0, 0, 0, 0);
+          reinterpret_cast<wvec*>(nbits)[tid] = wvec{};
         }
       }
 #pragma unroll
@@ -1194,57 +1192,64 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(6))) 
 }
 
 // Buckets with too many distinct candidates: a direct first-owner table over
-// a quarter of the bucket at a time (16384 signals, 64 KiB of LDS).
+// one eighth of the bucket (8192 signals, 32 KiB of LDS) per job; the
+// (bucket, eighth) jobs are independent (each owns its eighth's 256 bitmap
+// words), so a few huge spilled buckets spread over many workgroups.
+constexpr int kDThreads = 1024;
 template <bool kEmit>
-__global__ __launch_bounds__(kBThreads) void k_bucket_direct(BucketArgs a) {
-  constexpr uint32_t kQ = 16384;
+__global__ __launch_bounds__(kDThreads) void k_bucket_direct(BucketArgs a) {
+  constexpr uint32_t kQ = 8192, kNQ = 65536 / kQ, kQW = kQ / 32;
   __shared__ uint32_t owner[kQ];
-  __shared__ uint32_t mslice[kBucketWords];
-  __shared__ uint32_t nbits[kBucketWords];
+  __shared__ uint32_t mpart[kQW];
+  __shared__ uint32_t nbits[kQW];
   __shared__ uint32_t gb[kMaxGroups];
   __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];
   const int tid = threadIdx.x;
   const uint32_t nsp = *a.nspill, NG = a.NG;
   if (kEmit) {
-    for (uint32_t i = tid; i < kMaxShards; i += kBThreads) shcnt[i] = 0;
+    for (uint32_t i = tid; i < kMaxShards; i += kDThreads) shcnt[i] = 0;
     __syncthreads();
   }
-  for (uint32_t j = blockIdx.x; j < nsp; j += gridDim.x) {
-    const uint32_t b = a.spill[j];
+  for (uint32_t job = blockIdx.x; job < nsp * kNQ; job += gridDim.x) {
+    const uint32_t b = a.spill[job / kNQ], qq = job % kNQ;
     const uint4 q = a.bdesc[b];
-    for (uint32_t i = tid; i < kBucketWords; i += kBThreads) {
-      mslice[i] = a.mwords[bucket_word(b, i)];
+    for (uint32_t i = tid; i < kQW; i += kDThreads) {
+      mpart[i] = a.mwords[bucket_word(b, qq * kQW + i)];
       nbits[i] = 0;
     }
-    for (uint32_t i = tid; i < NG; i += kBThreads) gb[i] = a.gbnd[(uint64_t)b * NG + i];
-    for (uint32_t qq = 0; qq < 65536 / kQ; qq++) {
-      for (uint32_t i = tid; i < kQ; i += kBThreads) owner[i] = kEmpty;
-      __syncthreads();
-      for (uint32_t i = q.x + tid; i < q.y; i += kBThreads) {
-        const uint32_t x = a.in[i];
-        const uint32_t sl = x >> 16;
-        if (sl / kQ != qq || ((mslice[sl >> 5] >> (sl & 31)) & 1u)) continue;
-        atomicMin(&owner[sl % kQ], entry_record(group_of(gb, NG, i), x));
-        atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
-      }
-      __syncthreads();
-      if (kEmit) {
-        constexpr int kPer = kQ / kBThreads;
-        uint32_t sig[kPer], rec[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-          const uint32_t i = k * kBThreads + tid;
-          sig[k] = part_sig((b << 16) | (qq * kQ + i));
-          rec[k] = owner[i];
-        }
-        emit_pairs(a, sig, rec, shcnt);
-      } else {
-        for (uint32_t i = tid; i < kQ; i += kBThreads)
-          if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
-      }
-      __syncthreads();
+    for (uint32_t i = tid; i < NG; i += kDThreads) gb[i] = a.gbnd[(uint64_t)b * NG + i];
+    for (uint32_t i = tid; i < kQ; i += kDThreads) owner[i] = kEmpty;
+    __syncthreads();
+    for (uint32_t i = q.x + tid; i < q.y; i += kDThreads) {
+      const uint32_t x = a.in[i];
+      const uint32_t sl = x >> 16, sq = sl % kQ;
+      if (sl / kQ != qq || ((mpart[sq >> 5] >> (sq & 31)) & 1u)) continue;
+      atomicMin(&owner[sq], entry_record(group_of(gb, NG, i), x));
+      atomicOr(&nbits[sq >> 5], 1u << (sq & 31));
     }
-    if (!kEmit) flush_new_bits(a, b, mslice, nbits, tid, kBThreads);
+    __syncthreads();
+    if (kEmit) {
+      constexpr int kPer = kQ / kDThreads;
+      uint32_t sig[kPer], rec[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+        const uint32_t i = k * kDThreads + tid;
+        sig[k] = part_sig((b << 16) | (qq * kQ + i));
+        rec[k] = owner[i];
+      }
+      emit_pairs(a, sig, rec, shcnt);
+    } else {
+      for (uint32_t i = tid; i < kQ; i += kDThreads)
+        if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
+      for (uint32_t i = tid; i < kQW; i += kDThreads) {
+        const uint32_t nb = nbits[i];
+        if (nb) {
+          const uint64_t w = bucket_word(b, qq * kQW + i);
+          a.mwords[w] = mpart[i] | nb;
+          if (a.nwords) a.nwords[w] |= nb;
+        }
+      }
+    }
     __syncthreads();
   }
   if (kEmit) flush_shard_counts(a, shcnt);
@@ -1634,9 +1639,9 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   {
     ScopedTimer tm(ctx, "bucket_spill");
     if (emit)
-      hipLaunchKernelGGL(k_bucket_direct<true>, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
+      hipLaunchKernelGGL(k_bucket_direct<true>, dim3(512), dim3(kDThreads), 0, ctx->stream, ba);
     else
-      hipLaunchKernelGGL(k_bucket_direct<false>, dim3(1024), dim3(kBThreads), 0, ctx->stream, ba);
+      hipLaunchKernelGGL(k_bucket_direct<false>, dim3(512), dim3(kDThreads), 0, ctx->stream, ba);
   }
   SG_HIP(hipGetLastError());
   if (dbg) {  // diagnostics: chunk and spill counts (syncs)
