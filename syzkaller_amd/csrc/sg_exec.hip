@@ -19,6 +19,10 @@
 #include <cmath>
 #include <cstring>
 
+#ifndef SG_EXEC_FENCE
+#define SG_EXEC_FENCE 0
+#endif
+
 namespace sg {
 
 constexpr uint32_t kDedupSize = 8192;  // executor.h:506
@@ -172,11 +176,17 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
               __hip_atomic_fetch_min(&markA[d1 & (kMarkN - 1)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               __hip_atomic_fetch_min(&markB[d1 >> 4], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+#if SG_EXEC_FENCE
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#endif
+            // (one wave: its LDS operations complete in issue order, so the
+            // reads below see every lane's atomicMin without a fence)
             __builtin_amdgcn_wave_barrier();
             const unsigned long long a0 = markA[d0 & (kMarkN - 1)], b0 = markB[d0 >> 4];
             const unsigned long long a1 = markA[d1 & (kMarkN - 1)], b1 = markB[d1 >> 4];
+#if SG_EXEC_FENCE
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+#endif
             __builtin_amdgcn_wave_barrier();
             if (wr0) markA[d0 & (kMarkN - 1)] = markB[d0 >> 4] = kNoMark;
             if (wr1) markA[d1 & (kMarkN - 1)] = markB[d1 >> 4] = kNoMark;
