@@ -227,7 +227,21 @@ __device__ __forceinline__ void multi_bound(P p, uint64_t n, const uint32_t (&v)
   }
 }
 
-__global__ __launch_bounds__(kMT) void k_merge_small(SmallArgs m) {
+// #{j in [j0, ns): S[j] < x} + j0 (kLe: <= x) for sorted S in LDS, j0 below
+// the answer: a wave's ballot per 64 candidates (the lanes where it holds
+// are a prefix)
+template <bool kLe>
+__device__ __forceinline__ uint32_t ballot_count(const uint32_t* sv, uint32_t ns, uint32_t j0, uint32_t x, int lane) {
+  for (;;) {
+    const uint32_t j = j0 + (uint32_t)lane;
+    const bool c = j < ns && (kLe ? sv[j] <= x : sv[j] < x);
+    const uint64_t b = __ballot(c);
+    if (b != ~0ull) return j0 + (uint32_t)__popcll(b);
+    j0 += 64;
+  }
+}
+
+__global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_merge_small(SmallArgs m) {
   __shared__ uint32_t sv[kMS];
   __shared__ uint32_t skp[kMS + 1];    // kept small elements before j
   __shared__ uint32_t sidx[kMS];       // insertion point of small element j in L
@@ -307,25 +321,77 @@ __global__ __launch_bounds__(kMT) void k_merge_small(SmallArgs m) {
   __syncthreads();
   const uint32_t KS = skp[ns];
   // L: stream tiles in index order
-  uint32_t KL = 0, jlo = 0;
+  uint32_t KL = 0, jlo = 0, jp = 0;
+  // the next tile's L values and each one's predecessor (a later copy of a
+  // value is rare, but telling needs L[i - 1]), in flight while a tile is
+  // processed
+  uint32_t xn[kML], pn[kML];
+#pragma unroll
+  for (int s = 0; s < kML; s++) {
+    const uint64_t i = (uint64_t)s * kMT + tid;
+    xn[s] = i < nl ? L[i] : kSent;
+    pn[s] = i > 0 && i < nl ? L[i - 1] : 0u;
+  }
   for (uint64_t tb = 0; tb < nl; tb += kMTile) {
-    uint32_t x[kML];
-    uint64_t lbs[kML], ubs[kML];
+    uint32_t x[kML], xp[kML];
+    uint32_t lbs[kML], ubs[kML];  // bounds in S (<= kMS)
     bool valid[kML];
 #pragma unroll
     for (int s = 0; s < kML; s++) {
       const uint64_t i = tb + (uint64_t)s * kMT + tid;
       valid[s] = i < nl;
-      x[s] = valid[s] ? L[i] : kSent;
+      x[s] = xn[s];
+      xp[s] = pn[s];
+      const uint64_t in = i + kMTile;
+      xn[s] = in < nl ? L[in] : kSent;
+      pn[s] = in < nl ? L[in - 1] : 0u;
     }
-    multi_bound<kML, false>(sv, ns, x, lbs);
-    multi_bound<kML, true>(sv, ns, x, ubs);
+    // each step s of a wave covers 64 consecutive L values: the S elements in
+    // their value range are found with ballots from the wave's running
+    // position jp (usually none or one), so the per-element bounds need no
+    // search; a dense range falls back to a search inside it
+#pragma unroll
+    for (int s = 0; s < kML; s++) {
+      const uint64_t vb = __ballot(valid[s]);
+      if (!vb) {
+        lbs[s] = ubs[s] = 0;
+        continue;
+      }
+      const uint32_t xf = __builtin_amdgcn_readfirstlane(x[s]);
+      const uint32_t xl = __builtin_amdgcn_readlane(x[s], 63 - __clzll((unsigned long long)vb));
+      const uint32_t jA = ballot_count<false>(sv, ns, jp, xf, lane);
+      const uint32_t jB = ballot_count<true>(sv, ns, jA, xl, lane);
+      jp = jA;
+      uint32_t lt = jA, le = jA;
+      if (jB - jA <= 16) {
+        for (uint32_t j = jA; j < jB; j++) {
+          const uint32_t v = sv[j];
+          lt += v < x[s] ? 1u : 0u;
+          le += v <= x[s] ? 1u : 0u;
+        }
+      } else {
+        uint32_t lo = jA, hi = jB;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sv[mid] < x[s]) lo = mid + 1; else hi = mid;
+        }
+        lt = lo;
+        hi = jB;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sv[mid] <= x[s]) lo = mid + 1; else hi = mid;
+        }
+        le = lo;
+      }
+      lbs[s] = lt;
+      ubs[s] = le;
+    }
     bool kp[kML];
 #pragma unroll
     for (int s = 0; s < kML; s++) {
       const uint64_t i = tb + (uint64_t)s * kMT + tid;
       uint64_t t = 0;
-      if (valid[s] && i > 0 && L[i - 1] == x[s]) {  // later copy (rare): first index by search
+      if (valid[s] && i > 0 && xp[s] == x[s]) {  // later copy (rare): first index by search
         uint64_t lo = 0, hi = i;
         while (lo < hi) {
           const uint64_t mid = (lo + hi) >> 1;
@@ -360,14 +426,18 @@ __global__ __launch_bounds__(kMT) void k_merge_small(SmallArgs m) {
       }
     // S elements whose insertion point lies in this tile
     uint32_t jhi;
-    {
-      uint32_t lo = jlo, hi = ns;
+    {  // #{j : sidx[j] < tile end} by ballots from jlo (sidx is non-decreasing)
       const uint64_t end = tb + kMTile;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sidx[mid] < end) lo = mid + 1; else hi = mid;
+      uint32_t j0 = jlo;
+      for (;;) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        const uint64_t b = __ballot(j < ns && sidx[j] < end);
+        if (b != ~0ull) {
+          jhi = j0 + (uint32_t)__popcll(b);
+          break;
+        }
+        j0 += 64;
       }
-      jhi = lo;
     }
     for (uint32_t j = jlo + tid; j < jhi; j += kMT)
       if (skp[j + 1] > skp[j]) {
