@@ -322,18 +322,14 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   const uint32_t KS = skp[ns];
   // L: stream tiles in index order
   uint32_t KL = 0, jlo = 0, jp = 0;
-  // the next tile's L values and each one's predecessor (a later copy of a
-  // value is rare, but telling needs L[i - 1]), in flight while a tile is
-  // processed
-  uint32_t xn[kML], pn[kML];
+  uint32_t xn[kML];  // the next tile's L values, in flight while a tile is processed
 #pragma unroll
   for (int s = 0; s < kML; s++) {
     const uint64_t i = (uint64_t)s * kMT + tid;
     xn[s] = i < nl ? L[i] : kSent;
-    pn[s] = i > 0 && i < nl ? L[i - 1] : 0u;
   }
   for (uint64_t tb = 0; tb < nl; tb += kMTile) {
-    uint32_t x[kML], xp[kML];
+    uint32_t x[kML];
     uint32_t lbs[kML], ubs[kML];  // bounds in S (<= kMS)
     bool valid[kML];
 #pragma unroll
@@ -341,10 +337,8 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       const uint64_t i = tb + (uint64_t)s * kMT + tid;
       valid[s] = i < nl;
       x[s] = xn[s];
-      xp[s] = pn[s];
       const uint64_t in = i + kMTile;
       xn[s] = in < nl ? L[in] : kSent;
-      pn[s] = in < nl ? L[in - 1] : 0u;
     }
     // each step s of a wave covers 64 consecutive L values: the S elements in
     // their value range are found with ballots from the wave's running
@@ -391,7 +385,10 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     for (int s = 0; s < kML; s++) {
       const uint64_t i = tb + (uint64_t)s * kMT + tid;
       uint64_t t = 0;
-      if (valid[s] && i > 0 && xp[s] == x[s]) {  // later copy (rare): first index by search
+      // the copy index t only matters against a non-zero count in S (every
+      // keep rule keeps all copies of a value S lacks): rare, so only then
+      // look at L[i - 1] and search for the value's first index
+      if (valid[s] && ubs[s] > lbs[s] && i > 0 && L[i - 1] == x[s]) {
         uint64_t lo = 0, hi = i;
         while (lo < hi) {
           const uint64_t mid = (lo + hi) >> 1;
