@@ -171,8 +171,11 @@ __global__ void k_merge_scatter(MergeArgs m) {
 constexpr int kMS = 4096;               // max small side
 constexpr int kMT = 1024;               // threads
 constexpr int kMU = kMS / kMT;          // small elements per thread (consecutive)
-constexpr int kML = 4;                  // large elements per thread per tile
-constexpr int kMTile = kMT * kML;       // 4096
+#ifndef SG_KML
+#define SG_KML 8
+#endif
+constexpr int kML = SG_KML;             // large elements per thread per tile
+constexpr int kMTile = kMT * kML;       // 8192
 constexpr int kMWaves = kMT / 64;       // 16
 
 struct SmallArgs {
@@ -401,16 +404,29 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       if (lane == 0) tw[s * kMWaves + w] = bw;
     }
     __syncthreads();
-    if (tid < 64) {  // word prefix over the tile (index order = (s, wave))
-      const uint32_t c = tid < kML * kMWaves ? (uint32_t)__popcll(tw[tid]) : 0u;
+    if (tid < 64) {  // word prefix over the tile (index order = (s, wave)); kWL words per lane
+      constexpr int kNWd = kML * kMWaves, kWL = (kNWd + 63) / 64;
+      uint32_t cw[kWL], c = 0;
+#pragma unroll
+      for (int q = 0; q < kWL; q++) {
+        const int wi = tid * kWL + q;
+        cw[q] = wi < kNWd ? (uint32_t)__popcll(tw[wi]) : 0u;
+        c += cw[q];
+      }
       uint32_t incl = c;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
       }
-      if (tid < kML * kMWaves) twp[tid] = KL + incl - c;
-      if (tid == kML * kMWaves - 1) twp[kML * kMWaves] = KL + incl;
+      uint32_t run = KL + incl - c;
+#pragma unroll
+      for (int q = 0; q < kWL; q++) {
+        const int wi = tid * kWL + q;
+        if (wi < kNWd) twp[wi] = run;
+        run += cw[q];
+      }
+      if (tid == 63) twp[kNWd] = KL + incl;
     }
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1;
