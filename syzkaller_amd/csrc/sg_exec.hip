@@ -19,6 +19,9 @@
 #include <cmath>
 #include <cstring>
 
+#ifndef SG_COMPACT_UNROLL
+#define SG_COMPACT_UNROLL 1
+#endif
 #ifndef SG_EXEC_FENCE
 #define SG_EXEC_FENCE 0
 #endif
@@ -225,7 +228,24 @@ __global__ __launch_bounds__(256) void k_exec_compact(const uint32_t* __restrict
   if (c >= ncalls) return;
   const int lane = threadIdx.x & 63;
   uint64_t src = call_off[c], dst = sig_off[c], n = sig_off[c + 1] - sig_off[c];
+#if SG_COMPACT_UNROLL
+  // four loads per lane in flight before their stores
+  for (uint64_t i0 = 0; i0 < n; i0 += 256) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint64_t i = i0 + u * 64 + lane;
+      v[u] = i < n ? __builtin_nontemporal_load(tmp + src + i) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint64_t i = i0 + u * 64 + lane;
+      if (i < n) out[dst + i] = v[u];
+    }
+  }
+#else
   for (uint64_t i = lane; i < n; i += 64) out[dst + i] = tmp[src + i];
+#endif
 }
 
 // ---- Zipf generator ----------------------------------------------------------
