@@ -665,13 +665,17 @@ __device__ __forceinline__ uint32_t shard_of(uint32_t s, uint32_t nshards) {
 
 constexpr uint32_t kMaxShards = 64;
 
-// Wave-aggregated append of up to kPer pairs per lane (valid where rec !=
-// kEmpty); each pair is also counted in the block's LDS shard counters.
+// Block-aggregated append of up to kPer pairs per lane (valid where rec !=
+// kEmpty): one global atomic per call and block (a per-wave atomic on the one
+// pair counter was the emitting launch's bottleneck); each pair is also
+// counted in the block's LDS shard counters.  Called by every thread.
 template <int kPer>
 __device__ __forceinline__ void emit_pairs(const BucketArgs& a, const uint32_t (&sig)[kPer], const uint32_t (&rec)[kPer],
                                            uint32_t* shcnt) {
   constexpr uint32_t kNone = 0xFFFFFFFFu;
-  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t ewc[16];  // per-wave totals, then offsets (<= 1024 threads)
+  __shared__ unsigned long long ebase;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   uint32_t c = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) c += rec[k] != kNone ? 1u : 0u;
@@ -681,18 +685,26 @@ __device__ __forceinline__ void emit_pairs(const BucketArgs& a, const uint32_t (
     const uint32_t y = __shfl_up(incl, o);
     if (lane >= o) incl += y;
   }
-  const uint32_t tot = __shfl(incl, 63);
-  if (tot == 0) return;
-  unsigned long long base = 0;
-  if (lane == 63) base = atomicAdd(a.npairs, (unsigned long long)tot);
-  base = __shfl(base, 63);
-  uint64_t pos = base + incl - c;
+  if (lane == 63) ewc[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < nw; i++) {
+      const uint32_t v = ewc[i];
+      ewc[i] = acc;
+      acc += v;
+    }
+    ebase = acc ? atomicAdd(a.npairs, (unsigned long long)acc) : 0ull;
+  }
+  __syncthreads();
+  uint64_t pos = ebase + ewc[w] + incl - c;
 #pragma unroll
   for (int k = 0; k < kPer; k++)
     if (rec[k] != kNone) {
       a.pairs[pos++] = make_uint2(sig[k], a.rec_base + rec[k]);
       atomicAdd(&shcnt[shard_of(sig[k], a.nshards)], 1u);
     }
+  __syncthreads();  // ewc / ebase are rewritten by the next call
 }
 
 __device__ __forceinline__ void flush_shard_counts(const BucketArgs& a, const uint32_t* shcnt) {

@@ -26,7 +26,11 @@
 namespace sg {
 
 constexpr uint32_t kShardMax = 64;  // == kMaxShards of sg_bucket.hip
-constexpr uint64_t kLaunchEntries = 1ull << 31;  // entries per emitting launch (< the partition's 2^32 cap)
+// entries per emitting launch: about one C2 batch, so the buckets stay the
+// size the LDS candidate map is built for (a launch twice that spilled a
+// tenth of its buckets to the slow direct-table kernel); well under the
+// partition's 2^32 cap
+constexpr uint64_t kLaunchEntries = 1ull << 30;
 
 __device__ __forceinline__ uint32_t shard_hash(uint32_t s, uint32_t nshards) {  // == shard_of (sg_bucket.hip)
   s ^= s >> 16;
@@ -101,31 +105,73 @@ __global__ void k_shard_claim(const uint2* __restrict__ pairs, uint64_t n, uint3
   }
 }
 
-// the owning pair of each s: its record's bit, and s once in the new list
-__global__ void k_shard_resolve(const uint2* __restrict__ pairs, uint64_t n, const uint32_t* __restrict__ owner,
-                                uint32_t key_lo, uint32_t* __restrict__ rec_bits, uint32_t* __restrict__ new_vals,
-                                unsigned long long* __restrict__ nnew) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const int lane = threadIdx.x & 63;
+// the owning pair of each s: its record's flag (a byte store: a record owns
+// many signals, and atomics on its bit word were the stage's bottleneck), and
+// s once in the new list, each block reserving its round's run with one
+// atomic
+constexpr int kResT = 1024, kResPer = 4;
+__global__ __launch_bounds__(kResT) void k_shard_resolve(const uint2* __restrict__ pairs, uint64_t n,
+                                                         const uint32_t* __restrict__ owner, uint32_t key_lo,
+                                                         uint8_t* __restrict__ rec_flag, uint32_t* __restrict__ new_vals,
+                                                         unsigned long long* __restrict__ nnew) {
+  __shared__ uint32_t wcnt[kResT / 64 + 1];
+  __shared__ unsigned long long sbase;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // whole waves iterate together (the ballot below)
-  const uint64_t n_up = (n + 63) & ~63ull;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
-    bool own = false;
-    uint2 p = make_uint2(0, 0);
-    if (i < n) {
-      p = pairs[i];
-      own = owner[p.x] == key_lo + p.y;
+  constexpr uint64_t kRound = (uint64_t)kResT * kResPer;
+  for (uint64_t base = (uint64_t)blockIdx.x * kRound; base < n; base += (uint64_t)gridDim.x * kRound) {
+    uint2 p[kResPer];
+    bool own[kResPer];
+#pragma unroll
+    for (int k = 0; k < kResPer; k++) {
+      const uint64_t i = base + (uint64_t)k * kResT + tid;
+      own[k] = false;
+      p[k] = make_uint2(0, 0);
+      if (i < n) p[k] = pairs[i];
     }
-    if (own) atomicOr(&rec_bits[p.y >> 5], 1u << (p.y & 31));
-    const uint64_t m = __ballot(own);
-    if (!m) continue;
-    unsigned long long base = 0;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    if (lane == leader) base = atomicAdd(nnew, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    if (own) new_vals[base + __popcll(m & lt)] = p.x;
+#pragma unroll
+    for (int k = 0; k < kResPer; k++)
+      if (base + (uint64_t)k * kResT + tid < n) own[k] = owner[p[k].x] == key_lo + p[k].y;
+    uint64_t m[kResPer];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kResPer; k++) {
+      if (own[k]) rec_flag[p[k].y] = 1;
+      m[k] = __ballot(own[k]);
+      c += (uint32_t)__popcll(m[k]);
+    }
+    if (lane == 0) wcnt[w] = c;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int i = 0; i < kResT / 64; i++) {
+        const uint32_t v = wcnt[i];
+        wcnt[i] = acc;
+        acc += v;
+      }
+      sbase = acc ? atomicAdd(nnew, (unsigned long long)acc) : 0ull;
+    }
+    __syncthreads();
+    uint64_t pos = sbase + wcnt[w];
+#pragma unroll
+    for (int k = 0; k < kResPer; k++) {
+      if (own[k]) new_vals[pos + __popcll(m[k] & lt)] = p[k].x;
+      pos += __popcll(m[k]);
+    }
+    __syncthreads();
   }
+}
+
+// bit r of bits = flag[r]
+__global__ void k_pack_flags(const uint8_t* __restrict__ flag, uint64_t n, uint32_t* __restrict__ bits) {
+  const uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (wi * 32 >= n) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 32; b++) {
+    const uint64_t r = wi * 32 + b;
+    if (r < n && flag[r]) v |= 1u << b;
+  }
+  bits[wi] = v;
 }
 
 // rec_new[i] = bit (rec_lo + i) of the OR of nparts bitsets, each holding
@@ -219,7 +265,7 @@ int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_val
       uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
       rc = read_u64(ctx, d_rec_off + r1, &e1);
       if (rc) return rc;
-      if (e1 - e0 >= kLaunchEntries) {  // largest r1 with entries < 2^31 (a record holds < 2^31)
+      if (e1 - e0 >= kLaunchEntries) {  // largest r1 with entries < 2^30 (a record holds < 2^30)
         uint64_t lo = r0 + 1, hi = r1;
         while (lo < hi) {
           const uint64_t mid = (lo + hi + 1) / 2;
@@ -235,7 +281,7 @@ int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_val
         rc = read_u64(ctx, d_rec_off + r1, &e1);
         if (rc) return rc;
         if (e1 - e0 >= kLaunchEntries) {
-          set_error("sg_shard_candidates_dev: a record holds >= 2^31 signal entries");
+          set_error("sg_shard_candidates_dev: a record holds >= 2^30 signal entries");
           return SG_EINVAL;
         }
       }
@@ -274,6 +320,10 @@ int sg_shard_owners_dev(sg_ctx* ctx, const uint32_t* d_pairs, uint64_t npairs, u
   SG_HIP(hipMemsetAsync(d_rec_bits, 0, ((nrec_total + 31) / 32) * 4, ctx->stream));
   SG_HIP(hipMemsetAsync(d_nnew, 0, 8, ctx->stream));
   if (npairs == 0) return SG_OK;
+  rc = dstage_reserve(ctx, nrec_total + 64);
+  if (rc) return rc;
+  uint8_t* rec_flag = (uint8_t*)ctx->dstage;
+  SG_HIP(hipMemsetAsync(rec_flag, 0, nrec_total, ctx->stream));
   uint32_t key_lo = 0;
   rc = owner_keys(ctx, nrec_total ? nrec_total : 1, &key_lo);
   if (rc) return rc;
@@ -285,8 +335,11 @@ int sg_shard_owners_dev(sg_ctx* ctx, const uint32_t* d_pairs, uint64_t npairs, u
   }
   {
     ScopedTimer tm(ctx, "shard_resolve");
-    hipLaunchKernelGGL(k_shard_resolve, dim3(grid), dim3(256), 0, ctx->stream, (const uint2*)d_pairs, npairs,
-                       (const uint32_t*)ctx->owner, key_lo, d_rec_bits, d_new_vals, (unsigned long long*)d_nnew);
+    hipLaunchKernelGGL(k_shard_resolve, dim3(std::min<uint64_t>(div_up(npairs, (uint64_t)kResT * kResPer), 4096)),
+                       dim3(kResT), 0, ctx->stream, (const uint2*)d_pairs, npairs, (const uint32_t*)ctx->owner, key_lo,
+                       rec_flag, d_new_vals, (unsigned long long*)d_nnew);
+    hipLaunchKernelGGL(k_pack_flags, dim3(div_up(div_up(nrec_total, 32), 256)), dim3(256), 0, ctx->stream,
+                       (const uint8_t*)rec_flag, nrec_total, d_rec_bits);
   }
   SG_HIP(hipGetLastError());
   return SG_OK;
