@@ -19,10 +19,10 @@ import torch.distributed as dist
 
 from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, kernel_table, n_uniq, pmc_bytes_per_step, step_bytes,
                    triage, HBM_PEAK_GBS, SignalSet, U32_WORDS, StepTimer)
-from syzkaller_amd.shard import Comm, HipStages, ShardedTriage
+from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
-                                "set_add"]
+                                "set_add", "prefix_or", "set_or", "set_copy"]
 
 
 def _max_over_ranks(x, world):
@@ -58,7 +58,8 @@ def run_c3(ctx, args, cfg, rank, world):
         counts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
         dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device="cuda"))
         assert len({int(c.item()) for c in counts}) == 1, "maxSignal snapshots differ between ranks"
-    tri = ShardedTriage(HipStages(ctx), Comm())
+    prefix = getattr(args, "c3_proto", "prefix") == "prefix"
+    tri = (PrefixTriage if prefix else ShardedTriage)(HipStages(ctx), Comm())
     rec_base = rank * nprog * calls
 
     def step(b):
@@ -95,13 +96,16 @@ def run_c3(ctx, args, cfg, rank, world):
     last = dict(tri.last)
     queued = int(rec_new[: b.nrec].sum().item())
     acct_rank = {"n_in": b.nvals, "n_uniq": n_uniq(b, calls), "n_cand": c.value, "n_rec": b.nrec,
-                 "n_queued": queued, "pairs_sent": last["pairs_sent"], "pairs_received": last["pairs_received"]}
+                 "n_queued": queued, "pairs_sent": last.get("pairs_sent", 0),
+                 "pairs_received": last.get("pairs_received", 0)}
     acct = {k: _sum_over_ranks(v, world) for k, v in acct_rank.items()}
-    acct["n_new_signal"] = last["new_signal"]
-    acct["n_diff"] = last["new_signal"]  # diff multiplicity not emitted by the sharded path
+    after = len(maxsig)
+    new_signal = last["new_signal"] if "new_signal" in last else after - m0_count
+    acct["n_new_signal"] = new_signal
+    acct["n_diff"] = new_signal  # diff multiplicity not emitted by the sharded path
     acct["queued_frac"] = acct["n_queued"] / acct["n_rec"] if acct["n_rec"] else None
-    acct["maxsignal_after"] = len(maxsig)
-    acct["consistent"] = acct["maxsignal_after"] == m0_count + last["new_signal"]
+    acct["maxsignal_after"] = after
+    acct["consistent"] = after == m0_count + new_signal
     ms_step = wall * 1e3 / args.steps
     # roofline: whole-job step bytes over all ranks / step time / aggregate peak
     bpr = step_bytes(acct) / world
@@ -110,7 +114,10 @@ def run_c3(ctx, args, cfg, rank, world):
             "scope": "whole sharded step per GPU (wall clock, max over ranks; exchanges included)",
             "algo_bytes_per_step_per_gpu": bpr,
             "formula": "SURVEY.md §8(d) C2/C3 bytes over all ranks / N (N_out taken as the new-signal count)"}
-    xgmi = 8 * acct["pairs_sent"] / world + 4 * (acct["n_rec"] / 32) / world + 4 * last["new_signal"]
+    if prefix:
+        xgmi = last.get("exchange_bytes", 0)
+    else:
+        xgmi = 8 * acct["pairs_sent"] / world + 4 * (acct["n_rec"] / 32) / world + 4 * last["new_signal"]
     if rank != 0:
         return None
     return {
@@ -129,20 +136,25 @@ def run_c3(ctx, args, cfg, rank, world):
         "config": {
             "workload": f"C3 recipe: one batch of {world} x {nprog} programs x {calls} calls x {cfg['pcs_per_call']} "
                         f"Zipf PCs (N=8: C3's 1Mi programs), records split contiguously, {nprog} programs "
-                        f"({nprog * calls} call records) per rank; one sequential triage loop hash-sharded by signal "
-                        f"(RCCL all-to-all of candidates, OR of record-flag slices, all-gather of new signal) vs a "
-                        f"replicated {m0_count}-entry maxSignal restored before every step",
+                        f"({nprog * calls} call records) per rank; one sequential triage loop over the whole batch, "
+                        + ("by bitmap prefixes (local new signal, RCCL all-to-all of bitmap slices and exclusive "
+                           "prefix-OR, local triage against maxSignal | prefix)" if prefix else
+                           "hash-sharded by signal (RCCL all-to-all of candidates, OR of record-flag slices, "
+                           "all-gather of new signal)")
+                        + f" vs a replicated {m0_count}-entry maxSignal restored before every step",
             "programs_per_gpu": nprog, "batch_programs": world * nprog, "calls": calls,
             "pcs_per_call": cfg["pcs_per_call"], "signal_per_step": units / args.steps,
             "maxsignal_start": m0_count, "queued_frac": acct["queued_frac"],
-            "parallelism": f"signal-sharded x{world} (one rank per GPU, RCCL)",
+            "parallelism": (f"record-sliced x{world}, bitmap-prefix exchange" if prefix else
+                            f"signal-sharded x{world}") + " (one rank per GPU, RCCL)",
         },
         "roofline": roof,
         "cpu_baseline": None,
         "kernels": kernels,
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,
-        "path": "sharded (syzkaller_amd/shard.py + sg_shard.hip)",
+        "path": ("prefix (syzkaller_amd/shard.py PrefixTriage)" if prefix else
+                 "sharded (syzkaller_amd/shard.py ShardedTriage + sg_shard.hip)"),
         "gen_s": round(t_gen, 2),
     }
 

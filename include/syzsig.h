@@ -150,7 +150,7 @@ int sg_shard_of(uint32_t s, uint32_t nshards);
  * first record}, grouped by owning shard: shard k's pairs are pairs
  * d_shard_off[k] .. d_shard_off[k+1]-1 of d_pairs (u32 pairs, capacity nvals
  * pairs; d_shard_off: G+1 device u64).  The snapshot is only read.  Any
- * number of entries (record slices of < 2^31 entries each). */
+ * number of entries (record slices of < 2^30 entries each). */
 int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_vals, const uint64_t* d_rec_off,
 			    uint64_t nvals, uint64_t nrec, uint64_t rec_base, uint32_t nshards, uint32_t* d_pairs,
 			    uint64_t* d_shard_off);
@@ -169,6 +169,12 @@ int sg_shard_flags_dev(sg_ctx* ctx, const uint32_t* d_bits, uint32_t nparts, uin
 /* SignalAdd of n device-resident values (fuzzer.go:673-674 for the new signal
  * every shard found). */
 int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
+/* Bitmap prefix exchange of the prefix protocol (syzkaller_amd/shard.py
+ * PrefixTriage): d_parts holds nparts bitmap slices of `words` u32 words each,
+ * part k from rank k.  d_prefix[k] = OR of parts 0..k-1 (part 0: zero),
+ * d_total = OR of all parts.  RCCL has no bitwise-OR reduction. */
+int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
+			    uint32_t* d_total);
 
 /* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:
  * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */

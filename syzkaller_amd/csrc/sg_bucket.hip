@@ -1732,6 +1732,17 @@ __global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t 
 // the sequential loop (fuzzer.go:665) cut between two records sees the same
 // maxSignal at every record.  The rebased offsets of a slice live in a
 // grow-only context buffer.
+static int read_off(sg_ctx* ctx, const uint64_t* d_off, uint64_t r, uint64_t* v) {
+  SG_HIP(hipMemcpyAsync(v, d_off + r, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+// Entries per launch above which a batch is cut into record slices: about one
+// C2 batch.  Twice that makes the (b2, b1) buckets twice as large, and a
+// tenth of them overflow the LDS candidate map into the slow spill kernel.
+constexpr uint64_t kSliceEntries = 1ull << 30;
+
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
                   uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
   if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
@@ -1740,7 +1751,7 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   }
   if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
   const uint64_t m = ctx->max_launch_recs;
-  if (nrec <= m) return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new);
+  if (nrec <= m && n <= kSliceEntries) return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new);
   if (ctx->slice_off_cap < m + 1) {
     SG_HIP(hipStreamSynchronize(ctx->stream));
     if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
@@ -1750,16 +1761,39 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     ctx->slice_off_cap = m + 1;
   }
   uint64_t* roff = ctx->slice_off;
-  for (uint64_t r0 = 0; r0 < nrec; r0 += m) {
-    const uint64_t r1 = nrec - r0 < m ? nrec : r0 + m;
-    uint64_t e[2] = {0, 0};
-    SG_HIP(hipMemcpyAsync(&e[0], d_off + r0, 8, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipMemcpyAsync(&e[1], d_off + r1, 8, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1,
-                       e[0], roff);
-    const int rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e[0], roff, e[1] - e[0], r1 - r0, d_rec_new + r0);
+  uint64_t e0 = 0;
+  int rc = read_off(ctx, d_off, 0, &e0);
+  if (rc) return rc;
+  for (uint64_t r0 = 0; r0 < nrec;) {
+    // record slices: <= m records, and <= kSliceEntries entries unless one
+    // record alone holds more.  The sequential loop (fuzzer.go:665) cut
+    // between two records sees the same maxSignal at every record.
+    uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
+    rc = read_off(ctx, d_off, r1, &e1);
     if (rc) return rc;
+    if (e1 - e0 > kSliceEntries) {  // largest r1 > r0 with e1 - e0 <= kSliceEntries (at least one record)
+      uint64_t lo = r0 + 1, hi = r1;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) / 2;
+        uint64_t em = 0;
+        rc = read_off(ctx, d_off, mid, &em);
+        if (rc) return rc;
+        if (em - e0 <= kSliceEntries)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      r1 = lo;
+      rc = read_off(ctx, d_off, r1, &e1);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1, e0,
+                       roff);
+    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e0, roff, e1 - e0, r1 - r0, d_rec_new + r0);
+    if (rc) return rc;
+    SG_HIP(hipStreamSynchronize(ctx->stream));  // the next slice's offsets overwrite roff
+    r0 = r1;
+    e0 = e1;
   }
   return SG_OK;
 }

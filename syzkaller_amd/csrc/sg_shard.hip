@@ -191,6 +191,20 @@ __global__ void k_set_add_vals(uint32_t* __restrict__ words, const uint32_t* __r
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sgd::set_bit(words, v[i]);
 }
 
+// exclusive prefix-OR over the parts, word by word, and the total
+__global__ void k_prefix_or(const uint32_t* __restrict__ parts, uint32_t nparts, uint64_t words,
+                            uint32_t* __restrict__ prefix, uint32_t* __restrict__ total) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += stride) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < nparts; k++) {
+      prefix[(uint64_t)k * words + w] = acc;
+      acc |= parts[(uint64_t)k * words + w];
+    }
+    total[w] = acc;
+  }
+}
+
 __global__ void k_rebase_off(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = off[i] - base;
@@ -359,6 +373,23 @@ int sg_shard_flags_dev(sg_ctx* ctx, const uint32_t* d_bits, uint32_t nparts, uin
   ScopedTimer tm(ctx, "shard_flags");
   hipLaunchKernelGGL(k_shard_flags, dim3(div_up(nrec, 256)), dim3(256), 0, ctx->stream, d_bits, nparts,
                      words_per_part, rec_lo, nrec, d_rec_new);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
+                            uint32_t* d_total) {
+  if (!ctx || nparts == 0 || (words && (!d_parts || !d_prefix || !d_total))) {
+    set_error("sg_bitmap_prefix_or_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  if (words == 0) return SG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "prefix_or");
+  hipLaunchKernelGGL(k_prefix_or, dim3(std::min<uint64_t>(div_up(words, 256), 16384)), dim3(256), 0, ctx->stream,
+                     d_parts, nparts, words, d_prefix, d_total);
   SG_HIP(hipGetLastError());
   return SG_OK;
 }

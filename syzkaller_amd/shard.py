@@ -27,10 +27,12 @@ product; the CPU tests drive the same protocol with a numpy restatement of the
 stages over gloo (tests/test_shard.py).  Collectives run on device tensors
 under RCCL ("nccl"); under gloo they are staged through host memory.
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
 
-from ._lib import call
+from ._lib import call, lib
 
 
 class Comm:
@@ -75,6 +77,33 @@ class Comm:
         recv = torch.empty(sum(recv_splits), dtype=send.dtype, device="cpu" if self.host else dev)
         dist.all_to_all_single(recv, self._stage(send[: sum(send_splits)]), recv_splits, send_splits, group=self.group)
         return recv.to(dev) if self.host else recv
+
+    def all_to_all_equal(self, out, t):
+        """Dense all_to_all_single: part k of t (equal parts) goes to rank k,
+        out's part j comes from rank j."""
+        if self.world == 1:
+            out.copy_(t)
+            return out
+        if self.host:
+            o = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_to_all_single(o, self._stage(t), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, t, group=self.group)
+        return out
+
+    def all_gather_equal(self, out, t):
+        """out = the t of every rank, concatenated in rank order."""
+        if self.world == 1:
+            out.copy_(t)
+            return out
+        if self.host:
+            o = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_gather(list(o.view(self.world, -1).unbind(0)), self._stage(t), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
 
     def all_gather_var(self, t, n):
         """The first n elements of t from every rank, concatenated."""
@@ -124,6 +153,56 @@ class HipStages:
     def add(self, sset, vals, n):
         if n:
             call("sg_set_add_dev", sset.h, vals.data_ptr(), n)
+
+    # the prefix protocol's stages (PrefixTriage)
+    words = 1 << 27  # a set's 2^32-bit bitmap
+
+    def new_set(self):
+        from .cover import SignalSet
+
+        return SignalSet(self.ctx)
+
+    def wrap(self, t):
+        """A set over the first 2^27 words of the int32 device tensor t."""
+        return _WrappedSet(self.ctx, t)
+
+    def copy(self, dst, src):
+        call("sg_set_copy", dst.h, src.h)
+
+    def clear(self, sset):
+        call("sg_set_clear", sset.h)
+
+    def or_words(self, sset, t):
+        call("sg_set_or_dev", sset.h, ctypes.c_void_p(t.data_ptr()))
+
+    def prefix_or(self, parts, nparts, words, prefix, total):
+        call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
+             total.data_ptr())
+
+    def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
+        call("sg_triage_batch_dev", self.ctx.h, maxset.h, newset.h if newset is not None else None,
+             vals.data_ptr() if nvals else None, off.data_ptr(), nvals, nrec, rec_new.data_ptr() if nrec else None,
+             None, None)
+
+
+class _WrappedSet:
+    """sg_set_wrap_dev over a torch tensor (kept alive with the handle)."""
+
+    def __init__(self, ctx, t):
+        h = ctypes.c_void_p()
+        call("sg_set_wrap_dev", ctx.h, ctypes.c_void_p(t.data_ptr()), ctypes.byref(h))
+        self.h, self.t = h, t
+
+    def close(self):
+        if self.h:
+            lib.sg_set_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ShardedTriage:
@@ -189,3 +268,72 @@ class ShardedTriage:
                      "nrec_total": nrec_total}
         return nrec_total
 
+
+
+class PrefixTriage:
+    """fuzzer.go:645-693 over one batch whose call records are split
+    contiguously across the ranks of `comm` (rank order = record order), by
+    bitmap prefixes instead of candidate pairs:
+
+      1. C_k = the signal of rank k's records not in M0 (the replicated
+         maxSignal): rank k's local triage against a copy of M0, its newSignal
+         output (its flags are not used).
+      2. P_k = OR of C_j over ranks j < k, T = OR of every C_j: all-to-all of
+         bitmap slices, an exclusive prefix-OR per slice on the owning rank
+         (sg_bitmap_prefix_or_dev; RCCL has no bitwise OR), all-to-all of the
+         prefixes back, all-gather of the totals.
+      3. The local triage of rank k's records against M0 | P_k.  M0 | P_k is
+         the sequential loop's maxSignal before rank k's first record (P_k is
+         the new signal of every earlier record), and within the rank the
+         local triage is the loop itself, so the flags are the loop's.
+      4. maxSignal = M0 | T and newSignal |= T on every rank.
+    Per rank and step the exchange moves about 2.5 bitmaps (512 MiB each)
+    whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
+    rank it is the plain local triage.  Stage contracts: HipStages."""
+
+    def __init__(self, stages, comm=None, device="cuda"):
+        self.st = stages
+        self.comm = comm if comm is not None else Comm()
+        self.device = device
+        G, W = self.comm.world, stages.words
+        self.S = -(-W // G)  # words per slice (the last slice padded)
+        n = self.S * G
+        if G > 1:
+            self.C = torch.zeros(n, dtype=torch.int32, device=device)
+            self.P = torch.zeros(n, dtype=torch.int32, device=device)
+            self.T = torch.zeros(n, dtype=torch.int32, device=device)
+            self.recv = torch.empty(n, dtype=torch.int32, device=device)
+            self.pref = torch.empty(n, dtype=torch.int32, device=device)
+            self.tot = torch.empty(self.S, dtype=torch.int32, device=device)
+            self.cset = stages.wrap(self.C)
+            self.work = stages.new_set()
+        self.last = {}
+
+    def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new):
+        """Same contract as ShardedTriage.step."""
+        c, st, G = self.comm, self.st, self.comm.world
+        ranges = c.all_gather_i64([rec_base, nrec])
+        nrec_total = max(rb + n for rb, n in ranges)
+        if G == 1:
+            st.triage(maxsig, newsig, vals, off, nvals, nrec, rec_new)
+            self.last = {"nrec_total": nrec_total, "exchange_bytes": 0}
+            return nrec_total
+        # 1. this rank's new signal against M0
+        st.copy(self.work, maxsig)
+        st.clear(self.cset)
+        st.triage(self.work, self.cset, vals, off, nvals, nrec, rec_new)
+        # 2. exclusive prefix and total over the ranks, slice by slice
+        c.all_to_all_equal(self.recv, self.C)
+        st.prefix_or(self.recv, G, self.S, self.pref, self.tot)
+        c.all_to_all_equal(self.P, self.pref)
+        c.all_gather_equal(self.T, self.tot)
+        # 3. the flags against M0 | P_k
+        st.copy(self.work, maxsig)
+        st.or_words(self.work, self.P)
+        st.triage(self.work, None, vals, off, nvals, nrec, rec_new)
+        # 4. the replicated state after the whole batch
+        st.or_words(maxsig, self.T)
+        if newsig is not None:
+            st.or_words(newsig, self.T)
+        self.last = {"nrec_total": nrec_total, "exchange_bytes": 4 * self.S * (3 * (G - 1))}
+        return nrec_total

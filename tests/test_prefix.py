@@ -1,0 +1,156 @@
+"""The bitmap-prefix one-batch triage protocol (syzkaller_amd/shard.py
+PrefixTriage) on CPU: world size 2 and 4 over gloo, with the stages restated
+in numpy from their contracts (sg_triage_batch_dev, sg_set_copy/clear/or_dev,
+sg_bitmap_prefix_or_dev) over a 2^20-signal bitmap (the protocol is word-wise,
+so a smaller signal space exercises it fully; the full 2^32 space runs on the
+GPU in tests/test_shard_gpu.py).  The flags of every record and the final
+maxSignal / newSignal must equal the single-rank oracle's sequential loop
+(syz-fuzzer/fuzzer.go:645-693) over the whole batch in record order."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.test_shard import _free_port, split
+
+BITS = 20
+WORDS = 1 << (BITS - 5)
+
+
+class BitSet:
+    """A signal set as a bitmap of WORDS uint32 words (bit s & 31 of word s >> 5)."""
+
+    def __init__(self, w=None):
+        self.w = np.zeros(WORDS, np.uint32) if w is None else w
+
+    def has(self, s):
+        s = np.asarray(s, dtype=np.uint64)
+        return ((self.w[s >> np.uint64(5)] >> (s & np.uint64(31)).astype(np.uint32)) & 1).astype(bool)
+
+    def add(self, s):
+        s = np.asarray(s, dtype=np.uint64)
+        np.bitwise_or.at(self.w, s >> np.uint64(5), (np.uint32(1) << (s & np.uint64(31)).astype(np.uint32)))
+
+    def export(self):
+        i = np.nonzero(np.unpackbits(self.w.view(np.uint8), bitorder="little"))[0]
+        return i.astype(np.uint32).tolist()
+
+
+class NumpyPrefixStages:
+    words = WORDS
+
+    def new_set(self):
+        return BitSet()
+
+    def wrap(self, t):
+        return BitSet(t.numpy().view(np.uint32)[:WORDS])
+
+    def copy(self, dst, src):
+        dst.w[:] = src.w
+
+    def clear(self, s):
+        s.w[:] = 0
+
+    def or_words(self, s, t):
+        s.w |= t.numpy().view(np.uint32)[:WORDS]
+
+    def prefix_or(self, parts, nparts, words, prefix, total):
+        p = parts.numpy().view(np.uint32)[: nparts * words].reshape(nparts, words)
+        pre = prefix.numpy().view(np.uint32)[: nparts * words].reshape(nparts, words)
+        acc = np.zeros(words, np.uint32)
+        for k in range(nparts):
+            pre[k] = acc
+            acc = acc | p[k]
+        total.numpy().view(np.uint32)[:words] = acc
+
+    def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
+        """The sequential loop (fuzzer.go:665-690) restated over bitmaps."""
+        v = vals[:nvals].numpy().view(np.uint32)
+        o = off.numpy().astype(np.int64)
+        for r in range(nrec):
+            sig = v[o[r]:o[r + 1]]
+            new = sig[~maxset.has(sig)] if sig.size else sig
+            rec_new[r] = 1 if new.size else 0
+            if new.size:
+                maxset.add(new)
+                if newset is not None:
+                    newset.add(new)
+
+
+def batch(seed, nrec):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 30, size=nrec)
+    lens[rng.integers(0, nrec, size=nrec // 4)] = 0
+    vals = rng.integers(0, 3000, size=int(lens.sum())).astype(np.uint32)
+    if vals.size > 10:
+        vals[rng.integers(0, vals.size, size=5)] = (1 << BITS) - 1
+        vals[rng.integers(0, vals.size, size=5)] = 0
+        vals[-3:] = rng.integers(0, 1 << BITS, size=3).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    return vals, off
+
+
+M0 = np.arange(0, 3000, 5, dtype=np.uint32)
+BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from syzkaller_amd.shard import Comm, PrefixTriage
+
+        tri = PrefixTriage(NumpyPrefixStages(), Comm(), device="cpu")
+        ms, ns = BitSet(), BitSet()
+        ms.add(M0)
+        out = []
+        for seed, nrec in BATCHES:
+            vals, off = batch(seed, nrec)
+            r0, r1 = split(nrec, world, seed)[rank]
+            e0, e1 = int(off[r0]), int(off[r1])
+            v = torch.from_numpy(vals[e0:e1].view(np.int32).copy())
+            o = torch.from_numpy((off[r0:r1 + 1] - off[r0]).astype(np.int64))
+            rec_new = torch.zeros(max(r1 - r0, 1), dtype=torch.uint8)
+            total = tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new)
+            assert total == nrec
+            out.append((r0, rec_new[: r1 - r0].tolist()))
+        q.put((rank, out, ms.export(), ns.export()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_prefix_triage_equals_sequential_loop(world):
+    from oracle import pyoracle as O
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out, m, n = q.get(timeout=240)
+        res[r] = (out, m, n)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    om, on = O.OSet(M0), O.OSet()
+    for b, (seed, nrec) in enumerate(BATCHES):
+        vals, off = batch(seed, nrec)
+        ef = O.triage_flags_only(om, on, vals, off)
+        got = np.zeros(nrec, np.uint8)
+        for r in range(world):
+            r0, fl = res[r][0][b]
+            got[r0:r0 + len(fl)] = fl
+        assert np.array_equal(got, ef), (world, seed)
+        if nrec > 100:
+            assert 0 < ef.sum() < nrec  # mixed flags
+    for r in range(world):  # the replicated state is the sequential loop's on every rank
+        assert res[r][1] == om.export().tolist()
+        assert res[r][2] == on.export().tolist()

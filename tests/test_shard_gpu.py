@@ -132,13 +132,13 @@ def test_shard_owners_and_flags_vs_numpy(ctx):
         assert np.array_equal(got.cpu().numpy(), exp.numpy()), (rec_lo, nrec)
 
 
-def _run_protocol(ctx_dev, world, rank, batches, m0):
+def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
     from syzkaller_amd import cover as C
-    from syzkaller_amd.shard import Comm, HipStages, ShardedTriage
+    from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
     from tests.test_shard import split
 
     ctx = C.Context(ctx_dev)
-    tri = ShardedTriage(HipStages(ctx), Comm())
+    tri = (PrefixTriage if proto == "prefix" else ShardedTriage)(HipStages(ctx), Comm())
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
     C.SignalAdd(ms, m0)
     out = []
@@ -170,8 +170,9 @@ def _expected():
     return flags, om.export().tolist(), on.export().tolist()
 
 
-def test_sharded_protocol_one_rank_vs_oracle(ctx):
-    out, m, n = _run_protocol(0, 1, 0, BATCHES, M0)
+@pytest.mark.parametrize("proto", ["pairs", "prefix"])
+def test_sharded_protocol_one_rank_vs_oracle(ctx, proto):
+    out, m, n = _run_protocol(0, 1, 0, BATCHES, M0, proto)
     ef, em, en = _expected()
     for b, (r0, fl) in enumerate(out):
         assert np.array_equal(np.array(fl, np.uint8), ef[b]), b
@@ -188,26 +189,27 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, proto):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _run_protocol(0, world, rank, BATCHES, M0)))
+        q.put((rank, _run_protocol(0, world, rank, BATCHES, M0, proto)))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_sharded_protocol_two_ranks_one_gpu():
+@pytest.mark.parametrize("proto", ["pairs", "prefix"])
+def test_sharded_protocol_two_ranks_one_gpu(proto):
     import torch.multiprocessing as mp
 
     world = 2
     port = _free_port()
     mctx = mp.get_context("spawn")
     q = mctx.Queue()
-    procs = [mctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [mctx.Process(target=_worker, args=(r, world, port, q, proto)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
