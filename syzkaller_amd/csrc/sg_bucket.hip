@@ -1493,33 +1493,22 @@ static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
   return grid;
 }
 
-// One launch sequence over a batch of <= kMaxGroups groups (rec_new zeroed).
-// With `emit`, the bucket stage writes the distinct candidates instead of
-// flagging records and updating the sets (mwords is then only read).  The
-// launch's scratch starts at workspace offset ws_base (reserved by the caller
-// when ws_base != 0).
-static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
-                             const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new,
-                             const EmitArgs* emit = nullptr, size_t ws_base = 0) {
-  if (n == 0) return SG_OK;
-  if (nrec == 0) {
-    set_error("bucket triage: signal entries without records");
-    return SG_EINVAL;
-  }
-  BucketPlan bp(n, nrec);
+// Stage A of one partitioned launch: tiles, both partition passes, the
+// bucket descriptors and the list of non-empty buckets, in the workspace from
+// ws_base (reserved by the caller when `reserved`).  n > 0, nrec > 0.
+static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n, uint64_t nrec,
+                         size_t ws_base, bool reserved, BucketPlan& bp) {
   if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
     set_error("bucket triage: batch too large");
     return SG_EINVAL;
   }
-  int rc = ws_base ? SG_OK : ws_reserve(ctx, bp.p.total);
+  int rc = reserved ? SG_OK : ws_reserve(ctx, ws_base + bp.p.total);
   if (rc) return rc;
-  if (ws_base) {
-    if (ctx->ws_cap < ws_base + bp.p.total) {
-      set_error("bucket triage: workspace not reserved");
-      return SG_EINVAL;
-    }
-    bp.rebase(ws_base);
+  if (ctx->ws_cap < ws_base + bp.p.total) {
+    set_error("bucket triage: workspace not reserved");
+    return SG_EINVAL;
   }
+  bp.rebase(ws_base);
   uint32_t* tstart = (uint32_t*)ws_at(ctx, bp.oTS);
   uint32_t* trec = (uint32_t*)ws_at(ctx, bp.oTR);
   uint32_t* gt = (uint32_t*)ws_at(ctx, bp.oGT);
@@ -1538,8 +1527,7 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   uint32_t* hist2 = (uint32_t*)ws_at(ctx, bp.oH2);
   uint32_t* goff2 = (uint32_t*)ws_at(ctx, bp.oO2);
   uint32_t* v2 = (uint32_t*)ws_at(ctx, bp.oV2);
-  uint32_t* nspill = (uint32_t*)ws_at(ctx, bp.oSP);
-  uint32_t* scr = (uint32_t*)ws_at(ctx, bp.oSC);
+    uint32_t* scr = (uint32_t*)ws_at(ctx, bp.oSC);
   const uint32_t T = (uint32_t)bp.T, G = (uint32_t)bp.gmax, NG = (uint32_t)bp.NG;
   const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
 
@@ -1613,6 +1601,34 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
     ScopedTimer tm(ctx, "p2_scatter");
     hipLaunchKernelGGL(k_p2_scatter, dim3(G), dim3(kPThreads), 0, ctx->stream, a2);
   }
+  hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
+                     gcount, (const uint32_t*)cfirst, bdesc);
+  hipLaunchKernelGGL(k_bucket_groups, dim3(div_up((uint64_t)kNumBuckets * NG, 256)), dim3(256), 0, ctx->stream,
+                     (const uint32_t*)goff2, gcount, (const uint32_t*)cbase, NG, gbnd);
+  uint32_t* bnz = (uint32_t*)ws_at(ctx, bp.oBN);
+  uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
+  hipLaunchKernelGGL(k_bucket_nz, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc, bnz);
+  rc = scan32(ctx, bnz, blpos, kNumBuckets, scr);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_bucket_compact, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc,
+                     (const uint32_t*)blpos, (uint32_t*)ws_at(ctx, bp.oLB), (uint4*)ws_at(ctx, bp.oLQ));
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+// Stage B: the bucket kernels over stage A's buckets (bp rebased by stage A):
+// flags and set updates, or (emit) the candidate pairs.
+static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new,
+                       const EmitArgs* emit, uint64_t n, uint64_t nrec) {
+  const uint32_t NG = (uint32_t)bp.NG;
+  const uint32_t* cbase = (const uint32_t*)ws_at(ctx, bp.oCB);
+  const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
+  uint4* bdesc = (uint4*)ws_at(ctx, bp.oBD);
+  uint32_t* gbnd = (uint32_t*)ws_at(ctx, bp.oGB);
+  uint32_t* v2 = (uint32_t*)ws_at(ctx, bp.oV2);
+  uint32_t* nspill = (uint32_t*)ws_at(ctx, bp.oSP);
+  uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
+  const bool dbg = ctx->debug_part;
   BucketArgs ba{};
   ba.in = v2;
   ba.bdesc = bdesc;
@@ -1639,17 +1655,6 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   }
   SG_HIP(hipMemsetAsync(ba.ticket, 0, 4, ctx->stream));
   SG_HIP(hipMemsetAsync(nspill, 0, 4, ctx->stream));
-  hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
-                     gcount, (const uint32_t*)cfirst, bdesc);
-  hipLaunchKernelGGL(k_bucket_groups, dim3(div_up((uint64_t)kNumBuckets * NG, 256)), dim3(256), 0, ctx->stream,
-                     (const uint32_t*)goff2, gcount, (const uint32_t*)cbase, NG, gbnd);
-  uint32_t* bnz = (uint32_t*)ws_at(ctx, bp.oBN);
-  uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
-  hipLaunchKernelGGL(k_bucket_nz, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc, bnz);
-  rc = scan32(ctx, bnz, blpos, kNumBuckets, scr);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_bucket_compact, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc,
-                     (const uint32_t*)blpos, (uint32_t*)ws_at(ctx, bp.oLB), (uint4*)ws_at(ctx, bp.oLQ));
   ba.blist_b = (const uint32_t*)ws_at(ctx, bp.oLB);
   ba.blist_q = (const uint4*)ws_at(ctx, bp.oLQ);
   ba.nlist = blpos + kNumBuckets;
@@ -1720,6 +1725,50 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
             (t1 - t0) / 100.0, dur.front(), dur[dur.size() / 2], dur.back(), (unsigned long long)maxr);
   }
   return SG_OK;
+}
+
+// One launch sequence over a batch of <= kMaxGroups groups (rec_new zeroed).
+// With `emit`, the bucket stage writes the distinct candidates instead of
+// flagging records and updating the sets (mwords is then only read).  The
+// launch's scratch starts at workspace offset ws_base (reserved by the caller
+// when ws_base != 0).
+static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
+                             const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new,
+                             const EmitArgs* emit = nullptr, size_t ws_base = 0) {
+  if (n == 0) return SG_OK;
+  if (nrec == 0) {
+    set_error("bucket triage: signal entries without records");
+    return SG_EINVAL;
+  }
+  BucketPlan bp(n, nrec);
+  int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp);
+  if (rc) return rc;
+  return buckets_one(ctx, bp, mwords, nwords, d_rec_new, emit, n, nrec);
+}
+
+// Marks: nwords |= every signal of stage A's buckets that is not in mwords
+// (a workgroup per bucket: its maxSignal slice in LDS, its newSignal words
+// written by it alone).
+__global__ __launch_bounds__(512) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
+                                                     const uint32_t* __restrict__ mwords,
+                                                     uint32_t* __restrict__ nwords) {
+  __shared__ uint32_t mslice[kBucketWords];
+  __shared__ uint32_t nbits[kBucketWords];
+  const uint32_t b = blockIdx.x;
+  const uint4 q = bdesc[b];
+  if (q.x >= q.y) return;
+  for (uint32_t i = threadIdx.x; i < kBucketWords; i += blockDim.x) {
+    mslice[i] = mwords[bucket_word(b, i)];
+    nbits[i] = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = q.x + threadIdx.x; i < q.y; i += blockDim.x) {
+    const uint32_t sl = __builtin_nontemporal_load(in + i) >> 16;
+    if (!((mslice[sl >> 5] >> (sl & 31)) & 1u)) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kBucketWords; i += blockDim.x)
+    if (nbits[i]) nwords[bucket_word(b, i)] |= nbits[i];
 }
 
 __global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
@@ -1794,6 +1843,112 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     SG_HIP(hipStreamSynchronize(ctx->stream));  // the next slice's offsets overwrite roff
     r0 = r1;
     e0 = e1;
+  }
+  return SG_OK;
+}
+
+// The record slices of a batch: <= max_launch_recs records and <=
+// kSliceEntries entries each (unless one record alone holds more).
+struct RecSlice {
+  uint64_t r0, r1, e0, e1;
+};
+static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
+  out.clear();
+  const uint64_t m = ctx->max_launch_recs;
+  uint64_t e0 = 0;
+  int rc = read_off(ctx, d_off, 0, &e0);
+  if (rc) return rc;
+  for (uint64_t r0 = 0; r0 < nrec;) {
+    uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
+    rc = read_off(ctx, d_off, r1, &e1);
+    if (rc) return rc;
+    if (e1 - e0 > kSliceEntries) {
+      uint64_t lo = r0 + 1, hi = r1;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) / 2;
+        uint64_t em = 0;
+        rc = read_off(ctx, d_off, mid, &em);
+        if (rc) return rc;
+        if (em - e0 <= kSliceEntries)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      r1 = lo;
+      rc = read_off(ctx, d_off, r1, &e1);
+      if (rc) return rc;
+    }
+    out.push_back({r0, r1, e0, e1});
+    r0 = r1;
+    e0 = e1;
+  }
+  return SG_OK;
+}
+
+// Two-phase triage (the prefix protocol, syzkaller_amd/shard.py): begin
+// partitions every record slice of the batch once, keeping the partitions in
+// the workspace, and marks the batch's signal that is not in `base`; end runs
+// the bucket stage of each kept slice in order against the caller's maxSignal.
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
+                 const uint64_t* d_off, uint64_t n, uint64_t nrec) {
+  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("prefix triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
+    return SG_EINVAL;
+  }
+  ctx->prefix_slices.clear();
+  ctx->prefix_open = false;
+  std::vector<RecSlice> sl;
+  int rc = nrec ? record_slices(ctx, d_off, nrec, sl) : SG_OK;
+  if (rc) return rc;
+  size_t total = 0;
+  for (const RecSlice& x : sl)
+    if (x.e1 > x.e0) total += align256(bucket_plan_bytes(x.e1 - x.e0, x.r1 - x.r0)) + align256((x.r1 - x.r0 + 1) * 8);
+  rc = ws_reserve(ctx, total ? total : 256);
+  if (rc) return rc;
+  size_t base = 0;
+  for (const RecSlice& x : sl) {
+    PrefixSlice ps{x.r0, x.r1, x.e0, x.e1, base};
+    if (x.e1 > x.e0) {
+      const uint64_t ns = x.e1 - x.e0, nr = x.r1 - x.r0;
+      BucketPlan bp(ns, nr);
+      const size_t roff_at = base + align256(bucket_plan_bytes(ns, nr));
+      uint64_t* roff = (uint64_t*)ws_at(ctx, roff_at);
+      hipLaunchKernelGGL(k_rebase, dim3(div_up(nr + 1, 256)), dim3(256), 0, ctx->stream, d_off + x.r0, nr + 1, x.e0,
+                         roff);
+      rc = partition_one(ctx, d_vals + x.e0, roff, ns, nr, base, true, bp);
+      if (rc) return rc;
+      {
+        ScopedTimer tm(ctx, "bucket_mark");
+        hipLaunchKernelGGL(k_bucket_mark, dim3(kNumBuckets), dim3(512), 0, ctx->stream,
+                           (const uint32_t*)ws_at(ctx, bp.oV2), (const uint4*)ws_at(ctx, bp.oBD), base_words,
+                           marks_words);
+      }
+      SG_HIP(hipGetLastError());
+      base = roff_at + align256((nr + 1) * 8);
+    }
+    ctx->prefix_slices.push_back(ps);
+  }
+  ctx->prefix_nrec = nrec;
+  ctx->prefix_open = true;
+  return SG_OK;
+}
+
+int prefix_end(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new) {
+  if (!ctx->prefix_open) {
+    set_error("prefix triage: no batch begun on this context");
+    return SG_EINVAL;
+  }
+  ctx->prefix_open = false;
+  if (ctx->prefix_nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, ctx->prefix_nrec, ctx->stream));
+  for (const PrefixSlice& x : ctx->prefix_slices) {
+    if (x.e1 == x.e0) continue;
+    const uint64_t ns = x.e1 - x.e0, nr = x.r1 - x.r0;
+    BucketPlan bp(ns, nr);
+    bp.rebase(x.ws_base);
+    const int rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new + x.r0, nullptr, ns, nr);
+    if (rc) return rc;
   }
   return SG_OK;
 }

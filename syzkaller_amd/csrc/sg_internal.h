@@ -53,6 +53,13 @@ struct KernelTimer {
 
 }  // namespace sg
 
+// one record slice of a two-phase (prefix) triage: records [r0, r1),
+// entries [e0, e1), its partition at workspace offset ws_base
+struct PrefixSlice {
+  uint64_t r0, r1, e0, e1;
+  size_t ws_base;
+};
+
 struct sg_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -75,6 +82,10 @@ struct sg_ctx {
   // tests of the record slicing) and diagnostics (SG_DEBUG_PART); the
   // environment is read once, at context creation
   uint64_t max_launch_recs = 0;
+  // two-phase triage state (prefix_begin / prefix_end, sg_bucket.hip)
+  std::vector<PrefixSlice> prefix_slices;
+  uint64_t prefix_nrec = 0;
+  bool prefix_open = false;
   bool debug_part = false;
   // rebased record offsets of one record slice (grow-only, owned)
   uint64_t* slice_off = nullptr;
@@ -178,6 +189,13 @@ struct EmitArgs {
 };
 // Workspace bytes of one partitioned launch over n entries / nrec records.
 size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
+// Two-phase triage (sg_bucket.hip): begin partitions the batch (kept in the
+// workspace) and ORs into marks_words its signal not in base_words; end
+// triages the kept partitions against mwords (flags, mwords / nwords updated).
+// Between the two only set operations may run on the context.
+int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
+                 const uint64_t* d_off, uint64_t n, uint64_t nrec);
+int prefix_end(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new);
 // One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch
 // at ws_base (reserved by the caller).
 int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,

@@ -179,6 +179,13 @@ class HipStages:
         call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
              total.data_ptr())
 
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec):
+        call("sg_prefix_begin_dev", self.ctx.h, base.h, marks.h, vals.data_ptr() if nvals else None, off.data_ptr(),
+             nvals, nrec)
+
+    def prefix_end(self, maxset, newset, rec_new):
+        call("sg_prefix_end_dev", self.ctx.h, maxset.h, newset.h if newset is not None else None, rec_new.data_ptr())
+
     def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
         call("sg_triage_batch_dev", self.ctx.h, maxset.h, newset.h if newset is not None else None,
              vals.data_ptr() if nvals else None, off.data_ptr(), nvals, nrec, rec_new.data_ptr() if nrec else None,
@@ -276,13 +283,14 @@ class PrefixTriage:
     bitmap prefixes instead of candidate pairs:
 
       1. C_k = the signal of rank k's records not in M0 (the replicated
-         maxSignal): rank k's local triage against a copy of M0, its newSignal
-         output (its flags are not used).
+         maxSignal): sg_prefix_begin_dev partitions rank k's records once
+         (kept for step 3) and marks that signal bucket by bucket.
       2. P_k = OR of C_j over ranks j < k, T = OR of every C_j: all-to-all of
          bitmap slices, an exclusive prefix-OR per slice on the owning rank
          (sg_bitmap_prefix_or_dev; RCCL has no bitwise OR), all-to-all of the
          prefixes back, all-gather of the totals.
-      3. The local triage of rank k's records against M0 | P_k.  M0 | P_k is
+      3. The local triage of rank k's records against M0 | P_k
+         (sg_prefix_end_dev, on the partitions of step 1).  M0 | P_k is
          the sequential loop's maxSignal before rank k's first record (P_k is
          the new signal of every earlier record), and within the rank the
          local triage is the loop itself, so the flags are the loop's.
@@ -318,10 +326,9 @@ class PrefixTriage:
             st.triage(maxsig, newsig, vals, off, nvals, nrec, rec_new)
             self.last = {"nrec_total": nrec_total, "exchange_bytes": 0}
             return nrec_total
-        # 1. this rank's new signal against M0
-        st.copy(self.work, maxsig)
+        # 1. this rank's new signal against M0 (its partitions kept for 3.)
         st.clear(self.cset)
-        st.triage(self.work, self.cset, vals, off, nvals, nrec, rec_new)
+        st.prefix_begin(maxsig, self.cset, vals, off, nvals, nrec)
         # 2. exclusive prefix and total over the ranks, slice by slice
         c.all_to_all_equal(self.recv, self.C)
         st.prefix_or(self.recv, G, self.S, self.pref, self.tot)
@@ -330,7 +337,7 @@ class PrefixTriage:
         # 3. the flags against M0 | P_k
         st.copy(self.work, maxsig)
         st.or_words(self.work, self.P)
-        st.triage(self.work, None, vals, off, nvals, nrec, rec_new)
+        st.prefix_end(self.work, None, rec_new)
         # 4. the replicated state after the whole batch
         st.or_words(maxsig, self.T)
         if newsig is not None:

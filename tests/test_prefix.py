@@ -1,9 +1,10 @@
 """The bitmap-prefix one-batch triage protocol (syzkaller_amd/shard.py
 PrefixTriage) on CPU: world size 2 and 4 over gloo, with the stages restated
-in numpy from their contracts (sg_triage_batch_dev, sg_set_copy/clear/or_dev,
-sg_bitmap_prefix_or_dev) over a 2^20-signal bitmap (the protocol is word-wise,
-so a smaller signal space exercises it fully; the full 2^32 space runs on the
-GPU in tests/test_shard_gpu.py).  The flags of every record and the final
+in numpy from their contracts (sg_triage_batch_dev, sg_prefix_begin_dev /
+sg_prefix_end_dev, sg_set_copy / clear / or_dev, sg_bitmap_prefix_or_dev) over
+a 2^20-signal bitmap (the protocol is word-wise, so a smaller signal space
+exercises it fully; the full 2^32 space runs on the GPU in
+tests/test_shard_gpu.py).  The flags of every record and the final
 maxSignal / newSignal must equal the single-rank oracle's sequential loop
 (syz-fuzzer/fuzzer.go:645-693) over the whole batch in record order."""
 import os
@@ -65,6 +66,16 @@ class NumpyPrefixStages:
             pre[k] = acc
             acc = acc | p[k]
         total.numpy().view(np.uint32)[:words] = acc
+
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec):
+        v = vals[:nvals].numpy().view(np.uint32)
+        if v.size:
+            marks.add(v[~base.has(v)])
+        self.kept = (vals, off, nvals, nrec)
+
+    def prefix_end(self, maxset, newset, rec_new):
+        vals, off, nvals, nrec = self.kept
+        self.triage(maxset, newset, vals, off, nvals, nrec, rec_new)
 
     def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
         """The sequential loop (fuzzer.go:665-690) restated over bitmaps."""

@@ -92,6 +92,39 @@ def test_shard_candidates_record_slices(C, monkeypatch):
     ctx2.close()
 
 
+def test_prefix_begin_end_equals_triage(C, monkeypatch):
+    """sg_prefix_begin_dev / sg_prefix_end_dev (the partitions kept between
+    the two calls, several record slices via a lowered per-launch record
+    limit) against sg_triage_batch_dev and the oracle: the marks are the
+    batch's signal not in the base set, and the flags and set updates after
+    end are the sequential loop's against the set passed to end."""
+    from syzkaller_amd.shard import HipStages
+
+    monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
+    ctx2 = C.Context(0)
+    st = HipStages(ctx2)
+    vals, off = _batch(305, 5000, hi=1 << 18)
+    m0 = np.unique(np.random.default_rng(306).integers(0, 1 << 18, size=20000)).astype(np.uint32)
+    extra = np.unique(np.random.default_rng(307).integers(0, 1 << 18, size=5000)).astype(np.uint32)
+    base, marks, ms, ns = C.SignalSet(ctx2), C.SignalSet(ctx2), C.SignalSet(ctx2), C.SignalSet(ctx2)
+    C.SignalAdd(base, m0)
+    C.SignalAdd(ms, np.union1d(m0, extra))  # end runs against base | extra (the prefix)
+    v, o = _dev(vals, np.int32), _dev(off, np.int64)
+    nrec = off.size - 1
+    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    st.prefix_begin(base, marks, v, o, vals.size, nrec)
+    st.prefix_end(ms, ns, rec_new)
+    torch.cuda.synchronize()
+    assert np.array_equal(marks.export(), np.setdiff1d(np.unique(vals), m0))
+    om, on = O.OSet(np.union1d(m0, extra)), O.OSet()
+    ef = O.triage_flags_only(om, on, vals, off)
+    assert np.array_equal(rec_new.cpu().numpy(), ef)
+    assert 0 < ef.sum() < nrec
+    assert np.array_equal(ms.export(), om.export()) and np.array_equal(ns.export(), on.export())
+    del base, marks, ms, ns
+    ctx2.close()
+
+
 @pytest.fixture(scope="module")
 def C(ctx):
     from syzkaller_amd import cover
