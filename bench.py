@@ -546,6 +546,8 @@ def main():
     ap.add_argument("--no-from-traces", dest="from_traces", action="store_false")
     ap.add_argument("--c3-proto", choices=["prefix", "pairs"], default="prefix",
                     help="C3 protocol: bitmap prefixes (default) or candidate pairs hash-sharded by signal")
+    ap.add_argument("--c3-two-phase", action="store_true",
+                    help="measurement: the prefix protocol's two-phase path at one rank too")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of single-thread CPU baseline work")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-cores CPU leg")
     ap.add_argument("--no-cpu", action="store_true")

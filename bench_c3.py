@@ -22,7 +22,7 @@ from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, kernel_table, n_un
 from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
-                                "set_add", "prefix_or", "set_or", "set_copy"]
+                                "set_add", "prefix_or", "bucket_mark"]
 
 
 def _max_over_ranks(x, world):
@@ -59,7 +59,10 @@ def run_c3(ctx, args, cfg, rank, world):
         dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device="cuda"))
         assert len({int(c.item()) for c in counts}) == 1, "maxSignal snapshots differ between ranks"
     prefix = getattr(args, "c3_proto", "prefix") == "prefix"
-    tri = (PrefixTriage if prefix else ShardedTriage)(HipStages(ctx), Comm())
+    if prefix:
+        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=getattr(args, "c3_two_phase", False))
+    else:
+        tri = ShardedTriage(HipStages(ctx), Comm())
     rec_base = rank * nprog * calls
 
     def step(b):

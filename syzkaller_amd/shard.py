@@ -299,14 +299,16 @@ class PrefixTriage:
     whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
     rank it is the plain local triage.  Stage contracts: HipStages."""
 
-    def __init__(self, stages, comm=None, device="cuda"):
+    def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False):
         self.st = stages
         self.comm = comm if comm is not None else Comm()
         self.device = device
+        # (measurement: run the two-phase path with its local exchange at one rank too)
+        self.two_phase_at_one = two_phase_at_one
         G, W = self.comm.world, stages.words
         self.S = -(-W // G)  # words per slice (the last slice padded)
         n = self.S * G
-        if G > 1:
+        if G > 1 or two_phase_at_one:
             self.C = torch.zeros(n, dtype=torch.int32, device=device)
             self.P = torch.zeros(n, dtype=torch.int32, device=device)
             self.T = torch.zeros(n, dtype=torch.int32, device=device)
@@ -322,7 +324,7 @@ class PrefixTriage:
         c, st, G = self.comm, self.st, self.comm.world
         ranges = c.all_gather_i64([rec_base, nrec])
         nrec_total = max(rb + n for rb, n in ranges)
-        if G == 1:
+        if G == 1 and not self.two_phase_at_one:
             st.triage(maxsig, newsig, vals, off, nvals, nrec, rec_new)
             self.last = {"nrec_total": nrec_total, "exchange_bytes": 0}
             return nrec_total
