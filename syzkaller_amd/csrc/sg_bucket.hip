@@ -633,6 +633,7 @@ struct BucketArgs {
   const uint32_t* gbnd;    // [bucket][group]: first bucket position of each group's entries
   uint32_t NG;             // groups
   uint32_t* mwords;        // maxSignal
+  const uint32_t* owords;  // nullable: the test is against mwords | owords (words that gain bits get both)
   uint32_t* nwords;        // newSignal (nullable)
   uint8_t* rec_new;        // per record: owns some new signal
   uint32_t* spill;         // buckets left for the direct-table kernel
@@ -814,7 +815,8 @@ __device__ __forceinline__ void bucket_round_load(const BucketArgs& a, uint32_t 
 __device__ __forceinline__ void bucket_pre_load(const BucketArgs& a, uint32_t b, BucketPre& P) {
   // LDS slice words kWPT tid .. + kWPT - 1
   const uint64_t w0 = bucket_word(b, kWPT * threadIdx.x);
-  const wvec m = *reinterpret_cast<const wvec*>(a.mwords + w0);
+  wvec m = *reinterpret_cast<const wvec*>(a.mwords + w0);
+  if (a.owords) m |= *reinterpret_cast<const wvec*>(a.owords + w0);
   wvec nw = {};
   if (a.nwords) nw = *reinterpret_cast<const wvec*>(a.nwords + w0);
 #pragma unroll
@@ -1240,7 +1242,8 @@ __global__ __launch_bounds__(kDThreads) void k_bucket_direct(BucketArgs a) {
     const uint32_t b = a.spill[job / kNQ], qq = job % kNQ;
     const uint4 q = a.bdesc[b];
     for (uint32_t i = tid; i < kQW; i += kDThreads) {
-      mpart[i] = a.mwords[bucket_word(b, qq * kQW + i)];
+      const uint64_t w = bucket_word(b, qq * kQW + i);
+      mpart[i] = a.mwords[w] | (a.owords ? a.owords[w] : 0u);
       nbits[i] = 0;
     }
     for (uint32_t i = tid; i < NG; i += kDThreads) gb[i] = a.gbnd[(uint64_t)b * NG + i];
@@ -1619,7 +1622,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
 // Stage B: the bucket kernels over stage A's buckets (bp rebased by stage A):
 // flags and set updates, or (emit) the candidate pairs.
 static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new,
-                       const EmitArgs* emit, uint64_t n, uint64_t nrec) {
+                       const EmitArgs* emit, uint64_t n, uint64_t nrec, const uint32_t* owords = nullptr) {
   const uint32_t NG = (uint32_t)bp.NG;
   const uint32_t* cbase = (const uint32_t*)ws_at(ctx, bp.oCB);
   const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
@@ -1635,6 +1638,7 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
   ba.gbnd = gbnd;
   ba.NG = NG;
   ba.mwords = mwords;
+  ba.owords = owords;
   ba.nwords = nwords;
   ba.rec_new = d_rec_new;
   ba.nspill = nspill;
@@ -1748,26 +1752,58 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
 
 // Marks: nwords |= every signal of stage A's buckets that is not in mwords
 // (a workgroup per bucket: its maxSignal slice in LDS, its newSignal words
-// written by it alone).
-__global__ __launch_bounds__(512) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
-                                                     const uint32_t* __restrict__ mwords,
-                                                     uint32_t* __restrict__ nwords) {
+// written by it alone).  Entries are read as 16-B quads from the bucket start
+// rounded down (the pass-2 buffer is padded), kMarkU quads per thread in
+// flight; the first ones are issued before the slice is installed.
+constexpr int kMarkT = 256, kMarkU = 2;
+__global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
+                                                        const uint32_t* __restrict__ mwords,
+                                                        uint32_t* __restrict__ nwords) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint4 q = bdesc[b];
   if (q.x >= q.y) return;
-  for (uint32_t i = threadIdx.x; i < kBucketWords; i += blockDim.x) {
-    mslice[i] = mwords[bucket_word(b, i)];
-    nbits[i] = 0;
+  constexpr uint32_t kStep = kMarkT * 4 * kMarkU;
+  auto load = [&](uint32_t base, v4u32 (&v)[kMarkU]) {
+#pragma unroll
+    for (int u = 0; u < kMarkU; u++) {
+      const uint32_t p = base + (u * kMarkT + tid) * 4;
+      v[u] = v4u32{0, 0, 0, 0};
+      if (p < q.y) v[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(in + p));
+    }
+  };
+  uint32_t base = q.x & ~3u;
+  v4u32 v[kMarkU];
+  load(base, v);
+  constexpr int kW = kBucketWords / kMarkT;  // slice words per thread
+  {
+    typedef uint32_t mvec __attribute__((ext_vector_type(kW)));
+    const uint64_t w0 = bucket_word(b, kW * tid);
+    reinterpret_cast<mvec*>(mslice)[tid] = *reinterpret_cast<const mvec*>(mwords + w0);
+    reinterpret_cast<mvec*>(nbits)[tid] = mvec{};
   }
   __syncthreads();
-  for (uint32_t i = q.x + threadIdx.x; i < q.y; i += blockDim.x) {
-    const uint32_t sl = __builtin_nontemporal_load(in + i) >> 16;
-    if (!((mslice[sl >> 5] >> (sl & 31)) & 1u)) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+  for (;;) {
+    const uint32_t next = base + kStep;
+    v4u32 y[kMarkU];
+    if (next < q.y) load(next, y);
+#pragma unroll
+    for (int u = 0; u < kMarkU; u++) {
+      const uint32_t p = base + (u * kMarkT + tid) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t sl = v[u][j] >> 16;
+        const bool live = p + j >= q.x && p + j < q.y;
+        if (live && !((mslice[sl >> 5] >> (sl & 31)) & 1u)) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+      }
+    }
+    if (next >= q.y) break;
+    base = next;
+    for (int u = 0; u < kMarkU; u++) v[u] = y[u];
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < kBucketWords; i += blockDim.x)
+  for (uint32_t i = tid; i < kBucketWords; i += kMarkT)
     if (nbits[i]) nwords[bucket_word(b, i)] |= nbits[i];
 }
 
@@ -1921,7 +1957,7 @@ int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words,
       if (rc) return rc;
       {
         ScopedTimer tm(ctx, "bucket_mark");
-        hipLaunchKernelGGL(k_bucket_mark, dim3(kNumBuckets), dim3(512), 0, ctx->stream,
+        hipLaunchKernelGGL(k_bucket_mark, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream,
                            (const uint32_t*)ws_at(ctx, bp.oV2), (const uint4*)ws_at(ctx, bp.oBD), base_words,
                            marks_words);
       }
@@ -1935,7 +1971,7 @@ int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words,
   return SG_OK;
 }
 
-int prefix_end(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new) {
+int prefix_end(sg_ctx* ctx, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new) {
   if (!ctx->prefix_open) {
     set_error("prefix triage: no batch begun on this context");
     return SG_EINVAL;
@@ -1947,7 +1983,7 @@ int prefix_end(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_n
     const uint64_t ns = x.e1 - x.e0, nr = x.r1 - x.r0;
     BucketPlan bp(ns, nr);
     bp.rebase(x.ws_base);
-    const int rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new + x.r0, nullptr, ns, nr);
+    const int rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new + x.r0, nullptr, ns, nr, owords);
     if (rc) return rc;
   }
   return SG_OK;

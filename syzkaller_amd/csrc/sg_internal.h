@@ -195,7 +195,7 @@ size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
 // Between the two only set operations may run on the context.
 int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec);
-int prefix_end(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new);
+int prefix_end(sg_ctx* ctx, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new);
 // One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch
 // at ws_base (reserved by the caller).
 int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,

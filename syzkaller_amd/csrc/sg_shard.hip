@@ -406,7 +406,7 @@ int sg_prefix_begin_dev(sg_ctx* ctx, sg_set* base, sg_set* marks, const uint32_t
   return prefix_begin(ctx, base->words, marks->words, d_vals, d_rec_off, nvals, nrec);
 }
 
-int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, uint8_t* d_rec_new) {
+int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig, uint8_t* d_rec_new) {
   if (!ctx || !maxsig || maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {
     set_error("sg_prefix_end_dev: invalid argument");
     return SG_EINVAL;
@@ -418,7 +418,7 @@ int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, uint8_t* d_re
     set_error("sg_prefix_end_dev: no flag buffer");
     return SG_EINVAL;
   }
-  return prefix_end(ctx, maxsig->words, newsig ? newsig->words : nullptr, d_rec_new);
+  return prefix_end(ctx, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new);
 }
 
 int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {

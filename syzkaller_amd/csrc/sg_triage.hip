@@ -599,37 +599,25 @@ int sg_accept_batch(sg_ctx* ctx, sg_set* corpus_sig, sg_set* corpus_cov, const u
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = check_alloc(ctx);
   if (rc) return rc;
-  WsPlan p;
-  size_t o[5];
-  size_t o_in = p.add(nv * 4), o_off = p.add((n + 1) * 8), o_flag = p.add(n);
-  size_t o_cv = p.add(nc * 4), o_co = p.add((n + 1) * 8);
-  scratch_plan(p, nv, o);
-  rc = ws_reserve(ctx, p.total);
+  // The NewInput loop (manager.go:907-911) is the fuzzer's new-signal loop
+  // with corpusSignal as the running set and no newSignal: the partitioned
+  // triage path.  The batch is staged in dstage (the workspace is the
+  // partition's).
+  const size_t b_in = (nv * 4 + 255) & ~size_t(255), b_off = ((n + 1) * 8 + 255) & ~size_t(255),
+               b_flag = (n + 255) & ~size_t(255), b_cv = (nc * 4 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_in + 2 * b_off + b_flag + b_cv + 256);
   if (rc) return rc;
-  Scratch s = scratch_bind(ctx, nv, o);
-  uint32_t* din = (uint32_t*)ws_at(ctx, o_in);
-  uint64_t* doff = (uint64_t*)ws_at(ctx, o_off);
-  uint8_t* dflag = (uint8_t*)ws_at(ctx, o_flag);
+  char* st = (char*)ctx->dstage;
+  uint32_t* din = (uint32_t*)st;
+  uint64_t* doff = (uint64_t*)(st + b_in);
+  uint8_t* dflag = (uint8_t*)(st + b_in + b_off);
   if (nv) SG_HIP(hipMemcpyAsync(din, sig_vals, nv * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(doff, sig_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemsetAsync(dflag, 0, n, ctx->stream));
-  uint32_t key_lo;
-  rc = owner_keys(ctx, n, &key_lo);
-  if (rc) return rc;
-  PipeArgs a{};
-  a.vals = din;
-  a.n = nv;
-  a.off = doff;
-  a.nseg = n;
-  a.filter = corpus_sig->words;
-  a.key_lo = key_lo;
-  a.seg_flag = dflag;
-  a.set_a = corpus_sig->words;  // corpusSignal ∪= S_k (manager.go:911)
-  rc = run_pipe(ctx, a, s);
+  rc = bucket_triage(ctx, corpus_sig->words, nullptr, din, doff, nv, n, dflag);
   if (rc) return rc;
   if (nc) {
-    uint32_t* dcv = (uint32_t*)ws_at(ctx, o_cv);
-    uint64_t* dco = (uint64_t*)ws_at(ctx, o_co);
+    uint32_t* dcv = (uint32_t*)(st + b_in + b_off + b_flag);
+    uint64_t* dco = (uint64_t*)(st + b_in + b_off + b_flag + b_cv);
     SG_HIP(hipMemcpyAsync(dcv, cov_vals, nc * 4, hipMemcpyHostToDevice, ctx->stream));
     SG_HIP(hipMemcpyAsync(dco, cov_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_add_flagged_segs, dim3(std::min<uint64_t>(div_up(nc, 256), 8192)), dim3(256), 0,

@@ -105,6 +105,14 @@ class Comm:
             dist.all_gather_into_tensor(out, t, group=self.group)
         return out
 
+    def start_all_gather_equal(self, out, t):
+        """all_gather_equal left running on RCCL's stream; wait() on the handle
+        orders the current stream after it (under gloo: done on return)."""
+        if self.world == 1 or self.host:
+            self.all_gather_equal(out, t)
+            return _Done()
+        return dist.all_gather_into_tensor(out, t, group=self.group, async_op=True)
+
     def all_gather_var(self, t, n):
         """The first n elements of t from every rank, concatenated."""
         if self.world == 1:
@@ -122,6 +130,11 @@ class Comm:
             dist.all_gather_into_tensor(out, buf, group=self.group)
         got = torch.cat([out[k * m: k * m + counts[k]] for k in range(self.world)])
         return got.to(dev) if self.host else got
+
+
+class _Done:
+    def wait(self):
+        pass
 
 
 class HipStages:
@@ -183,8 +196,10 @@ class HipStages:
         call("sg_prefix_begin_dev", self.ctx.h, base.h, marks.h, vals.data_ptr() if nvals else None, off.data_ptr(),
              nvals, nrec)
 
-    def prefix_end(self, maxset, newset, rec_new):
-        call("sg_prefix_end_dev", self.ctx.h, maxset.h, newset.h if newset is not None else None, rec_new.data_ptr())
+    def prefix_end(self, maxset, prefix, newset, rec_new):
+        """prefix: None or an int32 device tensor of >= 2^27 words (bitmap layout)."""
+        call("sg_prefix_end_dev", self.ctx.h, maxset.h, ctypes.c_void_p(prefix.data_ptr()) if prefix is not None
+             else None, newset.h if newset is not None else None, rec_new.data_ptr())
 
     def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
         call("sg_triage_batch_dev", self.ctx.h, maxset.h, newset.h if newset is not None else None,
@@ -290,11 +305,13 @@ class PrefixTriage:
          (sg_bitmap_prefix_or_dev; RCCL has no bitwise OR), all-to-all of the
          prefixes back, all-gather of the totals.
       3. The local triage of rank k's records against M0 | P_k
-         (sg_prefix_end_dev, on the partitions of step 1).  M0 | P_k is
-         the sequential loop's maxSignal before rank k's first record (P_k is
-         the new signal of every earlier record), and within the rank the
-         local triage is the loop itself, so the flags are the loop's.
-      4. maxSignal = M0 | T and newSignal |= T on every rank.
+         (sg_prefix_end_dev, on the partitions of step 1, reading P_k beside
+         maxSignal; the all-gather of T runs meanwhile).  M0 | P_k is the
+         sequential loop's maxSignal before rank k's first record (P_k is the
+         new signal of every earlier record), and within the rank the local
+         triage is the loop itself, so the flags are the loop's.
+      4. maxSignal = M0 | T and newSignal |= T on every rank (step 3 left
+         maxSignal between M0 and M0 | T).
     Per rank and step the exchange moves about 2.5 bitmaps (512 MiB each)
     whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
     rank it is the plain local triage.  Stage contracts: HipStages."""
@@ -316,7 +333,6 @@ class PrefixTriage:
             self.pref = torch.empty(n, dtype=torch.int32, device=device)
             self.tot = torch.empty(self.S, dtype=torch.int32, device=device)
             self.cset = stages.wrap(self.C)
-            self.work = stages.new_set()
         self.last = {}
 
     def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new):
@@ -335,12 +351,11 @@ class PrefixTriage:
         c.all_to_all_equal(self.recv, self.C)
         st.prefix_or(self.recv, G, self.S, self.pref, self.tot)
         c.all_to_all_equal(self.P, self.pref)
-        c.all_gather_equal(self.T, self.tot)
+        gather_t = c.start_all_gather_equal(self.T, self.tot)
         # 3. the flags against M0 | P_k
-        st.copy(self.work, maxsig)
-        st.or_words(self.work, self.P)
-        st.prefix_end(self.work, None, rec_new)
+        st.prefix_end(maxsig, self.P, None, rec_new)
         # 4. the replicated state after the whole batch
+        gather_t.wait()
         st.or_words(maxsig, self.T)
         if newsig is not None:
             st.or_words(newsig, self.T)

@@ -440,6 +440,26 @@ def test_accept_batch_vs_oracle(C):
         assert np.array_equal(cc.export(), ov.export())
 
 
+def test_accept_batch_groups_and_empty(C):
+    """sg_accept_batch runs the partitioned path: > 2^16 inputs (two record
+    groups), empty inputs, an all-empty batch, no coverage."""
+    rng = np.random.default_rng(115)
+    cs, oc = C.SignalSet(), O.OSet()
+    lens = rng.integers(0, 6, size=70_000)
+    lens[rng.integers(0, lens.size, size=5000)] = 0
+    so = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    sv = rng.integers(0, 1 << 18, size=int(so[-1])).astype(np.uint32)
+    sv[-1] = 0xFFFFFFFF
+    sums = []
+    for v, o in ((sv, so), (np.zeros(0, np.uint32), np.zeros(9, np.uint64)), (sv, so)):
+        acc = C.accept_batch(cs, None, v, o)
+        eacc = O.accept_batch(oc, None, v, o)
+        assert np.array_equal(acc, eacc)
+        assert np.array_equal(cs.export(), oc.export())
+        sums.append(int(eacc.sum()))
+    assert 0 < sums[0] < 70_000 and sums[1:] == [0, 0]
+
+
 def test_merge_poll_vs_oracle(C):
     rng = np.random.default_rng(114)
     mm, om = C.SignalSet(), O.OSet()

@@ -92,12 +92,25 @@ def test_shard_candidates_record_slices(C, monkeypatch):
     ctx2.close()
 
 
-def test_prefix_begin_end_equals_triage(C, monkeypatch):
+class _Words:
+    """A set's device words as the prefix argument of sg_prefix_end_dev."""
+
+    def __init__(self, s):
+        self.s = s
+
+    def data_ptr(self):
+        return self.s.device_words()
+
+
+@pytest.mark.parametrize("as_prefix", [False, True])
+def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix):
     """sg_prefix_begin_dev / sg_prefix_end_dev (the partitions kept between
     the two calls, several record slices via a lowered per-launch record
-    limit) against sg_triage_batch_dev and the oracle: the marks are the
-    batch's signal not in the base set, and the flags and set updates after
-    end are the sequential loop's against the set passed to end."""
+    limit) against the oracle: the marks are the batch's signal not in the
+    base set, and the flags after end are the sequential loop's against
+    maxsig | prefix.  Without a prefix maxsig / newsig end as the loop's; with
+    one, maxsig ends between M0 ∪ new and M0 ∪ prefix ∪ new, and is the loop's
+    after the prefix is ORed in."""
     from syzkaller_amd.shard import HipStages
 
     monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
@@ -108,20 +121,32 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch):
     extra = np.unique(np.random.default_rng(307).integers(0, 1 << 18, size=5000)).astype(np.uint32)
     base, marks, ms, ns = C.SignalSet(ctx2), C.SignalSet(ctx2), C.SignalSet(ctx2), C.SignalSet(ctx2)
     C.SignalAdd(base, m0)
-    C.SignalAdd(ms, np.union1d(m0, extra))  # end runs against base | extra (the prefix)
+    pre = C.SignalSet(ctx2)
+    if as_prefix:  # end runs against ms | pre = base | extra
+        C.SignalAdd(ms, m0)
+        C.SignalAdd(pre, extra)
+    else:
+        C.SignalAdd(ms, np.union1d(m0, extra))
     v, o = _dev(vals, np.int32), _dev(off, np.int64)
     nrec = off.size - 1
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
     st.prefix_begin(base, marks, v, o, vals.size, nrec)
-    st.prefix_end(ms, ns, rec_new)
+    st.prefix_end(ms, _Words(pre) if as_prefix else None, ns, rec_new)
     torch.cuda.synchronize()
     assert np.array_equal(marks.export(), np.setdiff1d(np.unique(vals), m0))
     om, on = O.OSet(np.union1d(m0, extra)), O.OSet()
     ef = O.triage_flags_only(om, on, vals, off)
     assert np.array_equal(rec_new.cpu().numpy(), ef)
     assert 0 < ef.sum() < nrec
-    assert np.array_equal(ms.export(), om.export()) and np.array_equal(ns.export(), on.export())
-    del base, marks, ms, ns
+    assert np.array_equal(ns.export(), on.export())
+    got = ms.export()
+    if as_prefix:
+        new = on.export()
+        assert np.isin(np.union1d(m0, new), got).all() and np.isin(got, np.union1d(om.export(), extra)).all()
+        ms.or_device(pre.device_words())
+        got = ms.export()
+    assert np.array_equal(got, om.export())
+    del base, marks, ms, ns, pre
     ctx2.close()
 
 
