@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, kernel_table, n_uniq, pmc_bytes_per_step, step_bytes,
-                   triage, HBM_PEAK_GBS, SignalSet, U32_WORDS, StepTimer)
+                   triage, HBM_PEAK_GBS, Context, SignalSet, U32_WORDS, StepTimer)
 from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
@@ -59,32 +59,65 @@ def run_c3(ctx, args, cfg, rank, world):
         dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device="cuda"))
         assert len({int(c.item()) for c in counts}) == 1, "maxSignal snapshots differ between ranks"
     prefix = getattr(args, "c3_proto", "prefix") == "prefix"
+    two_phase = getattr(args, "c3_two_phase", False)
+    # the prefix protocol's exchange: batches overlapped through PrefixTriage's
+    # two slots (batch i's bitmaps travel while batch i+1 is partitioned), the
+    # prefix-OR on a side stream of a second context
+    pipelined = prefix and (world > 1 or two_phase)
+    side_ctx = None
     if prefix:
-        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=getattr(args, "c3_two_phase", False))
+        side_st = side = None
+        if pipelined:
+            side = torch.cuda.Stream()
+            side_ctx = Context(ctx.device)
+            with torch.cuda.stream(side):
+                side_st = HipStages(side_ctx)
+        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=two_phase, side_stages=side_st, side_stream=side)
     else:
         tri = ShardedTriage(HipStages(ctx), Comm())
     rec_base = rank * nprog * calls
+    nrec_total = world * nprog * calls
+    # every step runs against the restored snapshot: overlapped steps use a
+    # maxSignal (and flag buffer) each
+    maxsigs = [maxsig, SignalSet(ctx)] if pipelined else [maxsig]
+    rec_news = [rec_new, torch.empty_like(rec_new)] if pipelined else [rec_new]
 
-    def step(b):
-        call("sg_set_copy", maxsig.h, m0set.h)
-        tri.step(maxsig, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
+    def run(bs):
+        pend = None
+        for i, b in enumerate(bs):
+            ms = maxsigs[i % len(maxsigs)]
+            call("sg_set_copy", ms.h, m0set.h)
+            if not pipelined:
+                tri.step(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
+                continue
+            p = tri.start(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_news[i % 2], nrec_total)
+            if pend is not None:
+                tri.finish(pend)
+            pend = p
+        if pend is not None:
+            tri.finish(pend)
 
-    for b in batches[: args.warmup]:
-        step(b)
+    run(batches[: args.warmup])
     torch.cuda.synchronize()
     timed = batches[args.warmup:]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.timing(True)
+    if side_ctx is not None:
+        side_ctx.timing(True)
     t0 = time.perf_counter()
-    for b in timed:
-        step(b)
+    run(timed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     kernels = kernel_table(ctx, SHARD_KERNELS, args.steps)
+    if side_ctx is not None:
+        side_kernels = kernel_table(side_ctx, ["prefix_or"], args.steps)
+        if "prefix_or" in side_kernels:
+            kernels["prefix_or"] = side_kernels["prefix_or"]
+        side_ctx.timing(False)
     ctx.timing(False)
     wall = _max_over_ranks(wall, world)
     units = _sum_over_ranks(sum(b.nvals for b in timed), world)
@@ -148,7 +181,8 @@ def run_c3(ctx, args, cfg, rank, world):
             "programs_per_gpu": nprog, "batch_programs": world * nprog, "calls": calls,
             "pcs_per_call": cfg["pcs_per_call"], "signal_per_step": units / args.steps,
             "maxsignal_start": m0_count, "queued_frac": acct["queued_frac"],
-            "parallelism": (f"record-sliced x{world}, bitmap-prefix exchange" if prefix else
+            "parallelism": (f"record-sliced x{world}, bitmap-prefix exchange"
+                            + (" overlapped with the next batch's partition" if pipelined else "") if prefix else
                             f"signal-sharded x{world}") + " (one rank per GPU, RCCL)",
         },
         "roofline": roof,

@@ -177,20 +177,21 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
 			    uint32_t* d_total);
 /* The two halves of sg_triage_batch_dev (flags and set updates, no diff) for
  * the prefix protocol.  Begin: the batch's partitions are built once and
- * kept in the context, and marks |= every signal of the batch not in base
- * (the local new signal, fuzzer.go:666).  End: the sequential loop
+ * kept in the context's slot (0 or 1: two batches can be kept, so one batch's
+ * exchange runs while the next is partitioned), and marks |= every signal of
+ * the batch not in base (the local new signal, fuzzer.go:666).  End: the sequential loop
  * (fuzzer.go:645-693) over the kept batch against maxsig | d_prefix (d_prefix:
  * nullable, 2^27 words in the set layout, e.g. another set's or an exchanged
  * bitmap), writing the flags of its nrec records to d_rec_new.  maxsig gains
  * the batch's new signal, and the words that gain bits also gain their
  * d_prefix bits (the prefix protocol ORs a superset of d_prefix into maxsig
- * afterwards); newsig (nullable) gains the new signal.  The batch's device
- * buffers must stay valid until end; between the two calls only set
- * operations (sg_set_copy, sg_set_or_dev, sg_set_clear) and
- * sg_bitmap_prefix_or_dev may run on the context. */
-int sg_prefix_begin_dev(sg_ctx* ctx, sg_set* base, sg_set* marks, const uint32_t* d_vals, const uint64_t* d_rec_off,
-			uint64_t nvals, uint64_t nrec);
-int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig, uint8_t* d_rec_new);
+ * afterwards); newsig (nullable) gains the new signal.  Only begin's launches
+ * read the batch's buffers; other calls may run on the context between begin
+ * and end (the slots have workspaces of their own).  End closes the slot. */
+int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks, const uint32_t* d_vals,
+			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec);
+int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
+		      uint8_t* d_rec_new);
 
 /* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:
  * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */

@@ -1927,22 +1927,62 @@ static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std:
 // the bucket stage of each kept slice in order against the caller's maxSignal.
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
+// The slot's workspace stands in for the context's during one call (the
+// partition code addresses the workspace through ctx->ws); grown to the exact
+// size, since it is kept.
+struct SlotWs {
+  sg_ctx* c;
+  PrefixSlot& s;
+  void* ws;
+  size_t cap;
+  SlotWs(sg_ctx* c_, PrefixSlot& s_) : c(c_), s(s_), ws(c_->ws), cap(c_->ws_cap) {
+    c->ws = s.ws;
+    c->ws_cap = s.ws_cap;
+  }
+  ~SlotWs() {
+    s.ws = c->ws;
+    s.ws_cap = c->ws_cap;
+    c->ws = ws;
+    c->ws_cap = cap;
+  }
+};
+
+static int slot_reserve(sg_ctx* ctx, PrefixSlot& s, size_t bytes) {
+  if (bytes <= s.ws_cap) return SG_OK;
+  const size_t cap = (bytes + (64u << 20) - 1) & ~size_t((64u << 20) - 1);
+  if (s.ws) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    SG_HIP(hipFree(s.ws));
+    s.ws = nullptr;
+    s.ws_cap = 0;
+  }
+  SG_HIP(hipMalloc(&s.ws, cap));
+  s.ws_cap = cap;
+  return SG_OK;
+}
+
+int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec) {
+  if (slot >= kPrefixSlots) {
+    set_error("prefix triage: slot %u out of range", slot);
+    return SG_EINVAL;
+  }
   if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
     set_error("prefix triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
     return SG_EINVAL;
   }
-  ctx->prefix_slices.clear();
-  ctx->prefix_open = false;
+  PrefixSlot& S = ctx->prefix[slot];
+  S.slices.clear();
+  S.open = false;
   std::vector<RecSlice> sl;
   int rc = nrec ? record_slices(ctx, d_off, nrec, sl) : SG_OK;
   if (rc) return rc;
   size_t total = 0;
   for (const RecSlice& x : sl)
     if (x.e1 > x.e0) total += align256(bucket_plan_bytes(x.e1 - x.e0, x.r1 - x.r0)) + align256((x.r1 - x.r0 + 1) * 8);
-  rc = ws_reserve(ctx, total ? total : 256);
+  rc = slot_reserve(ctx, S, total ? total : 256);
   if (rc) return rc;
+  SlotWs guard(ctx, S);
   size_t base = 0;
   for (const RecSlice& x : sl) {
     PrefixSlice ps{x.r0, x.r1, x.e0, x.e1, base};
@@ -1964,21 +2004,24 @@ int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words,
       SG_HIP(hipGetLastError());
       base = roff_at + align256((nr + 1) * 8);
     }
-    ctx->prefix_slices.push_back(ps);
+    S.slices.push_back(ps);
   }
-  ctx->prefix_nrec = nrec;
-  ctx->prefix_open = true;
+  S.nrec = nrec;
+  S.open = true;
   return SG_OK;
 }
 
-int prefix_end(sg_ctx* ctx, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new) {
-  if (!ctx->prefix_open) {
-    set_error("prefix triage: no batch begun on this context");
+int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords,
+               uint8_t* d_rec_new) {
+  if (slot >= kPrefixSlots || !ctx->prefix[slot].open) {
+    set_error("prefix triage: no batch begun in slot %u", slot);
     return SG_EINVAL;
   }
-  ctx->prefix_open = false;
-  if (ctx->prefix_nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, ctx->prefix_nrec, ctx->stream));
-  for (const PrefixSlice& x : ctx->prefix_slices) {
+  PrefixSlot& S = ctx->prefix[slot];
+  S.open = false;
+  if (S.nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, S.nrec, ctx->stream));
+  SlotWs guard(ctx, S);
+  for (const PrefixSlice& x : S.slices) {
     if (x.e1 == x.e0) continue;
     const uint64_t ns = x.e1 - x.e0, nr = x.r1 - x.r0;
     BucketPlan bp(ns, nr);

@@ -450,6 +450,8 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   }
   for (auto ev : ctx->timer.pool) hipEventDestroy(ev);
   if (ctx->ws) hipFree(ctx->ws);
+  for (auto& s : ctx->prefix)
+    if (s.ws) hipFree(s.ws);
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);

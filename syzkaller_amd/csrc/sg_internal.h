@@ -60,6 +60,18 @@ struct PrefixSlice {
   size_t ws_base;
 };
 
+// One kept batch of the two-phase triage: its record slices and their
+// partitions, in a workspace of its own (two slots, so one batch's exchange
+// can run while the next one is partitioned)
+struct PrefixSlot {
+  std::vector<PrefixSlice> slices;
+  uint64_t nrec = 0;
+  bool open = false;
+  void* ws = nullptr;
+  size_t ws_cap = 0;
+};
+constexpr uint32_t kPrefixSlots = 2;
+
 struct sg_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -83,9 +95,7 @@ struct sg_ctx {
   // environment is read once, at context creation
   uint64_t max_launch_recs = 0;
   // two-phase triage state (prefix_begin / prefix_end, sg_bucket.hip)
-  std::vector<PrefixSlice> prefix_slices;
-  uint64_t prefix_nrec = 0;
-  bool prefix_open = false;
+  PrefixSlot prefix[kPrefixSlots];
   bool debug_part = false;
   // rebased record offsets of one record slice (grow-only, owned)
   uint64_t* slice_off = nullptr;
@@ -193,9 +203,9 @@ size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
 // workspace) and ORs into marks_words its signal not in base_words; end
 // triages the kept partitions against mwords (flags, mwords / nwords updated).
 // Between the two only set operations may run on the context.
-int prefix_begin(sg_ctx* ctx, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
+int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec);
-int prefix_end(sg_ctx* ctx, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new);
+int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new);
 // One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch
 // at ws_base (reserved by the caller).
 int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,

@@ -394,8 +394,8 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
   return SG_OK;
 }
 
-int sg_prefix_begin_dev(sg_ctx* ctx, sg_set* base, sg_set* marks, const uint32_t* d_vals, const uint64_t* d_rec_off,
-                        uint64_t nvals, uint64_t nrec) {
+int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks, const uint32_t* d_vals,
+                        const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec) {
   if (!ctx || !base || !marks || base->ctx != ctx || marks->ctx != ctx || !d_rec_off || (nvals && !d_vals)) {
     set_error("sg_prefix_begin_dev: invalid argument");
     return SG_EINVAL;
@@ -403,10 +403,11 @@ int sg_prefix_begin_dev(sg_ctx* ctx, sg_set* base, sg_set* marks, const uint32_t
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
-  return prefix_begin(ctx, base->words, marks->words, d_vals, d_rec_off, nvals, nrec);
+  return prefix_begin(ctx, slot, base->words, marks->words, d_vals, d_rec_off, nvals, nrec);
 }
 
-int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig, uint8_t* d_rec_new) {
+int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
+                      uint8_t* d_rec_new) {
   if (!ctx || !maxsig || maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {
     set_error("sg_prefix_end_dev: invalid argument");
     return SG_EINVAL;
@@ -414,11 +415,11 @@ int sg_prefix_end_dev(sg_ctx* ctx, sg_set* maxsig, const uint32_t* d_prefix, sg_
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
-  if (ctx->prefix_nrec && !d_rec_new) {
+  if (slot < kPrefixSlots && ctx->prefix[slot].nrec && !d_rec_new) {
     set_error("sg_prefix_end_dev: no flag buffer");
     return SG_EINVAL;
   }
-  return prefix_end(ctx, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new);
+  return prefix_end(ctx, slot, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new);
 }
 
 int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {

@@ -105,6 +105,13 @@ class Comm:
             dist.all_gather_into_tensor(out, t, group=self.group)
         return out
 
+    def start_all_to_all_equal(self, out, t):
+        """all_to_all_equal left running on RCCL's stream (see start_all_gather_equal)."""
+        if self.world == 1 or self.host:
+            self.all_to_all_equal(out, t)
+            return _Done()
+        return dist.all_to_all_single(out, t, group=self.group, async_op=True)
+
     def start_all_gather_equal(self, out, t):
         """all_gather_equal left running on RCCL's stream; wait() on the handle
         orders the current stream after it (under gloo: done on return)."""
@@ -192,13 +199,13 @@ class HipStages:
         call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
              total.data_ptr())
 
-    def prefix_begin(self, base, marks, vals, off, nvals, nrec):
-        call("sg_prefix_begin_dev", self.ctx.h, base.h, marks.h, vals.data_ptr() if nvals else None, off.data_ptr(),
-             nvals, nrec)
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0):
+        call("sg_prefix_begin_dev", self.ctx.h, slot, base.h, marks.h, vals.data_ptr() if nvals else None,
+             off.data_ptr(), nvals, nrec)
 
-    def prefix_end(self, maxset, prefix, newset, rec_new):
+    def prefix_end(self, maxset, prefix, newset, rec_new, slot=0):
         """prefix: None or an int32 device tensor of >= 2^27 words (bitmap layout)."""
-        call("sg_prefix_end_dev", self.ctx.h, maxset.h, ctypes.c_void_p(prefix.data_ptr()) if prefix is not None
+        call("sg_prefix_end_dev", self.ctx.h, slot, maxset.h, ctypes.c_void_p(prefix.data_ptr()) if prefix is not None
              else None, newset.h if newset is not None else None, rec_new.data_ptr())
 
     def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
@@ -306,58 +313,110 @@ class PrefixTriage:
          prefixes back, all-gather of the totals.
       3. The local triage of rank k's records against M0 | P_k
          (sg_prefix_end_dev, on the partitions of step 1, reading P_k beside
-         maxSignal; the all-gather of T runs meanwhile).  M0 | P_k is the
-         sequential loop's maxSignal before rank k's first record (P_k is the
-         new signal of every earlier record), and within the rank the local
-         triage is the loop itself, so the flags are the loop's.
+         maxSignal).  M0 | P_k is the sequential loop's maxSignal before rank
+         k's first record (P_k is the new signal of every earlier record), and
+         within the rank the local triage is the loop itself, so the flags are
+         the loop's.
       4. maxSignal = M0 | T and newSignal |= T on every rank (step 3 left
          maxSignal between M0 and M0 | T).
     Per rank and step the exchange moves about 2.5 bitmaps (512 MiB each)
     whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
-    rank it is the plain local triage.  Stage contracts: HipStages."""
+    rank it is the plain local triage.
 
-    def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False):
+    start() runs steps 1-2 and leaves the exchange running on RCCL's stream
+    (the prefix-OR on a side stream between the collectives); finish() runs
+    steps 3-4.  Batches alternate between two slots, so the next batch can be
+    started -- partitioned and marked while this one's bitmaps travel -- before
+    this one is finished:  start(b0), start(b1), finish(b0), start(b2),
+    finish(b1), ...  Marking batch i+1 against a maxSignal that still lacks
+    batch i's total T_i only adds signal of M0' = M0 | T_i to C, and
+    M0' | P' = M0' | P, so the flags are unchanged.  Stage contracts:
+    HipStages."""
+
+    def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None):
         self.st = stages
         self.comm = comm if comm is not None else Comm()
         self.device = device
         # (measurement: run the two-phase path with its local exchange at one rank too)
         self.two_phase_at_one = two_phase_at_one
+        # the prefix-OR between the two collectives: stages on a second context
+        # whose stream is side_stream (None: on the main stream, in start)
+        self.side_st, self.side = side_stages, side_stream
         G, W = self.comm.world, stages.words
         self.S = -(-W // G)  # words per slice (the last slice padded)
-        n = self.S * G
+        self.slots = []
         if G > 1 or two_phase_at_one:
-            self.C = torch.zeros(n, dtype=torch.int32, device=device)
-            self.P = torch.zeros(n, dtype=torch.int32, device=device)
-            self.T = torch.zeros(n, dtype=torch.int32, device=device)
-            self.recv = torch.empty(n, dtype=torch.int32, device=device)
-            self.pref = torch.empty(n, dtype=torch.int32, device=device)
-            self.tot = torch.empty(self.S, dtype=torch.int32, device=device)
-            self.cset = stages.wrap(self.C)
+            n = self.S * G
+            for _ in range(2):
+                b = {k: torch.zeros(n, dtype=torch.int32, device=device) for k in ("C", "P", "T")}
+                b.update(recv=torch.empty(n, dtype=torch.int32, device=device),
+                         pref=torch.empty(n, dtype=torch.int32, device=device),
+                         tot=torch.empty(self.S, dtype=torch.int32, device=device))
+                b["cset"] = stages.wrap(b["C"])
+                self.slots.append(b)
+        self.next_slot = 0
         self.last = {}
 
-    def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new):
+    def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new, nrec_total=None):
         """Same contract as ShardedTriage.step."""
+        return self.finish(self.start(maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new, nrec_total))
+
+    def start(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new, nrec_total=None):
+        """Steps 1-2 for records rec_base .. rec_base+nrec-1 (vals / off this
+        rank's CSR slice, off[0] == 0); rec_new gets their flags in finish().
+        Returns the pending step.  nrec_total (the batch's record count) may be
+        given by the caller; otherwise it is gathered, which waits for the
+        collectives already in flight."""
         c, st, G = self.comm, self.st, self.comm.world
-        ranges = c.all_gather_i64([rec_base, nrec])
-        nrec_total = max(rb + n for rb, n in ranges)
-        if G == 1 and not self.two_phase_at_one:
+        if nrec_total is None:
+            nrec_total = max(rb + n for rb, n in c.all_gather_i64([rec_base, nrec]))
+        pend = {"maxsig": maxsig, "newsig": newsig, "rec_new": rec_new, "nrec_total": nrec_total}
+        if not self.slots:
             st.triage(maxsig, newsig, vals, off, nvals, nrec, rec_new)
-            self.last = {"nrec_total": nrec_total, "exchange_bytes": 0}
-            return nrec_total
+            pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": 0}
+            return pend
+        slot = self.next_slot
+        self.next_slot ^= 1
+        b = self.slots[slot]
         # 1. this rank's new signal against M0 (its partitions kept for 3.)
-        st.clear(self.cset)
-        st.prefix_begin(maxsig, self.cset, vals, off, nvals, nrec)
+        st.clear(b["cset"])
+        st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
         # 2. exclusive prefix and total over the ranks, slice by slice
-        c.all_to_all_equal(self.recv, self.C)
-        st.prefix_or(self.recv, G, self.S, self.pref, self.tot)
-        c.all_to_all_equal(self.P, self.pref)
-        gather_t = c.start_all_gather_equal(self.T, self.tot)
-        # 3. the flags against M0 | P_k
-        st.prefix_end(maxsig, self.P, None, rec_new)
-        # 4. the replicated state after the whole batch
-        gather_t.wait()
-        st.or_words(maxsig, self.T)
-        if newsig is not None:
-            st.or_words(newsig, self.T)
-        self.last = {"nrec_total": nrec_total, "exchange_bytes": 4 * self.S * (3 * (G - 1))}
-        return nrec_total
+        got_c = c.start_all_to_all_equal(b["recv"], b["C"])
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                got_c.wait()
+                self.side_st.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
+                pend["got_p"] = c.start_all_to_all_equal(b["P"], b["pref"])
+                pend["got_t"] = c.start_all_gather_equal(b["T"], b["tot"])
+                # (one rank, or gloo: the "collectives" were copies on this stream)
+                pend["side_done"] = torch.cuda.Event()
+                pend["side_done"].record(self.side)
+        else:
+            got_c.wait()
+            st.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
+            pend["got_p"] = c.start_all_to_all_equal(b["P"], b["pref"])
+            pend["got_t"] = c.start_all_gather_equal(b["T"], b["tot"])
+        pend["slot"] = slot
+        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": 4 * self.S * (3 * (G - 1))}
+        return pend
+
+    def finish(self, pend):
+        """Steps 3-4 of a started batch; returns the batch's record count."""
+        st = self.st
+        if "slot" in pend:
+            b, slot = self.slots[pend["slot"]], pend["slot"]
+            maxsig, newsig = pend["maxsig"], pend["newsig"]
+            # 3. the flags against M0 | P_k
+            if "side_done" in pend:
+                torch.cuda.current_stream().wait_event(pend["side_done"])
+            pend["got_p"].wait()
+            st.prefix_end(maxsig, b["P"], None, pend["rec_new"], slot)
+            # 4. the replicated state after the whole batch
+            pend["got_t"].wait()
+            st.or_words(maxsig, b["T"])
+            if newsig is not None:
+                st.or_words(newsig, b["T"])
+        self.last = pend["last"]
+        return pend["nrec_total"]

@@ -43,6 +43,9 @@ class BitSet:
 class NumpyPrefixStages:
     words = WORDS
 
+    def __init__(self):
+        self.kept = {}
+
     def new_set(self):
         return BitSet()
 
@@ -67,16 +70,16 @@ class NumpyPrefixStages:
             acc = acc | p[k]
         total.numpy().view(np.uint32)[:words] = acc
 
-    def prefix_begin(self, base, marks, vals, off, nvals, nrec):
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0):
         v = vals[:nvals].numpy().view(np.uint32)
         if v.size:
             marks.add(v[~base.has(v)])
-        self.kept = (vals, off, nvals, nrec)
+        self.kept[slot] = (vals, off, nvals, nrec)
 
-    def prefix_end(self, maxset, prefix, newset, rec_new):
+    def prefix_end(self, maxset, prefix, newset, rec_new, slot=0):
         """Against maxset | prefix; maxset gains the new signal, and the words
         that gain bits also gain their prefix bits (include/syzsig.h)."""
-        vals, off, nvals, nrec = self.kept
+        vals, off, nvals, nrec = self.kept.pop(slot)
         start = maxset.w | (prefix.numpy().view(np.uint32)[:WORDS] if prefix is not None else 0)
         work = BitSet(start.copy())
         self.triage(work, newset, vals, off, nvals, nrec, rec_new)
@@ -114,7 +117,7 @@ M0 = np.arange(0, 3000, 5, dtype=np.uint32)
 BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, pipelined):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -124,6 +127,7 @@ def _worker(rank, world, port, q):
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
+        pend = None
         for seed, nrec in BATCHES:
             vals, off = batch(seed, nrec)
             r0, r1 = split(nrec, world, seed)[rank]
@@ -131,23 +135,32 @@ def _worker(rank, world, port, q):
             v = torch.from_numpy(vals[e0:e1].view(np.int32).copy())
             o = torch.from_numpy((off[r0:r1 + 1] - off[r0]).astype(np.int64))
             rec_new = torch.zeros(max(r1 - r0, 1), dtype=torch.uint8)
-            total = tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new)
-            assert total == nrec
-            out.append((r0, rec_new[: r1 - r0].tolist()))
-        q.put((rank, out, ms.export(), ns.export()))
+            out.append((r0, r1, rec_new))
+            if not pipelined:
+                assert tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new) == nrec
+                continue
+            # the next batch started (marked against the maxSignal that still
+            # lacks this batch's total) before the previous one is finished
+            p = tri.start(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new, nrec_total=nrec)
+            if pend is not None:
+                assert tri.finish(pend[0]) == pend[1]
+            pend = (p, nrec)
+        if pend is not None:
+            assert tri.finish(pend[0]) == pend[1]
+        q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(), ns.export()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
-def test_prefix_triage_equals_sequential_loop(world):
+@pytest.mark.parametrize("world,pipelined", [(2, False), (4, False), (2, True), (4, True)])
+def test_prefix_triage_equals_sequential_loop(world, pipelined):
     from oracle import pyoracle as O
 
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -130,8 +130,8 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix):
     v, o = _dev(vals, np.int32), _dev(off, np.int64)
     nrec = off.size - 1
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
-    st.prefix_begin(base, marks, v, o, vals.size, nrec)
-    st.prefix_end(ms, _Words(pre) if as_prefix else None, ns, rec_new)
+    st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=1)
+    st.prefix_end(ms, _Words(pre) if as_prefix else None, ns, rec_new, slot=1)
     torch.cuda.synchronize()
     assert np.array_equal(marks.export(), np.setdiff1d(np.unique(vals), m0))
     om, on = O.OSet(np.union1d(m0, extra)), O.OSet()
@@ -196,10 +196,20 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
     from tests.test_shard import split
 
     ctx = C.Context(ctx_dev)
-    tri = (PrefixTriage if proto == "prefix" else ShardedTriage)(HipStages(ctx), Comm())
+    side_ctx = None
+    if proto == "prefix_pipelined":
+        # the PrefixTriage the bench runs at N > 1: batches overlapped through
+        # the two slots, the prefix-OR on a side stream (here also at one rank)
+        side = torch.cuda.Stream()
+        side_ctx = C.Context(ctx_dev)
+        with torch.cuda.stream(side):
+            side_st = HipStages(side_ctx)
+        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=True, side_stages=side_st, side_stream=side)
+    else:
+        tri = (PrefixTriage if proto == "prefix" else ShardedTriage)(HipStages(ctx), Comm())
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
     C.SignalAdd(ms, m0)
-    out = []
+    out, pend = [], None
     for seed, nrec in batches:
         vals, off = _batch(seed, nrec)
         r0, r1 = split(nrec, world, seed)[rank] if world > 1 else (0, nrec)
@@ -207,11 +217,23 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
         v = _dev(vals[e0:e1] if e1 > e0 else np.zeros(1, np.uint32), np.int32)
         o = _dev((off[r0:r1 + 1] - off[r0]).astype(np.uint64), np.int64)
         rec_new = torch.zeros(max(r1 - r0, 1), dtype=torch.uint8, device="cuda")
-        tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new)
-        out.append((r0, rec_new[: r1 - r0].cpu().tolist()))
+        out.append((r0, r1, rec_new))
+        if side_ctx is None:
+            tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new)
+            continue
+        p = tri.start(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new, nrec_total=nrec)
+        if pend is not None:
+            assert tri.finish(pend[0]) == pend[1]
+        pend = (p, nrec, v, o)  # (the batch's buffers live until its finish)
+    if pend is not None:
+        assert tri.finish(pend[0]) == pend[1]
+    torch.cuda.synchronize()
+    out = [(r0, fl[: r1 - r0].cpu().tolist()) for r0, r1, fl in out]
     res = (out, ms.export().tolist(), ns.export().tolist())
-    del ms, ns, tri
+    del ms, ns, tri, pend
     ctx.close()
+    if side_ctx is not None:
+        side_ctx.close()
     return res
 
 
@@ -228,7 +250,7 @@ def _expected():
     return flags, om.export().tolist(), on.export().tolist()
 
 
-@pytest.mark.parametrize("proto", ["pairs", "prefix"])
+@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
 def test_sharded_protocol_one_rank_vs_oracle(ctx, proto):
     out, m, n = _run_protocol(0, 1, 0, BATCHES, M0, proto)
     ef, em, en = _expected()
@@ -259,7 +281,7 @@ def _worker(rank, world, port, q, proto):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("proto", ["pairs", "prefix"])
+@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
 def test_sharded_protocol_two_ranks_one_gpu(proto):
     import torch.multiprocessing as mp
 
