@@ -557,9 +557,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 paths on a smaller box: SG_BENCH_BACKEND=gloo puts
+    # several ranks on one GPU (RCCL refuses that); the driver's runs use RCCL
+    backend = os.environ.get("SG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
     mode = args.mode if args.mode != "auto" else ("c2" if world == 1 else "c3")
     if args.programs is None:

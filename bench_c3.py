@@ -25,15 +25,20 @@ SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "sh
                                 "set_add", "prefix_or", "bucket_mark"]
 
 
+def _cdev():
+    """Device of small collective tensors: host ones under gloo (rehearsals)."""
+    return "cuda" if not dist.is_initialized() or dist.get_backend() == "nccl" else "cpu"
+
+
 def _max_over_ranks(x, world):
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_cdev())
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def _sum_over_ranks(x, world):
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_cdev())
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
@@ -55,8 +60,8 @@ def run_c3(ctx, args, cfg, rank, world):
     del warm
     m0_count = len(m0set)
     if world > 1:
-        counts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-        dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device="cuda"))
+        counts = [torch.zeros(1, dtype=torch.int64, device=_cdev()) for _ in range(world)]
+        dist.all_gather(counts, torch.tensor([m0_count], dtype=torch.int64, device=_cdev()))
         assert len({int(c.item()) for c in counts}) == 1, "maxSignal snapshots differ between ranks"
     prefix = getattr(args, "c3_proto", "prefix") == "prefix"
     two_phase = getattr(args, "c3_two_phase", False)
