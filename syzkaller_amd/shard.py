@@ -333,7 +333,8 @@ class PrefixTriage:
     M0' | P' = M0' | P, so the flags are unchanged.  Stage contracts:
     HipStages."""
 
-    def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None):
+    def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None,
+                 gather=None):
         self.st = stages
         self.comm = comm if comm is not None else Comm()
         self.device = device
@@ -344,14 +345,26 @@ class PrefixTriage:
         self.side_st, self.side = side_stages, side_stream
         G, W = self.comm.world, stages.words
         self.S = -(-W // G)  # words per slice (the last slice padded)
+        # gather mode: one all-gather of the whole C_k, every rank computes its
+        # own prefix: (G-1) bitmaps per rank against the all-to-all form's
+        # 3 (G-1) / G, so fewer bytes for G = 2
+        self.gather = (G == 2) if gather is None else gather
+        self.W = W
         self.slots = []
         if G > 1 or two_phase_at_one:
             n = self.S * G
             for _ in range(2):
-                b = {k: torch.zeros(n, dtype=torch.int32, device=device) for k in ("C", "P", "T")}
-                b.update(recv=torch.empty(n, dtype=torch.int32, device=device),
-                         pref=torch.empty(n, dtype=torch.int32, device=device),
-                         tot=torch.empty(self.S, dtype=torch.int32, device=device))
+                if self.gather:
+                    b = {"C": torch.zeros(W, dtype=torch.int32, device=device),
+                         "allc": torch.empty(G * W, dtype=torch.int32, device=device),
+                         "pref": torch.empty(G * W, dtype=torch.int32, device=device),
+                         "T": torch.empty(W, dtype=torch.int32, device=device)}
+                    b["P"] = b["pref"][self.comm.rank * W:(self.comm.rank + 1) * W]
+                else:
+                    b = {k: torch.zeros(n, dtype=torch.int32, device=device) for k in ("C", "P", "T")}
+                    b.update(recv=torch.empty(n, dtype=torch.int32, device=device),
+                             pref=torch.empty(n, dtype=torch.int32, device=device),
+                             tot=torch.empty(self.S, dtype=torch.int32, device=device))
                 b["cset"] = stages.wrap(b["C"])
                 self.slots.append(b)
         self.next_slot = 0
@@ -381,25 +394,35 @@ class PrefixTriage:
         # 1. this rank's new signal against M0 (its partitions kept for 3.)
         st.clear(b["cset"])
         st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
-        # 2. exclusive prefix and total over the ranks, slice by slice
-        got_c = c.start_all_to_all_equal(b["recv"], b["C"])
+        # 2. exclusive prefix and total over the ranks (slice by slice, or
+        # whole bitmaps in gather mode)
+        if self.gather:
+            got_c = c.start_all_gather_equal(b["allc"], b["C"])
+        else:
+            got_c = c.start_all_to_all_equal(b["recv"], b["C"])
+
+        def exchange(stages):
+            got_c.wait()
+            if self.gather:  # pref part k = P_k; this rank's is b["P"]
+                stages.prefix_or(b["allc"], G, self.W, b["pref"], b["T"])
+                pend["got_p"] = pend["got_t"] = _Done()
+            else:
+                stages.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
+                pend["got_p"] = c.start_all_to_all_equal(b["P"], b["pref"])
+                pend["got_t"] = c.start_all_gather_equal(b["T"], b["tot"])
+
         if self.side is not None:
             self.side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.side):
-                got_c.wait()
-                self.side_st.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
-                pend["got_p"] = c.start_all_to_all_equal(b["P"], b["pref"])
-                pend["got_t"] = c.start_all_gather_equal(b["T"], b["tot"])
-                # (one rank, or gloo: the "collectives" were copies on this stream)
+                exchange(self.side_st)
+                # (one rank, gloo or gather mode: the side stream's own work)
                 pend["side_done"] = torch.cuda.Event()
                 pend["side_done"].record(self.side)
         else:
-            got_c.wait()
-            st.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
-            pend["got_p"] = c.start_all_to_all_equal(b["P"], b["pref"])
-            pend["got_t"] = c.start_all_gather_equal(b["T"], b["tot"])
+            exchange(st)
         pend["slot"] = slot
-        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": 4 * self.S * (3 * (G - 1))}
+        xb = 4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))
+        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": xb}
         return pend
 
     def finish(self, pend):

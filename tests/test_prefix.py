@@ -117,13 +117,13 @@ M0 = np.arange(0, 3000, 5, dtype=np.uint32)
 BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
 
 
-def _worker(rank, world, port, q, pipelined):
+def _worker(rank, world, port, q, pipelined, gather):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from syzkaller_amd.shard import Comm, PrefixTriage
 
-        tri = PrefixTriage(NumpyPrefixStages(), Comm(), device="cpu")
+        tri = PrefixTriage(NumpyPrefixStages(), Comm(), device="cpu", gather=gather)
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
@@ -153,14 +153,15 @@ def _worker(rank, world, port, q, pipelined):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,pipelined", [(2, False), (4, False), (2, True), (4, True)])
-def test_prefix_triage_equals_sequential_loop(world, pipelined):
+@pytest.mark.parametrize("world,pipelined,gather", [(2, False, False), (4, False, False), (2, True, False),
+                                                    (4, True, False), (2, True, True), (4, False, True)])
+def test_prefix_triage_equals_sequential_loop(world, pipelined, gather):
     from oracle import pyoracle as O
 
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -199,12 +199,14 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
     side_ctx = None
     if proto == "prefix_pipelined":
         # the PrefixTriage the bench runs at N > 1: batches overlapped through
-        # the two slots, the prefix-OR on a side stream (here also at one rank)
+        # the two slots, the prefix-OR on a side stream (here also at one rank;
+        # the all-to-all form -- plain "prefix" at two ranks is gather mode)
         side = torch.cuda.Stream()
         side_ctx = C.Context(ctx_dev)
         with torch.cuda.stream(side):
             side_st = HipStages(side_ctx)
-        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=True, side_stages=side_st, side_stream=side)
+        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=True, side_stages=side_st, side_stream=side,
+                           gather=False)
     else:
         tri = (PrefixTriage if proto == "prefix" else ShardedTriage)(HipStages(ctx), Comm())
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
