@@ -32,6 +32,10 @@ int hip_fail(hipError_t e, const char* what) {
 int ensure_device(sg_ctx* ctx) {
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  // hipGetLastError after our launches must see only our errors: drop one
+  // left on this thread by another library (seen: torch's "invalid device
+  // ordinal" after spawning multiprocess workers)
+  (void)hipGetLastError();
   return SG_OK;
 }
 
