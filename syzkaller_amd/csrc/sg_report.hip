@@ -17,7 +17,8 @@
 // (two radix-indexed searches, first-query atomicMin per symbol, last-delete
 // atomicMax per call site), per symbol group (the first query per start
 // decides which symbol's range is added), per call site (final verdict), then
-// an ordered compaction.  Symbols must be sorted by start with non-decreasing
+// an ordered compaction.  The per-query pass is split in two (k_rep_first,
+// k_rep_del) so that each runs in the query order its read-check needs.  Symbols must be sorted by start with non-decreasing
 // ends (the condition under which the reference's binary search over ends is
 // meaningful).
 #include "sg_internal.h"
@@ -107,23 +108,57 @@ struct RepArgs {
   uint64_t* group_first;  // per group leader: (first query << 32) | symbol
   uint32_t* last_del;     // per call site: 1 + last deleting query (0 none)
   uint8_t* flag;          // per call site: uncovered
+  uint64_t* qbits;        // per query: inside a symbol (pass 1 -> pass 2)
   RadixIdx iend, ipcs;    // indexes over send and pcs
 };
 
-// One pass over the queries in query order: symbol (cover.go:278-285), the
-// symbol's first query (atomicMin, issued only while below the stored value)
-// and the call site's last deleting query (atomicMax).  Both searches go
-// through the radix indexes.
-__global__ __launch_bounds__(256) void k_rep_query(RepArgs a) {
+// Two passes over the queries, each ordered so that its read-check skips
+// almost every atomic: the first-query minimum per symbol wants ascending
+// query order, the last-delete maximum per call site descending order (a
+// call site is queried ~400 times in the C5 workload; one atomicMax per
+// query serialised ~100M memory-side atomics on a few 100K addresses).
+//
+// Pass 1, ascending: symbol (cover.go:278-285) through the radix index over
+// ends, the symbol's first query (atomicMin, issued only while below the
+// stored value), and one bit per query: "inside a symbol" (ballot words).
+// The grid stride is a multiple of 64, so a wave's lanes hold 64 consecutive
+// queries starting at a multiple of 64.
+__global__ __launch_bounds__(256) void k_rep_first(RepArgs a) {
   const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.ncov; i += S) {
-    const uint64_t pc = ((uint64_t)a.base << 32) + (uint64_t)a.cov[i] - 5;  // cover.go:101
-    const uint64_t idx = ub_idx(a.send, a.nsym, a.iend, pc);                // cover.go:278
-    if (idx == a.nsym || pc < a.sstart[idx] || pc > a.send[idx]) continue;  // cover.go:285
-    const uint32_t qi = (uint32_t)i;
-    if (a.first_q[idx] > qi) atomicMin(&a.first_q[idx], qi);
-    const uint64_t j = lb_idx(a.pcs, a.npcs, a.ipcs, pc);  // delete(uncovered, pc), cover.go:299
-    if (j < a.npcs && a.pcs[j] == pc && a.last_del[j] < qi + 1) atomicMax(&a.last_del[j], qi + 1);
+  const uint64_t n64 = (a.ncov + 63) & ~63ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n64; i += S) {
+    bool hit = false;
+    if (i < a.ncov) {
+      const uint64_t pc = ((uint64_t)a.base << 32) + (uint64_t)a.cov[i] - 5;  // cover.go:101
+      const uint64_t idx = ub_idx(a.send, a.nsym, a.iend, pc);                // cover.go:278
+      hit = idx < a.nsym && pc >= a.sstart[idx] && pc <= a.send[idx];         // cover.go:285
+      if (hit) {
+        const uint32_t qi = (uint32_t)i;
+        if (a.first_q[idx] > qi) atomicMin(&a.first_q[idx], qi);
+      }
+    }
+    const uint64_t w = __ballot(hit);
+    if ((threadIdx.x & 63) == 0) a.qbits[i >> 6] = w;
+  }
+}
+
+// Pass 2, descending: for the queries inside a symbol, the call site it
+// deletes (delete(uncovered, pc), cover.go:299) and its last deleting query
+// (atomicMax, issued only while above the stored value; a read may see an
+// older, smaller value than memory holds: then the atomic is merely
+// redundant).  Measured (C5): lookups, not atomics, bound this pass; a
+// call-site hash table and XCD-partitioned site ranges were both slower.
+__global__ __launch_bounds__(256) void k_rep_del(RepArgs a) {
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.ncov) return;
+  for (uint64_t k = (a.ncov - 1 - t) / S + 1; k-- > 0;) {
+    const uint64_t i = t + k * S;
+    if (!((a.qbits[i >> 6] >> (i & 63)) & 1ull)) continue;
+    const uint64_t pc = ((uint64_t)a.base << 32) + (uint64_t)a.cov[i] - 5;
+    const uint64_t j = lb_idx(a.pcs, a.npcs, a.ipcs, pc);
+    const uint32_t q1 = (uint32_t)i + 1;
+    if (j < a.npcs && a.pcs[j] == pc && a.last_del[j] < q1) atomicMax(&a.last_del[j], q1);
   }
 }
 
@@ -225,7 +260,8 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   size_t o_cov = p.add(ncov * 4), o_ss = p.add(nsym * 8), o_se = p.add(nsym * 8), o_pcs = p.add(nall * 8),
          o_fq = p.add(nsym * 4), o_gf = p.add(nsym * 8), o_ld = p.add(nall * 4), o_fl = p.add(nall),
          o_m = p.add(nchunks * 32), o_c = p.add(nchunks * 4), o_b = p.add((nchunks + 1) * 8),
-         o_out = p.add(nall * 8);
+         o_out = p.add(nall * 8), o_qb = p.add(((ncov + 63) / 64) * 8);
+
   // radix indexes: about one entry per bucket, at most 2^20 buckets (4 MiB: one XCD L2)
   auto plan_idx = [](uint64_t n, uint64_t lo, uint64_t hi, RadixIdx& I) {
     uint32_t nb = 1024;
@@ -256,6 +292,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   a.group_first = (uint64_t*)ws_at(ctx, o_gf);
   a.last_del = (uint32_t*)ws_at(ctx, o_ld);
   a.flag = (uint8_t*)ws_at(ctx, o_fl);
+  a.qbits = (uint64_t*)ws_at(ctx, o_qb);
   uint64_t* mask = (uint64_t*)ws_at(ctx, o_m);
   uint32_t* cnt = (uint32_t*)ws_at(ctx, o_c);
   uint64_t* bs = (uint64_t*)ws_at(ctx, o_b);
@@ -271,6 +308,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   SG_HIP(hipMemsetAsync(a.first_q, 0xFF, nsym * 4, ctx->stream));
   SG_HIP(hipMemsetAsync(a.group_first, 0xFF, nsym * 8, ctx->stream));
   SG_HIP(hipMemsetAsync(a.last_del, 0, nall * 4, ctx->stream));
+
   {
     ScopedTimer tm(ctx, "report_index");
     hipLaunchKernelGGL(k_radix_index, dim3(div_up((uint64_t)iend.nb + 1, 256)), dim3(256), 0, ctx->stream, a.send,
@@ -278,10 +316,14 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     hipLaunchKernelGGL(k_radix_index, dim3(div_up((uint64_t)ipcs.nb + 1, 256)), dim3(256), 0, ctx->stream, a.pcs,
                        (uint64_t)nall, ipcs.lo, ipcs.sh, ipcs.nb, (uint32_t*)ipcs.r);
   }
+  const dim3 qgrid((uint32_t)std::min<uint64_t>(div_up(ncov, 256), 16384));
   {
-    ScopedTimer tm(ctx, "report_query");
-    const dim3 qgrid((uint32_t)std::min<uint64_t>(div_up(ncov, 256), 16384));
-    hipLaunchKernelGGL(k_rep_query, qgrid, dim3(256), 0, ctx->stream, a);
+    ScopedTimer tm(ctx, "report_first");
+    hipLaunchKernelGGL(k_rep_first, qgrid, dim3(256), 0, ctx->stream, a);
+  }
+  {
+    ScopedTimer tm(ctx, "report_del");
+    hipLaunchKernelGGL(k_rep_del, qgrid, dim3(256), 0, ctx->stream, a);
   }
   {
     ScopedTimer tm(ctx, "report_sites");
