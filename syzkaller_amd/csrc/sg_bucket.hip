@@ -358,6 +358,54 @@ __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restri
   }
 }
 
+// Pass-2 histogram from the byte plane: hist[b * ncols + col] = count of
+// byte b over the chunk's positions [s0, s1).  The chunk's <= kPT bytes are
+// read as 16-B quads from s0 rounded down (<= kPT / 16 + 1 quads; the plane
+// is padded), bytes outside [s0, s1) masked.
+__global__ __launch_bounds__(kPThreads) void k_hist_bytes(const uint8_t* __restrict__ v,
+                                                           const uint4* __restrict__ desc,
+                                                           const uint32_t* __restrict__ ncols_dev,
+                                                           uint32_t* __restrict__ hist) {
+  __shared__ uint32_t rc[256 * 32];
+  const int tid = threadIdx.x;
+  const uint4 d = desc[blockIdx.x];
+  const uint32_t s0 = d.x, s1 = d.y, col = d.w;
+  if (s0 >= s1) return;
+  const uint32_t ncols = *ncols_dev;
+  const uint32_t b0 = s0 & ~15u;
+  constexpr int kQ = kPT / 16 / kPThreads + 1;  // quads per thread (the last one only for the rounding)
+  uint4 x[kQ];
+#pragma unroll
+  for (int k = 0; k < kQ; k++) {
+    const uint32_t q = b0 + (uint32_t)(k * kPThreads + tid) * 16u;
+    x[k] = q < s1 ? *reinterpret_cast<const uint4*>(v + q) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < 256 * 32 / 4 / kPThreads; k++)
+    reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const uint32_t cp = tid & 31;
+#pragma unroll
+  for (int k = 0; k < kQ; k++) {
+    const uint32_t q = b0 + (uint32_t)(k * kPThreads + tid) * 16u;
+    if (q < s1) {
+      const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t pos = q + j;
+        if (pos >= s0 && pos < s1) atomicAdd(&rc[((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) * 32 + cp], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) sum += rc[tid * 32 + ((k + tid) & 31)];
+    hist[(uint64_t)tid * ncols + col] = sum;
+  }
+}
+
 // Counting sort of one tile held in registers (kSteps entries per lane) by an
 // 8-bit digit, through LDS: counts, a one-wave exclusive scan, then every
 // entry takes a slot with an LDS atomic (order within a digit is arbitrary).
@@ -395,12 +443,20 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
 // is the end of digit d's slots.  Each half-wave copies whole digit runs
 // (16 half-waves, 16 digits each): 32 consecutive slots per store, and no
 // per-slot digit array in LDS.
+// With `top` (pass 1), the top byte of every entry also goes to the byte
+// plane top[] at the same position: the pass-2 digit, which the pass-2
+// histogram then reads at 1 B per entry instead of 4.
+template <bool kTop>
 __device__ __forceinline__ void tile_write(const uint32_t* stage, const uint32_t* cnt, const uint32_t* gbase,
-                                           uint32_t* __restrict__ out, int tid) {
+                                           uint32_t* __restrict__ out, uint8_t* __restrict__ top, int tid) {
   const int hw = tid >> 5, hl = tid & 31;
   for (int d = hw; d < 256; d += kPThreads / 32) {
     const uint32_t e = cnt[d], gb = gbase[d];
-    for (uint32_t p = (d ? cnt[d - 1] : 0u) + hl; p < e; p += 32) out[gb + p] = stage[p];
+    for (uint32_t p = (d ? cnt[d - 1] : 0u) + hl; p < e; p += 32) {
+      const uint32_t v = stage[p];
+      out[gb + p] = v;
+      if (kTop) top[gb + p] = (uint8_t)(v >> 24);
+    }
   }
 }
 
@@ -483,6 +539,7 @@ struct P1Args {
   const uint32_t* goff1;   // scanned [slice][tile]
   const uint32_t* hist1;   // [slice][tile] counts
   uint32_t* out;           // s << 8 | rec_in_tile
+  uint8_t* top;            // out's top bytes (the pass-2 digits)
   unsigned long long* dbg; // diagnostics (k_p1_scatter<true>): cycles per phase, summed over blocks
 };
 
@@ -550,7 +607,7 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
     if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
   __syncthreads();
   stamp(3);
-  tile_write(stage, cnt, gbase, a.out, tid);
+  tile_write<true>(stage, cnt, gbase, a.out, a.top, tid);
   stamp(4);
   if (kDbg && tid == 0) atomicAdd(&a.dbg[5], 1ull);
 }
@@ -623,7 +680,7 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
   for (int k = 0; k < kSteps; k++)
     if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
   __syncthreads();
-  tile_write(stage, cnt, gbase, a.out, tid);
+  tile_write<false>(stage, cnt, gbase, a.out, nullptr, tid);
 }
 
 // ---------------------------------------------------------------- bucket ---
@@ -1431,7 +1488,7 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, NG, ng, gmax;
   WsPlan p;
-  size_t oTS, oTR, oGT, oH1, oO1, oV1, oNC, oCB, oCS, oCG, oCF, oCD, oDT, oBD, oGB, oH2, oO2, oV2, oSP, oTK, oBN, oBP,
+  size_t oTS, oTR, oGT, oH1, oO1, oV1, oB1, oNC, oCB, oCS, oCG, oCF, oCD, oDT, oBD, oGB, oH2, oO2, oV2, oSP, oTK, oBN, oBP,
       oLB, oLQ, oSC;
   BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
     nA = (n + kPT - 1) / kPT;
@@ -1446,6 +1503,7 @@ struct BucketPlan {
     oH1 = p.add(256 * T * 4);
     oO1 = p.add((256 * T + 1) * 4);
     oV1 = p.add(n * 4);
+    oB1 = p.add(n + 64);  // pass-1 top bytes; k_hist_bytes reads 16-B quads past the end
     oNC = p.add(ng * 4);
     oCB = p.add((ng + 1) * 4);
     oCS = p.add((gmax + 1) * 4);
@@ -1467,7 +1525,7 @@ struct BucketPlan {
     oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
   }
   void rebase(size_t b) {
-    for (size_t* o : {&oTS, &oTR, &oGT, &oH1, &oO1, &oV1, &oNC, &oCB, &oCS, &oCG, &oCF, &oCD, &oDT, &oBD, &oGB, &oH2,
+    for (size_t* o : {&oTS, &oTR, &oGT, &oH1, &oO1, &oV1, &oB1, &oNC, &oCB, &oCS, &oCG, &oCF, &oCD, &oDT, &oBD, &oGB, &oH2,
                       &oO2, &oV2, &oSP, &oTK, &oBN, &oBP, &oLB, &oLQ, &oSC})
       *o += b;
   }
@@ -1518,6 +1576,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   uint32_t* hist1 = (uint32_t*)ws_at(ctx, bp.oH1);
   uint32_t* goff1 = (uint32_t*)ws_at(ctx, bp.oO1);
   uint32_t* v1 = (uint32_t*)ws_at(ctx, bp.oV1);
+  uint8_t* b1 = (uint8_t*)ws_at(ctx, bp.oB1);
   uint32_t* nch = (uint32_t*)ws_at(ctx, bp.oNC);
   uint32_t* cbase = (uint32_t*)ws_at(ctx, bp.oCB);
   uint32_t* cstart = (uint32_t*)ws_at(ctx, bp.oCS);
@@ -1558,7 +1617,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
-  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, nullptr};
+  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, b1, nullptr};
   const bool dbg = ctx->debug_part;
   unsigned long long* p1dbg = nullptr;
   if (dbg) {
@@ -1594,8 +1653,8 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
                      cdesc, dtile);
   {
     ScopedTimer tm(ctx, "p2_hist");
-    hipLaunchKernelGGL(k_hist_rep<true>, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint32_t*)v1,
-                       (const uint32_t*)nullptr, (const uint4*)cdesc, G, gcount, hist2);
+    hipLaunchKernelGGL(k_hist_bytes, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint8_t*)b1,
+                       (const uint4*)cdesc, gcount, hist2);
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
   if (rc) return rc;
