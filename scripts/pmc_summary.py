@@ -13,7 +13,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"p1_hist": "k_hist_rep<false>", "p1_scatter": "k_p1_scatter", "p2_hist": "k_hist_rep<true>", "p2_scatter": "k_p2_scatter",
+KERNELS = {"p1_hist": "k_hist_rep<false>", "p1_scatter": "k_p1_scatter", "p2_hist": "k_hist_bytes", "p2_scatter": "k_p2_scatter",
            "bucket_triage": "k_bucket<false, false>", "bucket_spill": "k_bucket_direct<false>",
            "triage_claim": "k_claim<true>", "triage_resolve": "k_resolve<true>", "count_missing": "k_count_missing",
            "emit_scatter": "k_scatter("}
