@@ -361,39 +361,41 @@ __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restri
 // Pass-2 histogram from the byte plane: hist[b * ncols + col] = count of
 // byte b over the chunk's positions [s0, s1).  The chunk's <= kPT bytes are
 // read as 16-B quads from s0 rounded down (<= kPT / 16 + 1 quads; the plane
-// is padded), bytes outside [s0, s1) masked.
-__global__ __launch_bounds__(kPThreads) void k_hist_bytes(const uint8_t* __restrict__ v,
-                                                           const uint4* __restrict__ desc,
-                                                           const uint32_t* __restrict__ ncols_dev,
-                                                           uint32_t* __restrict__ hist) {
-  __shared__ uint32_t rc[256 * 32];
+// is padded), bytes outside [s0, s1) masked.  512 threads, 16 counter copies
+// (the per-block zeroing and final sums are most of the work at 1 B per entry).
+constexpr int kHBThreads = 512, kHBCopies = 16;
+__global__ __launch_bounds__(kHBThreads) void k_hist_bytes(const uint8_t* __restrict__ v,
+                                                            const uint4* __restrict__ desc,
+                                                            const uint32_t* __restrict__ ncols_dev,
+                                                            uint32_t* __restrict__ hist) {
+  __shared__ uint32_t rc[256 * kHBCopies];
   const int tid = threadIdx.x;
   const uint4 d = desc[blockIdx.x];
   const uint32_t s0 = d.x, s1 = d.y, col = d.w;
   if (s0 >= s1) return;
   const uint32_t ncols = *ncols_dev;
   const uint32_t b0 = s0 & ~15u;
-  constexpr int kQ = kPT / 16 / kPThreads + 1;  // quads per thread (the last one only for the rounding)
+  constexpr int kQ = kPT / 16 / kHBThreads + 1;  // quads per thread (the last one only for the rounding)
   uint4 x[kQ];
 #pragma unroll
   for (int k = 0; k < kQ; k++) {
-    const uint32_t q = b0 + (uint32_t)(k * kPThreads + tid) * 16u;
+    const uint32_t q = b0 + (uint32_t)(k * kHBThreads + tid) * 16u;
     x[k] = q < s1 ? *reinterpret_cast<const uint4*>(v + q) : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
-  for (int k = 0; k < 256 * 32 / 4 / kPThreads; k++)
-    reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < 256 * kHBCopies / 4 / kHBThreads; k++)
+    reinterpret_cast<uint4*>(rc)[k * kHBThreads + tid] = make_uint4(0, 0, 0, 0);
   __syncthreads();
-  const uint32_t cp = tid & 31;
+  const uint32_t cp = tid & (kHBCopies - 1);
 #pragma unroll
   for (int k = 0; k < kQ; k++) {
-    const uint32_t q = b0 + (uint32_t)(k * kPThreads + tid) * 16u;
+    const uint32_t q = b0 + (uint32_t)(k * kHBThreads + tid) * 16u;
     if (q < s1) {
       const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const uint32_t pos = q + j;
-        if (pos >= s0 && pos < s1) atomicAdd(&rc[((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) * 32 + cp], 1u);
+        if (pos >= s0 && pos < s1) atomicAdd(&rc[((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) * kHBCopies + cp], 1u);
       }
     }
   }
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(kPThreads) void k_hist_bytes(const uint8_t* __restr
   if (tid < 256) {
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < 32; k++) sum += rc[tid * 32 + ((k + tid) & 31)];
+    for (int k = 0; k < kHBCopies; k++) sum += rc[tid * kHBCopies + ((k + tid) & (kHBCopies - 1))];
     hist[(uint64_t)tid * ncols + col] = sum;
   }
 }
@@ -1653,7 +1655,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
                      cdesc, dtile);
   {
     ScopedTimer tm(ctx, "p2_hist");
-    hipLaunchKernelGGL(k_hist_bytes, dim3(G), dim3(kPThreads), 0, ctx->stream, (const uint8_t*)b1,
+    hipLaunchKernelGGL(k_hist_bytes, dim3(G), dim3(kHBThreads), 0, ctx->stream, (const uint8_t*)b1,
                        (const uint4*)cdesc, gcount, hist2);
   }
   rc = scan32(ctx, hist2, goff2, 256 * bp.gmax, scr, gcount, 256);
