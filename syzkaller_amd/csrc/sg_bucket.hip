@@ -628,28 +628,30 @@ struct P2Args {
   uint32_t* out;           // (s & 0xFFFF) << 16 | record_in_group
 };
 
-__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p2_scatter(P2Args a) {
-  __shared__ uint32_t stage[kPT];
-  __shared__ uint32_t cnt[256];
-  __shared__ uint32_t gbase[256];
-  __shared__ SegLds<uint16_t> L;
+// One chunk; kFull: the chunk holds kPT entries (most do), so no entry is
+// predicated (no exec-mask branch per entry and step: the scatters are bound
+// by the instructions they issue).
+template <bool kFull>
+__device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint32_t* cnt, uint32_t* gbase,
+                                         SegLds<uint16_t>& L, uint32_t s0, uint32_t s1, uint32_t gov, uint32_t c,
+                                         uint2 dt) {
   uint16_t* sidx = reinterpret_cast<uint16_t*>(stage);  // tile's first record in the group; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint4 dsc = a.desc[blockIdx.x];
-  const uint2 dt = a.dtile[blockIdx.x];
-  const uint32_t s0 = dsc.x, s1 = dsc.y, gov = dsc.z, c = dsc.w;
-  if (s0 >= s1) return;
   const uint32_t G2 = *a.g2;
   const uint32_t d = gov / a.NG, rg0 = (gov % a.NG) << kGroupBits, tf = dt.x, m = dt.y - dt.x;
   const uint32_t ebase = s0 + w * kPerWave;
   uint32_t sv[kSteps];
-  uint32_t vmask = 0;
+  uint32_t vmask = kFull ? (1u << kSteps) - 1 : 0u;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t e = ebase + k * 64 + lane;
-    const bool ok = e < s1;
-    sv[k] = ok ? a.in[e] : 0u;
-    vmask |= (ok ? 1u : 0u) << k;
+    if (kFull) {
+      sv[k] = a.in[e];
+    } else {
+      const bool ok = e < s1;
+      sv[k] = ok ? a.in[e] : 0u;
+      vmask |= (ok ? 1u : 0u) << k;
+    }
   }
   for (int f = tid; f < 256; f += kPThreads) {
     gbase[f] = a.goff2[(uint64_t)f * G2 + c];
@@ -683,6 +685,21 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
     if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
   __syncthreads();
   tile_write<false>(stage, cnt, gbase, a.out, nullptr, tid);
+}
+
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p2_scatter(P2Args a) {
+  __shared__ uint32_t stage[kPT];
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t gbase[256];
+  __shared__ SegLds<uint16_t> L;
+  const uint4 dsc = a.desc[blockIdx.x];
+  const uint2 dt = a.dtile[blockIdx.x];
+  const uint32_t s0 = dsc.x, s1 = dsc.y;
+  if (s0 >= s1) return;
+  if (s1 - s0 == (uint32_t)kPT)
+    p2_chunk<true>(a, stage, cnt, gbase, L, s0, s1, dsc.z, dsc.w, dt);
+  else
+    p2_chunk<false>(a, stage, cnt, gbase, L, s0, s1, dsc.z, dsc.w, dt);
 }
 
 // ---------------------------------------------------------------- bucket ---
