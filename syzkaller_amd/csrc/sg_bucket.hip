@@ -439,7 +439,8 @@ __device__ __forceinline__ int wave_incl_max(int x) {
 // cnt[] arrives holding the tile's digit counts (read from the histogram
 // pass, not recounted); gbase[d] is lowered by the digit's first slot, so slot
 // p of digit d goes to gbase[d] + p.
-__device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t vmask, uint32_t* cnt,
+template <typename DigitF>
+__device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], DigitF digit, uint32_t vmask, uint32_t* cnt,
                                           uint32_t* gbase, uint32_t (&pos)[kSteps]) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 64) {
@@ -457,7 +458,7 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], uint32_t
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) pos[k] = atomicAdd(&cnt[dv[k]], 1u);
+    if ((vmask >> k) & 1u) pos[k] = atomicAdd(&cnt[digit(dv[k])], 1u);
 }
 
 // Write-out of a ranked tile: after tile_rank and the staging barrier, cnt[d]
@@ -558,18 +559,16 @@ struct P1Args {
   unsigned long long* dbg; // diagnostics (k_p1_scatter<true>): cycles per phase, summed over blocks
 };
 
+// One tile.  Only the values and their records (four 8-bit records per
+// register) stay live across the rank; digits and keys are recomputed from the
+// values (1.85 -> 1.67 ms per C2 launch against keeping digits and keys in
+// registers; an unpredicated path for full tiles, as pass 2 has, was slower
+// here: 1.93 ms).
 template <bool kDbg>
-__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p1_scatter(P1Args a) {
-  __shared__ uint32_t stage[kPT];
-  __shared__ uint32_t cnt[256];
-  __shared__ uint32_t gbase[256];
-  __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
-  __shared__ SegLds<uint8_t> L;
+__device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32_t* cnt, uint32_t* gbase,
+                                        uint16_t* win, SegLds<uint8_t>& L, uint32_t t, uint32_t s0, uint32_t s1) {
   uint8_t* sidx = reinterpret_cast<uint8_t*>(stage);  // record-in-tile index; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
-  const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
-  if (s0 >= s1) return;
   uint64_t tk = kDbg ? clock64() : 0;
   auto stamp = [&](int ph) {
     if (kDbg) {
@@ -605,26 +604,38 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
   const uint32_t nt = s1 - s0;
   seg_build(
       L, sidx, [&](uint32_t k) { return (uint32_t)win[k]; }, [](uint32_t k) { return k; }, wn, nt, tid);
-  uint32_t dv[kSteps], pk[kSteps];
+  uint32_t rp[kSteps / 4] = {};
   const uint32_t el0 = ebase + lane - s0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // record in tile
-    dv[k] = p1_digit(sv[k]);
-    pk[k] = (part_key(sv[k]) << 8) | r;
+    rp[k >> 2] |= r << (8 * (k & 3));
   }
   stamp(1);
   uint32_t pos[kSteps];
-  tile_rank(dv, vmask, cnt, gbase, pos);
+  tile_rank(sv, [](uint32_t v) { return p1_digit(v); }, vmask, cnt, gbase, pos);
   stamp(2);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
+    if ((vmask >> k) & 1u) stage[pos[k]] = (part_key(sv[k]) << 8) | ((rp[k >> 2] >> (8 * (k & 3))) & 0xFFu);
   __syncthreads();
   stamp(3);
   tile_write<true>(stage, cnt, gbase, a.out, a.top, tid);
   stamp(4);
   if (kDbg && tid == 0) atomicAdd(&a.dbg[5], 1ull);
+}
+
+template <bool kDbg>
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p1_scatter(P1Args a) {
+  __shared__ uint32_t stage[kPT];
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t gbase[256];
+  __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
+  __shared__ SegLds<uint8_t> L;
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
+  const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
+  if (s0 >= s1) return;
+  p1_tile<kDbg>(a, stage, cnt, gbase, win, L, t, s0, s1);
 }
 
 // ---------------------------------------------------------------- pass 2 ---
@@ -643,7 +654,8 @@ struct P2Args {
 
 // One chunk; kFull: the chunk holds kPT entries (most do), so no entry is
 // predicated (no exec-mask branch per entry and step: the scatters are bound
-// by the instructions they issue).
+// by the instructions they issue).  As in pass 1, only the values and the
+// records (two 16-bit records per register) stay live across the rank.
 template <bool kFull>
 __device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint32_t* cnt, uint32_t* gbase,
                                          SegLds<uint16_t>& L, uint32_t s0, uint32_t s1, uint32_t gov, uint32_t c,
@@ -683,19 +695,18 @@ __device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint3
         return o <= s0 ? 0u : (o - s0 >= (uint32_t)kPT ? (uint32_t)kPT : o - s0);
       },
       [&](uint32_t k) { return a.trec[tf + k] - rg0; }, m, nt, tid);
-  uint32_t dv[kSteps], pk[kSteps];
   const uint32_t el0 = ebase + lane - s0;
+  uint32_t rp[kSteps / 2] = {};  // records in group, two 16-bit per register
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t r1 = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // tile's record in group
-    dv[k] = sv[k] >> 24;
-    pk[k] = (((sv[k] >> 8) & 0xFFFFu) << 16) | (r1 + (sv[k] & (kRecCap - 1)));
+    rp[k >> 1] |= (r1 + (sv[k] & (kRecCap - 1))) << (16 * (k & 1));
   }
   uint32_t pos[kSteps];
-  tile_rank(dv, vmask, cnt, gbase, pos);
+  tile_rank(sv, [](uint32_t v) { return v >> 24; }, vmask, cnt, gbase, pos);
 #pragma unroll
   for (int k = 0; k < kSteps; k++)
-    if ((vmask >> k) & 1u) stage[pos[k]] = pk[k];
+    if ((vmask >> k) & 1u) stage[pos[k]] = (((sv[k] >> 8) & 0xFFFFu) << 16) | ((rp[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
   __syncthreads();
   tile_write<false>(stage, cnt, gbase, a.out, nullptr, tid);
 }
