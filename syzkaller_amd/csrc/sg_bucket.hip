@@ -408,30 +408,6 @@ __global__ __launch_bounds__(kHBThreads) void k_hist_bytes(const uint8_t* __rest
   }
 }
 
-// Inclusive wave64 scans through DPP: row shifts within the 16-lane rows,
-// then the row broadcasts of lanes 15 and 31 (no LDS-crossbar shuffles; the
-// per-tile scans run on one wave while the others wait at a barrier).
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return x;
-}
-
-// the same for max over values >= -1 (-1: nothing yet)
-__device__ __forceinline__ int wave_incl_max(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));
-  return x;
-}
-
 // Counting sort of one tile held in registers (kSteps entries per lane) by an
 // 8-bit digit, through LDS: counts, a one-wave exclusive scan, then every
 // entry takes a slot with an LDS atomic (order within a digit is arbitrary).
@@ -448,7 +424,7 @@ __device__ __forceinline__ void tile_rank(const uint32_t (&dv)[kSteps], DigitF d
 #pragma unroll
     for (int base = 0; base < 256; base += 64) {
       const uint32_t x = cnt[base + lane];
-      const uint32_t incl = wave_incl_add(x);
+      const uint32_t incl = sgd::wave_incl_add(x);
       const uint32_t ex = carry + incl - x;
       gbase[base + lane] -= ex;
       cnt[base + lane] = ex;
@@ -528,7 +504,7 @@ __device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, StF st, V
       if (b) run = max(run, (int)sidx[w * 32 + 31 - __clz(b)]);
       loc[j] = run;
     }
-    const int incl = wave_incl_max(run);
+    const int incl = sgd::wave_incl_max(run);
     int ex = __builtin_amdgcn_update_dpp(-1, incl, 0x138, 0xF, 0xF, false);  // wave_shr:1 (lane 0: -1)
     ex = max(ex, (int)L.kinit);
 #pragma unroll

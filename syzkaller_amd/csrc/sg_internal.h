@@ -255,4 +255,29 @@ __device__ __forceinline__ uint64_t seg_search(P off, uint64_t lo, uint64_t hi, 
   return lo;
 }
 
+// Inclusive wave64 scans through DPP: row shifts within the 16-lane rows,
+// then the row broadcasts of lanes 15 and 31 (no LDS-crossbar shuffles; the
+// per-tile scans of the partition and merge kernels run on one wave while
+// the others wait at a barrier).
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+// the same for max over values >= -1 (-1: nothing yet)
+__device__ __forceinline__ int wave_incl_max(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));
+  return x;
+}
+
 }  // namespace sgd

@@ -169,13 +169,16 @@ __global__ void k_merge_scatter(MergeArgs m) {
 // k_merge_scatter (copy t of a value against its count c in the other list;
 // ties: cov0's copies first).
 constexpr int kMS = 4096;               // max small side
+#ifndef SG_MERGE_SEG
+#define SG_MERGE_SEG 1  // L copied gap by gap (see k_merge_small)
+#endif
 constexpr int kMT = 1024;               // threads
 constexpr int kMU = kMS / kMT;          // small elements per thread (consecutive)
 #ifndef SG_KML
 #define SG_KML 8
 #endif
 constexpr int kML = SG_KML;             // large elements per thread per tile
-constexpr int kMTile = kMT * kML;       // 8192
+[[maybe_unused]] constexpr int kMTile = kMT * kML;  // 8192
 constexpr int kMWaves = kMT / 64;       // 16
 
 struct SmallArgs {
@@ -246,10 +249,18 @@ __device__ __forceinline__ uint32_t ballot_count(const uint32_t* sv, uint32_t ns
 
 __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_merge_small(SmallArgs m) {
   __shared__ uint32_t sv[kMS];
+#if SG_MERGE_SEG
+  __shared__ uint32_t sdx[kMS];        // dropped L elements of the values before element j's
+  __shared__ uint16_t rll[kMS];        // last S index of each run (distinct value)
+  __shared__ uint32_t red2[kMWaves + 1];
+  __shared__ uint64_t nl_eff_s;
+#endif
   __shared__ uint32_t skp[kMS + 1];    // kept small elements before j
   __shared__ uint32_t sidx[kMS];       // insertion point of small element j in L
+#if !SG_MERGE_SEG
   __shared__ unsigned long long tw[kML * kMWaves];
   __shared__ uint32_t twp[kML * kMWaves + 1];
+#endif
   __shared__ uint32_t red[kMWaves + 1];
   const uint32_t k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -264,6 +275,13 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   __syncthreads();
   // S: keep flags (copy t against the count in L) and insertion points in L
   uint32_t flags = 0;
+#if SG_MERGE_SEG
+  // L copies of a value S also holds are dropped up to S's count (the keep
+  // rule for L's side: Union when L is cov1, SymmetricDifference)
+  const bool ldrop = m.op == SG_OP_SYMDIFF || sL == 1;
+  uint32_t rlast = 0;  // bit u: element u is the last copy of its value in S
+  uint64_t dpk = 0;    // its value's dropped L copies, 16 bits per u
+#endif
   {
     uint32_t x[kMU];
     uint64_t lb[kMU], ub[kMU];
@@ -289,17 +307,26 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
       const bool kp = x[u] != kSent && keep_rule(m.op, sS, t, ub[u] - lb[u]);  // cover.go:97
       flags |= (kp ? 1u : 0u) << u;
+#if SG_MERGE_SEG
+      sidx[j] = (uint32_t)lb[u];
+      // the last copy of its value in S: the value's dropped L copies (the
+      // first min(cS, cL), cS = t + 1) are counted here, so the exclusive
+      // sum at any copy of a value excludes the value's own drops
+      const bool last = j + 1 == ns || sv[j + 1] != x[u];
+      if (last) {
+        const uint64_t cl = ub[u] - lb[u];
+        const uint32_t d = ldrop && x[u] != kSent ? (uint32_t)(cl < t + 1 ? cl : t + 1) : 0u;
+        rlast |= 1u << u;
+        dpk |= (uint64_t)d << (16 * u);
+      }
+#else
       sidx[j] = (uint32_t)(sS == 0 ? lb[u] : ub[u]);
+#endif
     }
   }
   {  // exclusive scan of the kept counts, thread order = element order
     const uint32_t c = __popc(flags);
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
+    const uint32_t incl = sgd::wave_incl_add(c);
     if (lane == 63) red[w] = incl;
     __syncthreads();
     if (tid == 0) {
@@ -323,6 +350,92 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
   __syncthreads();
   const uint32_t KS = skp[ns];
+#if SG_MERGE_SEG
+  {
+    // L is S's values' runs and the gaps between them: every kept L element
+    // of a gap moves by the same amount (kept S elements before it minus
+    // dropped L elements before it), so the gaps are copied whole, as
+    // coalesced streams, and the kept S elements are written on their own.
+    // Equal values: S's kept copies go first (they are identical values).
+    // L's sentinels (its sorted tail) are dropped (cover.go:97).
+    if (tid == 0) {
+      uint64_t lo = 0, hi = nl;  // first sentinel in L
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (L[mid] < kSent) lo = mid + 1; else hi = mid;
+      }
+      nl_eff_s = lo;
+    }
+    // exclusive scan of (run-last flag, drops): run ranks and drops before
+    uint32_t c = 0;
+#pragma unroll
+    for (int u = 0; u < kMU; u++) c += ((rlast >> u) & 1u) + ((uint32_t)(dpk >> (16 * u)) & 0xFFFFu) * 65536u;
+    const uint32_t incl = sgd::wave_incl_add(c);
+    if (lane == 63) red2[w] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int i = 0; i < kMWaves; i++) {
+        const uint32_t v = red2[i];
+        red2[i] = acc;
+        acc += v;
+      }
+      red2[kMWaves] = acc;
+    }
+    __syncthreads();
+    uint32_t run = red2[w] + incl - c;
+#pragma unroll
+    for (int u = 0; u < kMU; u++) {
+      const uint32_t j = tid * kMU + u;
+      if (j < ns) {
+        sdx[j] = run >> 16;  // drops of the values before j's
+        if ((rlast >> u) & 1u) rll[run & 0xFFFFu] = (uint16_t)j;
+      }
+      run += ((rlast >> u) & 1u) + ((uint32_t)(dpk >> (16 * u)) & 0xFFFFu) * 65536u;
+    }
+    __syncthreads();
+    const uint32_t nruns = red2[kMWaves] & 0xFFFFu, dtot = red2[kMWaves] >> 16;
+    const uint64_t nle = nl_eff_s;
+    // kept S elements
+#pragma unroll
+    for (int u = 0; u < kMU; u++) {
+      const uint32_t j = tid * kMU + u;
+      if (j < ns && ((flags >> u) & 1u)) out[(uint64_t)sidx[j] - sdx[j] + skp[j]] = sv[j];
+    }
+    // gaps: g = 0 before S's first value, g = r + 1 after run r; wave by wave
+    for (uint32_t g = w; g <= nruns; g += kMWaves) {
+      uint64_t a, b;
+      int64_t sh;
+      if (g == 0) {
+        a = 0;
+        b = ns ? sidx[0] : nle;
+        sh = 0;
+      } else {
+        const uint32_t jl = rll[g - 1];
+        const uint32_t dr = sdx[jl] + (jl + 1 < ns ? sdx[jl + 1] - sdx[jl] : dtot - sdx[jl]);  // drops through this run
+        const uint32_t dj = dr - sdx[jl];
+        a = (uint64_t)sidx[jl] + dj;
+        b = jl + 1 < ns ? sidx[jl + 1] : nle;
+        sh = (int64_t)skp[jl + 1] - (int64_t)dr;
+      }
+      if (b > nle) b = nle;
+      for (uint64_t p0 = a; p0 < b; p0 += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint64_t pp = p0 + q * 64 + lane;
+          v[q] = pp < b ? L[pp] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint64_t pp = p0 + q * 64 + lane;
+          if (pp < b) out[(uint64_t)((int64_t)pp + sh)] = v[q];
+        }
+      }
+    }
+    if (tid == 0) m.olen[k] = (uint64_t)KS + nle - dtot;
+  }
+#else
   // L: stream tiles in index order
   uint32_t KL = 0, jlo = 0, jp = 0;
   uint32_t xn[kML];  // the next tile's L values, in flight while a tile is processed
@@ -413,12 +526,7 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         cw[q] = wi < kNWd ? (uint32_t)__popcll(tw[wi]) : 0u;
         c += cw[q];
       }
-      uint32_t incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
+      const uint32_t incl = sgd::wave_incl_add(c);
       uint32_t run = KL + incl - c;
 #pragma unroll
       for (int q = 0; q < kWL; q++) {
@@ -465,6 +573,7 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (uint32_t j = jlo + tid; j < ns; j += kMT)  // insertion point past the end of L
     if (skp[j + 1] > skp[j]) out[skp[j] + KL] = sv[j];
   if (tid == 0) m.olen[k] = (uint64_t)KS + KL;
+#endif
 }
 
 __global__ void k_merge_len(MergeArgs m) {
