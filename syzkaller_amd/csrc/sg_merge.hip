@@ -169,16 +169,17 @@ __global__ void k_merge_scatter(MergeArgs m) {
 // k_merge_scatter (copy t of a value against its count c in the other list;
 // ties: cov0's copies first).
 constexpr int kMS = 4096;               // max small side
-#ifndef SG_MERGE_SEG
-#define SG_MERGE_SEG 1  // L copied gap by gap (see k_merge_small)
-#endif
+// A pair takes the gap-copy path (k_merge_small) when the large side is at
+// least this many times the small one (long gaps); dense interleavings (the
+// corpus folds of similar-sized lists) merge tile by tile.
+constexpr uint64_t kGapRatio = 32;
 constexpr int kMT = 1024;               // threads
 constexpr int kMU = kMS / kMT;          // small elements per thread (consecutive)
 #ifndef SG_KML
 #define SG_KML 8
 #endif
 constexpr int kML = SG_KML;             // large elements per thread per tile
-[[maybe_unused]] constexpr int kMTile = kMT * kML;  // 8192
+constexpr int kMTile = kMT * kML;       // 8192
 constexpr int kMWaves = kMT / 64;       // 16
 
 struct SmallArgs {
@@ -247,20 +248,17 @@ __device__ __forceinline__ uint32_t ballot_count(const uint32_t* sv, uint32_t ns
   }
 }
 
+template <bool kGap>
 __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_merge_small(SmallArgs m) {
   __shared__ uint32_t sv[kMS];
-#if SG_MERGE_SEG
-  __shared__ uint32_t sdx[kMS];        // dropped L elements of the values before element j's
-  __shared__ uint16_t rll[kMS];        // last S index of each run (distinct value)
+  __shared__ uint32_t sdx[kGap ? kMS : 1];  // gap path: dropped L elements of the values before element j's
+  __shared__ uint16_t rll[kGap ? kMS : 1];  // gap path: last S index of each run (distinct value)
   __shared__ uint32_t red2[kMWaves + 1];
   __shared__ uint64_t nl_eff_s;
-#endif
   __shared__ uint32_t skp[kMS + 1];    // kept small elements before j
   __shared__ uint32_t sidx[kMS];       // insertion point of small element j in L
-#if !SG_MERGE_SEG
-  __shared__ unsigned long long tw[kML * kMWaves];
-  __shared__ uint32_t twp[kML * kMWaves + 1];
-#endif
+  __shared__ unsigned long long tw[kGap ? 1 : kML * kMWaves];
+  __shared__ uint32_t twp[kGap ? 1 : kML * kMWaves + 1];
   __shared__ uint32_t red[kMWaves + 1];
   const uint32_t k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -275,13 +273,13 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   __syncthreads();
   // S: keep flags (copy t against the count in L) and insertion points in L
   uint32_t flags = 0;
-#if SG_MERGE_SEG
-  // L copies of a value S also holds are dropped up to S's count (the keep
+  if ((nl >= kGapRatio * ns) != kGap) return;  // the other instantiation's pair
+  constexpr bool gap = kGap;
+  // gap path: L copies of a value S also holds are dropped up to S's count (the keep
   // rule for L's side: Union when L is cov1, SymmetricDifference)
   const bool ldrop = m.op == SG_OP_SYMDIFF || sL == 1;
   uint32_t rlast = 0;  // bit u: element u is the last copy of its value in S
   uint64_t dpk = 0;    // its value's dropped L copies, 16 bits per u
-#endif
   {
     uint32_t x[kMU];
     uint64_t lb[kMU], ub[kMU];
@@ -307,7 +305,7 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
       const bool kp = x[u] != kSent && keep_rule(m.op, sS, t, ub[u] - lb[u]);  // cover.go:97
       flags |= (kp ? 1u : 0u) << u;
-#if SG_MERGE_SEG
+      if (gap) {
       sidx[j] = (uint32_t)lb[u];
       // the last copy of its value in S: the value's dropped L copies (the
       // first min(cS, cL), cS = t + 1) are counted here, so the exclusive
@@ -319,9 +317,9 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         rlast |= 1u << u;
         dpk |= (uint64_t)d << (16 * u);
       }
-#else
-      sidx[j] = (uint32_t)(sS == 0 ? lb[u] : ub[u]);
-#endif
+      } else {
+        sidx[j] = (uint32_t)(sS == 0 ? lb[u] : ub[u]);
+      }
     }
   }
   {  // exclusive scan of the kept counts, thread order = element order
@@ -350,8 +348,7 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
   __syncthreads();
   const uint32_t KS = skp[ns];
-#if SG_MERGE_SEG
-  {
+  if (gap) {
     // L is S's values' runs and the gaps between them: every kept L element
     // of a gap moves by the same amount (kept S elements before it minus
     // dropped L elements before it), so the gaps are copied whole, as
@@ -434,8 +431,8 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
     }
     if (tid == 0) m.olen[k] = (uint64_t)KS + nle - dtot;
+    return;
   }
-#else
   // L: stream tiles in index order
   uint32_t KL = 0, jlo = 0, jp = 0;
   uint32_t xn[kML];  // the next tile's L values, in flight while a tile is processed
@@ -573,7 +570,6 @@ __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (uint32_t j = jlo + tid; j < ns; j += kMT)  // insertion point past the end of L
     if (skp[j + 1] > skp[j]) out[skp[j] + KL] = sv[j];
   if (tid == 0) m.olen[k] = (uint64_t)KS + KL;
-#endif
 }
 
 __global__ void k_merge_len(MergeArgs m) {
@@ -855,7 +851,8 @@ int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint3
     SmallArgs sm{op, da, db, m_abeg, m_alen, m_bbeg, m_blen, m_obeg, m_olen, dout};
     {
       ScopedTimer tm(ctx, "merge_small");
-      hipLaunchKernelGGL(k_merge_small, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
+      hipLaunchKernelGGL(k_merge_small<true>, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
+      hipLaunchKernelGGL(k_merge_small<false>, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
     }
   } else {
     MergeArgs m{};
