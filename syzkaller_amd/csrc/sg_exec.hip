@@ -103,10 +103,14 @@ __device__ __forceinline__ unsigned long long mark_val(uint32_t pos, uint32_t d,
   return ((unsigned long long)pos << 45) | ((unsigned long long)d << 32) | sig;
 }
 
+// kCount (diagnostics, SG_DEBUG_PART): stats[0..2] += windows, speculative
+// passes, edges of the wave's program.
+template <bool kCount>
 __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__ pcs,
                                                     const uint64_t* __restrict__ call_off,
                                                     const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
-                                                    uint32_t* __restrict__ cnt) {
+                                                    uint32_t* __restrict__ cnt, unsigned long long* stats) {
+  uint64_t n_win = 0, n_pass = 0, n_edge = 0;
   __shared__ uint32_t table[kDedupSize];
   __shared__ unsigned long long markA[kMarkN], markB[kMarkN];
   const int lane = threadIdx.x;
@@ -146,7 +150,12 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
       const uint32_t sig0 = pc0 ^ hp0, sig1 = pc1 ^ hp1;  // executor.h:393-395
       carry = nvalid > 64 ? __builtin_amdgcn_readlane(h1, nvalid - 65) : __builtin_amdgcn_readlane(h0, nvalid - 1);
       uint64_t keep0 = 0, keep1 = 0;
+      if (kCount) {
+        n_win++;
+        n_edge += (uint64_t)nvalid;
+      }
       for (int start = 0; start < nvalid;) {
+        if (kCount) n_pass++;
         const bool act0 = (int)pos0 >= start && (int)pos0 < nvalid, act1 = (int)pos1 >= start && (int)pos1 < nvalid;
         uint32_t d0, d1;
         bool dup0, dup1;
@@ -216,6 +225,11 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
       outpos += __popcll(keep1);
     }
     if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
+  }
+  if (kCount && lane == 0) {
+    atomicAdd(&stats[0], (unsigned long long)n_win);
+    atomicAdd(&stats[1], (unsigned long long)n_pass);
+    atomicAdd(&stats[2], (unsigned long long)n_edge);
   }
 }
 
@@ -364,10 +378,21 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   uint32_t* tmp = (uint32_t*)ws_at(ctx, o_tmp);
   uint32_t* cnt = (uint32_t*)ws_at(ctx, o_cnt);
   SG_HIP(hipMemsetAsync(cnt, 0, ncalls * 4, ctx->stream));
-  if (nprog) {
+  if (nprog && ctx->debug_part) {  // diagnostics: speculative passes per 128-edge window (syncs)
+    unsigned long long* st = nullptr;
+    SG_HIP(hipMalloc(&st, 32));
+    SG_HIP(hipMemsetAsync(st, 0, 32, ctx->stream));
+    hipLaunchKernelGGL(k_exec_signal<true>, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off,
+                       d_prog_off, tmp, cnt, st);
+    unsigned long long h[3] = {0, 0, 0};
+    SG_HIP(hipMemcpy(h, st, 24, hipMemcpyDeviceToHost));
+    SG_HIP(hipFree(st));
+    fprintf(stderr, "sg exec: programs %llu windows %llu passes %llu (%.2f per window) edges %llu\n",
+            (unsigned long long)nprog, h[0], h[1], h[0] ? (double)h[1] / h[0] : 0.0, h[2]);
+  } else if (nprog) {
     ScopedTimer tm(ctx, "exec_signal");
-    hipLaunchKernelGGL(k_exec_signal, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off, d_prog_off,
-                       tmp, cnt);
+    hipLaunchKernelGGL(k_exec_signal<false>, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off,
+                       d_prog_off, tmp, cnt, (unsigned long long*)nullptr);
   }
   SG_HIP(hipGetLastError());
   rc = scan_counts(ctx, cnt, d_sig_off, ncalls, scan_off);
