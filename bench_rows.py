@@ -18,7 +18,10 @@ point (PCIe staging included), and the oracle on a bounded sample:
       output regions x 16 calls x 1024 signal words.
   f2  the manager's cover.Union folds (syz-manager/html.go:84/:94/:306): a
       50k-input corpus by syscall and over everything.
-Usage: python bench_rows.py [c1 c4 c5 a0 ipc f2]
+  f4  RPC payloads (pkg/rpctype/rpctype.go:8-63): delta-varint encode and
+      decode of 64k canonical RpcInput.Signal lists, and their sancov files
+      (tools/syz-execprog/execprog.go:159-177).
+Usage: python bench_rows.py [c1 c4 c5 a0 ipc f2 f4]
 """
 import json
 import os
@@ -271,11 +274,68 @@ def row_ipc(ctx, rng):
             "frac_hbm": algo / (dev / 1e3) / 1e9 / HBM, "parity_full": parity}
 
 
+def row_f4(ctx, rng):
+    """Delta-varint payloads of 64Ki canonical lists (Zipf PCs, up to 4096 per
+    list, as RpcInput.Signal carries) and the lists' sancov files: device time
+    of each batched entry point (host staging excluded), end to end with it,
+    parity with the oracle on a prefix and the decode round trip in full."""
+    from oracle import pyoracle as O
+
+    nl = 65536
+    lists = [np.unique(zipf_vals(rng, int(rng.integers(256, 6000)), s=1.05, nranks=1 << 22))[:4096]
+             for _ in range(nl)]
+    vals = np.concatenate(lists).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum([x.size for x in lists])]).astype(np.uint64)
+    N = int(vals.size)
+    C.delta_encode(vals[: off[64]], off[:65], ctx)  # warm
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    data, doff = C.delta_encode(vals, off, ctx)
+    t_enc = time.perf_counter() - t0
+    k_enc = ktime(ctx, ["rpc_encode"])
+    ctx.timing(False)
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    dv, dvo = C.delta_decode(data, doff, ctx)
+    t_dec = time.perf_counter() - t0
+    k_dec = ktime(ctx, ["rpc_decode"])
+    ctx.timing(False)
+    ncalls = 2048
+    ctx.timing(True)
+    sc = C.sancov(vals[: off[ncalls]], off[: ncalls + 1], ctx)
+    k_sc = ktime(ctx, ["sancov"])
+    ctx.timing(False)
+    m = 64
+    t0 = time.perf_counter()
+    ref = [O.delta_encode(x) for x in lists[:m]]
+    cpu = time.perf_counter() - t0
+    parity = (all(data[int(doff[k]):int(doff[k + 1])].tobytes() == ref[k] for k in range(m))
+              and np.array_equal(dv, vals) and np.array_equal(dvo, off)
+              and all(sc[k] == O.sancov(lists[k]) for k in range(8)))
+    B = int(doff[-1])
+    res = {"lists": nl, "values": N, "payload_bytes": B, "bytes_per_value": B / N, "parity": bool(parity),
+           "parity_scope": f"payload bytes of the first {m} lists and the first 8 sancov files vs the oracle; "
+                           "decode round trip of every list"}
+    # algorithmic bytes: values + offsets in, payload + byte offsets out (decode: the reverse)
+    algo = 4 * N + B + 16 * (nl + 1)
+    for name, k, wall in (("encode", k_enc.get("rpc_encode"), t_enc), ("decode", k_dec.get("rpc_decode"), t_dec)):
+        res[name] = {"device_ms": k, "end_to_end_ms": wall * 1e3, "values_per_s": N / (k / 1e3) if k else None,
+                     "frac_hbm": algo / (k / 1e3) / 1e9 / HBM if k else None}
+    nsc = int(off[ncalls])
+    res["sancov"] = {"calls": ncalls, "pcs": nsc, "device_ms": k_sc.get("sancov"),
+                     "frac_hbm": (12 * nsc + 16 * ncalls) / (k_sc["sancov"] / 1e3) / 1e9 / HBM if k_sc.get("sancov")
+                     else None}
+    res["byte_model"] = "4*values + payload bytes + 16*(lists+1) per encode / decode; 12 B per PC for sancov"
+    res["cpu_oracle_s_sample"] = cpu
+    res["cpu_sample"] = f"oracle delta_encode of the first {m} lists"
+    return {"row": "f4 RPC payloads", **res}
+
+
 def main():
     import torch
 
     torch.cuda.set_device(0)
-    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc", "f2"]
+    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc", "f2", "f4"]
     ctx = C.Context(0)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(2026)

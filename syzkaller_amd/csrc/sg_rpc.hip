@@ -44,10 +44,34 @@ __device__ __forceinline__ uint64_t list_of(const uint64_t* off, uint64_t n, uin
   return lo;
 }
 
+// kw[w] = list_of(min(32 w + 31, N - 1)) for w < ceil(N / 32).  Element i's
+// list lies between its word's bounds kw[w - 1] .. kw[w] (almost always one
+// list), so a per-element search of the whole offset table (a chain of ~17
+// dependent loads: 3-6 ms per 71M-value batch) becomes two cached loads.
+__global__ void k_word_lists(const uint64_t* __restrict__ off, uint64_t n, uint64_t N, uint64_t* __restrict__ kw) {
+  const uint64_t nw = (N + 31) / 32;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride)
+    kw[w] = list_of(off, n, 32 * w + 31 < N ? 32 * w + 31 : N - 1);
+}
+
+__device__ __forceinline__ uint64_t list_of_w(const uint64_t* off, const uint64_t* kw, uint64_t i) {
+  const uint64_t w = i >> 5;
+  uint64_t lo = w ? kw[w - 1] : 0, hi = kw[w];  // off[lo] <= 32 w - 1 < i (or lo = 0)
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
 // delta of element i within its list (the first one: itself); err on a descent
-__device__ __forceinline__ uint32_t elem_delta(const uint32_t* v, const uint64_t* off, uint64_t n, uint64_t i,
+__device__ __forceinline__ uint32_t elem_delta(const uint32_t* v, const uint64_t* off, const uint64_t* kw, uint64_t i,
                                                uint32_t* err) {
-  const uint64_t k = list_of(off, n, i);
+  const uint64_t k = list_of_w(off, kw, i);
   const uint32_t x = v[i];
   if (i == off[k]) return x;
   const uint32_t p = v[i - 1];
@@ -55,18 +79,20 @@ __device__ __forceinline__ uint32_t elem_delta(const uint32_t* v, const uint64_t
   return x - p;
 }
 
-__global__ void k_enc_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                          uint32_t* __restrict__ len, uint32_t* __restrict__ err) {
+__global__ void k_enc_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                          const uint64_t* __restrict__ kw, uint64_t N, uint32_t* __restrict__ len,
+                          uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride)
-    len[i] = varint_len(elem_delta(v, off, n, i, err));
+    len[i] = varint_len(elem_delta(v, off, kw, i, err));
 }
 
-__global__ void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                            const uint64_t* __restrict__ pos, uint8_t* __restrict__ out, uint32_t* __restrict__ err) {
+__global__ void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                            const uint64_t* __restrict__ kw, uint64_t N, const uint64_t* __restrict__ pos,
+                            uint8_t* __restrict__ out, uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
-    uint32_t d = elem_delta(v, off, n, i, err);
+    uint32_t d = elem_delta(v, off, kw, i, err);
     uint8_t* o = out + pos[i];
     while (d >= 0x80u) {  // binary.PutUvarint
       *o++ = (uint8_t)(d | 0x80u);
@@ -89,22 +115,32 @@ __global__ void k_dec_term(const uint8_t* __restrict__ in, uint64_t nb, uint32_t
     term[j] = (in[j] & 0x80u) ? 0u : 1u;
 }
 
+// heads bit j <=> byte j starts a non-empty list (the bitmap is zeroed first)
+__global__ void k_byte_heads(const uint64_t* __restrict__ in_off, uint64_t n, uint32_t* __restrict__ heads) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const uint64_t b = in_off[k];
+    if (b < in_off[k + 1]) atomicOr(&heads[b >> 5], 1u << (b & 31));
+  }
+}
+
+__device__ __forceinline__ bool is_head(const uint32_t* heads, uint64_t j) { return (heads[j >> 5] >> (j & 31)) & 1u; }
+
 // Each terminator decodes its run (back to the previous terminator or the
 // list's first byte); a run must be <= 5 bytes and fit 32 bits, and a list
-// must end on a terminator.
-__global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n, uint64_t nb,
+// must end on a terminator.  List starts come from the heads bitmap, so no
+// byte searches the offset table.
+__global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint32_t* __restrict__ heads, uint64_t nb,
                            const uint64_t* __restrict__ vidx, uint32_t* __restrict__ delta, uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
-    const uint64_t k = list_of(in_off, n, j);
-    const uint64_t b = in_off[k];
     const uint8_t c = in[j];
     if (c & 0x80u) {
-      if (j + 1 == in_off[k + 1]) *err = 1;  // the list ends inside a value
+      if (j + 1 == nb || is_head(heads, j + 1)) *err = 1;  // the list ends inside a value
       continue;
     }
     uint64_t s = j;
-    while (s > b && (in[s - 1] & 0x80u)) {
+    while (!is_head(heads, s) && s > 0 && (in[s - 1] & 0x80u)) {
       s--;
       if (j - s >= 5) break;
     }
@@ -120,25 +156,25 @@ __global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint64_t* __res
 
 // values of each list: running sums of its deltas (u64 scan), range-checked
 __global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t* __restrict__ excl,
-                             const uint64_t* __restrict__ voff, uint64_t n, uint64_t N, uint32_t* __restrict__ out,
-                             uint32_t* __restrict__ err) {
+                             const uint64_t* __restrict__ voff, const uint64_t* __restrict__ kw, uint64_t N,
+                             uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
-    const uint64_t k = list_of(voff, n, i);
+    const uint64_t k = list_of_w(voff, kw, i);
     const uint64_t v = excl[i] + delta[i] - excl[voff[k]];
     if (v > 0xFFFFFFFFull) *err = 1;
     out[i] = (uint32_t)v;
   }
 }
 
-__global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __restrict__ off, uint64_t n, uint64_t N,
-                         uint64_t* __restrict__ out) {
+__global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __restrict__ off,
+                         const uint64_t* __restrict__ kw, uint64_t n, uint64_t N, uint64_t* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N + n; i += stride) {
     if (i < n) {
       out[i + off[i]] = kSancovMagic;  // file i's header (execprog.go:166)
     } else {
-      const uint64_t e = i - n, k = list_of(off, n, e);
+      const uint64_t e = i - n, k = list_of_w(off, kw, e);
       out[k + 1 + e] = (0xFFFFFFFFull << 32) + cov[e];  // RestorePC(pc, 0xffffffff), cover.go:23-25
     }
   }
@@ -160,7 +196,7 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
                uint8_t** d_bytes) {
   WsPlan p;
   const size_t o_len = p.add(N * 4), o_pos = p.add((N + 1) * 8), o_lo = p.add((n + 1) * 8), o_err = p.add(8),
-               o_out = p.add(N * 5 + 8);
+               o_out = p.add(N * 5 + 8), o_kw = p.add((N + 31) / 32 * 8);
   const size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(N));
   if (rc) return rc;
@@ -169,15 +205,18 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
   uint64_t* lo = (uint64_t*)ws_at(ctx, o_lo);
   uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
   uint8_t* out = (uint8_t*)ws_at(ctx, o_out);
+  uint64_t* kw = (uint64_t*)ws_at(ctx, o_kw);
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   {
     ScopedTimer tm(ctx, "rpc_encode");
-    if (N)
-      hipLaunchKernelGGL(k_enc_len, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, n, N, len, err);
+    if (N) {
+      hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_off, n, N, kw);
+      hipLaunchKernelGGL(k_enc_len, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, kw, N, len, err);
+    }
     rc = scan_counts(ctx, len, pos, N, scan_off);
     if (rc) return rc;
     if (N)
-      hipLaunchKernelGGL(k_enc_write, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, n, N, pos, out, err);
+      hipLaunchKernelGGL(k_enc_write, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, kw, N, pos, out, err);
     hipLaunchKernelGGL(k_list_pos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_off, n, pos, lo);
   }
   SG_HIP(hipGetLastError());
@@ -199,7 +238,7 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
                uint64_t cap, uint64_t* h_off, uint64_t* d_voff) {
   WsPlan p;
   const size_t o_t = p.add(nb * 4), o_vi = p.add((nb + 1) * 8), o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8),
-               o_err = p.add(8);
+               o_err = p.add(8), o_hd = p.add((nb + 31) / 32 * 4), o_kwv = p.add((nb + 31) / 32 * 8);
   const size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nb));
   if (rc) return rc;
@@ -208,6 +247,8 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   uint32_t* delta = (uint32_t*)ws_at(ctx, o_d);
   uint64_t* excl = (uint64_t*)ws_at(ctx, o_x);
   uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
+  uint32_t* heads = (uint32_t*)ws_at(ctx, o_hd);
+  uint64_t* kwv = (uint64_t*)ws_at(ctx, o_kwv);  // N <= nb
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   ScopedTimer tm(ctx, "rpc_decode");
   if (nb) hipLaunchKernelGGL(k_dec_term, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, nb, term);
@@ -221,13 +262,18 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
     set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
     return SG_EINVAL;
   }
-  if (nb) hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, d_in_off, n, nb, vidx,
-                             delta, err);
+  if (nb) {
+    SG_HIP(hipMemsetAsync(heads, 0, (nb + 31) / 32 * 4, ctx->stream));
+    hipLaunchKernelGGL(k_byte_heads, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_in_off, n, heads);
+    hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, heads, nb, vidx, delta, err);
+  }
   rc = scan_counts(ctx, delta, excl, N, scan_off);
   if (rc) return rc;
-  if (N)
-    hipLaunchKernelGGL(k_dec_values, dim3(grid_for(N)), dim3(256), 0, ctx->stream, delta, excl, d_voff, n, N, d_vals,
+  if (N) {
+    hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_voff, n, N, kwv);
+    hipLaunchKernelGGL(k_dec_values, dim3(grid_for(N)), dim3(256), 0, ctx->stream, delta, excl, d_voff, kwv, N, d_vals,
                        err);
+  }
   SG_HIP(hipGetLastError());
   uint32_t herr = 0;
   SG_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -385,16 +431,21 @@ int sg_sancov_batch(sg_ctx* ctx, const uint32_t* cov, const uint64_t* cov_off, s
   int rc = ensure_device(ctx);
   if (rc) return rc;
   const size_t b_v = (N * 4 + 255) & ~size_t(255), b_o = ((n + 1) * 8 + 255) & ~size_t(255);
-  rc = dstage_reserve(ctx, b_v + b_o + (N + n) * 8);
+  const size_t b_w = ((N + 31) / 32 * 8 + 255) & ~size_t(255);
+  rc = dstage_reserve(ctx, b_v + b_o + b_w + (N + n) * 8);
   if (rc) return rc;
   uint32_t* dv = (uint32_t*)ctx->dstage;
   uint64_t* doff = (uint64_t*)((char*)ctx->dstage + b_v);
-  uint64_t* dout = (uint64_t*)((char*)ctx->dstage + b_v + b_o);
+  uint64_t* kw = (uint64_t*)((char*)ctx->dstage + b_v + b_o);
+  uint64_t* dout = (uint64_t*)((char*)ctx->dstage + b_v + b_o + b_w);
   if (N) SG_HIP(hipMemcpyAsync(dv, cov, N * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(doff, cov_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   {
     ScopedTimer tm(ctx, "sancov");
-    hipLaunchKernelGGL(k_sancov, dim3(grid_for(N + n)), dim3(256), 0, ctx->stream, dv, doff, (uint64_t)n, N, dout);
+    if (N)
+      hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, doff, (uint64_t)n, N,
+                         kw);
+    hipLaunchKernelGGL(k_sancov, dim3(grid_for(N + n)), dim3(256), 0, ctx->stream, dv, doff, kw, (uint64_t)n, N, dout);
   }
   SG_HIP(hipGetLastError());
   SG_HIP(hipMemcpyAsync(out, dout, (N + n) * 8, hipMemcpyDeviceToHost, ctx->stream));
