@@ -79,21 +79,39 @@ __device__ __forceinline__ uint32_t elem_delta(const uint32_t* v, const uint64_t
   return x - p;
 }
 
-__global__ void k_enc_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
-                          const uint64_t* __restrict__ kw, uint64_t N, uint32_t* __restrict__ len,
-                          uint32_t* __restrict__ err) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride)
-    len[i] = varint_len(elem_delta(v, off, kw, i, err));
+// Encode: per 64-element group (one wave, lanes in element order) the bytes
+// of its varints; a scan of the group totals; then each element's byte
+// position = its group's base + a wave prefix sum (no per-element position
+// array).  The grid-stride loops keep whole waves on whole groups.
+__device__ __forceinline__ uint32_t enc_len_at(const uint32_t* v, const uint64_t* off, const uint64_t* kw, uint64_t N,
+                                               uint64_t i, uint32_t* err) {
+  return i < N ? varint_len(elem_delta(v, off, kw, i, err)) : 0u;
 }
 
-__global__ void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
-                            const uint64_t* __restrict__ kw, uint64_t N, const uint64_t* __restrict__ pos,
-                            uint8_t* __restrict__ out, uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(256) void k_enc_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                                                 const uint64_t* __restrict__ kw, uint64_t N,
+                                                 uint32_t* __restrict__ gsum, uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
-    uint32_t d = elem_delta(v, off, kw, i, err);
-    uint8_t* o = out + pos[i];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < N; g0 += stride) {
+    const uint32_t incl = sgd::wave_incl_add(enc_len_at(v, off, kw, N, g0 + lane, err));
+    if (lane == 63) gsum[g0 >> 6] = incl;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                                                   const uint64_t* __restrict__ kw, uint64_t N,
+                                                   const uint64_t* __restrict__ gbase, uint8_t* __restrict__ out,
+                                                   uint32_t* __restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < N; g0 += stride) {
+    const uint64_t i = g0 + lane;
+    uint32_t d = i < N ? elem_delta(v, off, kw, i, err) : 0u;
+    const uint32_t len = i < N ? varint_len(d) : 0u;
+    const uint32_t incl = sgd::wave_incl_add(len);
+    if (i >= N) continue;
+    uint8_t* o = out + gbase[g0 >> 6] + (incl - len);
     while (d >= 0x80u) {  // binary.PutUvarint
       *o++ = (uint8_t)(d | 0x80u);
       d >>= 7;
@@ -102,17 +120,18 @@ __global__ void k_enc_write(const uint32_t* __restrict__ v, const uint64_t* __re
   }
 }
 
-// byte offsets of the lists: out_off[k] = pos[off[k]]
-__global__ void k_list_pos(const uint64_t* __restrict__ off, uint64_t n, const uint64_t* __restrict__ pos,
-                           uint64_t* __restrict__ out_off) {
+// byte offsets of the lists: out_off[k] = gbase[g] + the bytes of group g's
+// elements before off[k] (g = off[k] / 64)
+__global__ void k_list_bpos(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                            const uint64_t* __restrict__ kw, uint64_t n, uint64_t N,
+                            const uint64_t* __restrict__ gbase, uint32_t* __restrict__ err,
+                            uint64_t* __restrict__ out_off) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k <= n) out_off[k] = pos[off[k]];
-}
-
-__global__ void k_dec_term(const uint8_t* __restrict__ in, uint64_t nb, uint32_t* __restrict__ term) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride)
-    term[j] = (in[j] & 0x80u) ? 0u : 1u;
+  if (k > n) return;
+  const uint64_t o = off[k];
+  uint64_t p = gbase[o >> 6];
+  for (uint64_t i = o & ~63ull; i < o; i++) p += enc_len_at(v, off, kw, N, i, err);
+  out_off[k] = p;
 }
 
 // heads bit j <=> byte j starts a non-empty list (the bitmap is zeroed first)
@@ -126,31 +145,97 @@ __global__ void k_byte_heads(const uint64_t* __restrict__ in_off, uint64_t n, ui
 
 __device__ __forceinline__ bool is_head(const uint32_t* heads, uint64_t j) { return (heads[j >> 5] >> (j & 31)) & 1u; }
 
-// Each terminator decodes its run (back to the previous terminator or the
-// list's first byte); a run must be <= 5 bytes and fit 32 bits, and a list
-// must end on a terminator.  List starts come from the heads bitmap, so no
-// byte searches the offset table.
+// Decode works on 32-byte blocks (block b = bytes 32 b .. 32 b + 31; its
+// head bits are the word heads[b]).  Pass 1: each block's terminators (bytes
+// with the high bit clear end a value) as a mask and a count.
+__device__ __forceinline__ void load_block(const uint8_t* in, uint64_t nb, uint64_t b, uint32_t (&w)[8]) {
+  const uint64_t j0 = 32 * b;
+  if (j0 + 32 <= nb) {
+    const uint4* q = reinterpret_cast<const uint4*>(in + j0);
+    const uint4 x = q[0], y = q[1];
+    w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = 0x80808080u;  // past nb: continuation bytes (never terminators)
+    for (uint64_t j = j0; j < nb; j++) {
+      const uint32_t i = (uint32_t)(j - j0), sh = 8 * (i & 3);
+      w[i >> 2] = (w[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)in[j] << sh);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t block_terms(const uint32_t (&w)[8]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) m |= (((w[i >> 2] >> (8 * (i & 3) + 7)) & 1u) ^ 1u) << i;
+  return m;
+}
+
+__global__ void k_dec_count(const uint8_t* __restrict__ in, uint64_t nb, uint32_t* __restrict__ tmask,
+                            uint32_t* __restrict__ tcnt) {
+  const uint64_t nblk = (nb + 31) / 32, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += stride) {
+    uint32_t w[8];
+    load_block(in, nb, b, w);
+    const uint32_t m = block_terms(w);
+    tmask[b] = m;
+    tcnt[b] = __popc(m);
+  }
+}
+
+// value offsets of the lists: voff[k] = terminators before byte in_off[k]
+__global__ void k_list_vpos(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ vbase,
+                            const uint32_t* __restrict__ tmask, uint64_t* __restrict__ voff) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n) return;
+  const uint64_t o = in_off[k], b = o >> 5;
+  const uint32_t r = (uint32_t)(o & 31);
+  voff[k] = vbase[b] + (r ? __popc(tmask[b] & ((1u << r) - 1u)) : 0u);
+}
+
+// Pass 2: each block walks its bytes in order.  A run starts after a
+// terminator or at a list start; the run the block opens inside is found by
+// looking back at most 4 bytes.  Checks (as binary.Uvarint): a run must be <=
+// 5 bytes and fit 32 bits, and a list must end on a terminator.
 __global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint32_t* __restrict__ heads, uint64_t nb,
-                           const uint64_t* __restrict__ vidx, uint32_t* __restrict__ delta, uint32_t* __restrict__ err) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
-    const uint8_t c = in[j];
-    if (c & 0x80u) {
-      if (j + 1 == nb || is_head(heads, j + 1)) *err = 1;  // the list ends inside a value
-      continue;
+                           const uint64_t* __restrict__ vbase, uint32_t* __restrict__ delta,
+                           uint32_t* __restrict__ err) {
+  const uint64_t nblk = (nb + 31) / 32, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += stride) {
+    const uint64_t j0 = 32 * b;
+    uint32_t w[8];
+    load_block(in, nb, b, w);
+    const uint32_t hm = heads[b];
+    const uint32_t hnext = j0 + 32 < nb ? heads[b + 1] & 1u : 0u;  // does the next block start a list
+    // the run open at j0: its start s and the value bits so far
+    uint64_t s = j0;
+    while (s > 0 && !is_head(heads, s) && (in[s - 1] & 0x80u) && j0 - s < 5) s--;
+    uint64_t d = 0;
+    for (uint64_t q = s; q < j0; q++) d |= (uint64_t)(in[q] & 0x7Fu) << (7 * (q - s));
+    uint64_t vi = vbase[b];
+    bool bad = false;
+    const uint32_t len = j0 + 32 <= nb ? 32u : (uint32_t)(nb - j0);
+    for (uint32_t i = 0; i < len; i++) {
+      const uint64_t j = j0 + i;
+      if ((hm >> i) & 1u) {
+        s = j;
+        d = 0;
+      }
+      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      const uint64_t r = j - s;  // position in the run
+      if (r < 5) d |= (uint64_t)(c & 0x7Fu) << (7 * r);
+      if (c & 0x80u) {
+        // the list ends inside a value
+        const bool last = j + 1 == nb || (i < 31 ? ((hm >> (i + 1)) & 1u) : hnext);
+        bad |= last;
+      } else {
+        bad |= r >= 5 || d > 0xFFFFFFFFull;  // more than 32 bits
+        delta[vi++] = (uint32_t)d;
+        s = j + 1;
+        d = 0;
+      }
     }
-    uint64_t s = j;
-    while (!is_head(heads, s) && s > 0 && (in[s - 1] & 0x80u)) {
-      s--;
-      if (j - s >= 5) break;
-    }
-    if (j - s >= 5 || (j - s == 4 && c > 0x0Fu)) {  // more than 32 bits
-      *err = 1;
-      continue;
-    }
-    uint32_t d = 0;
-    for (uint64_t q = s; q <= j; q++) d |= (uint32_t)(in[q] & 0x7Fu) << (7 * (q - s));
-    delta[vidx[j]] = d;
+    if (bad) *err = 1;
   }
 }
 
@@ -195,7 +280,8 @@ bool offsets_ok(const uint64_t* off, size_t n) {
 int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t n, uint64_t N, uint64_t* h_out_off,
                uint8_t** d_bytes) {
   WsPlan p;
-  const size_t o_len = p.add(N * 4), o_pos = p.add((N + 1) * 8), o_lo = p.add((n + 1) * 8), o_err = p.add(8),
+  const uint64_t ng = (N + 63) / 64;
+  const size_t o_len = p.add(ng * 4 + 4), o_pos = p.add((ng + 1) * 8), o_lo = p.add((n + 1) * 8), o_err = p.add(8),
                o_out = p.add(N * 5 + 8), o_kw = p.add((N + 31) / 32 * 8);
   const size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(N));
@@ -213,11 +299,12 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
       hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_off, n, N, kw);
       hipLaunchKernelGGL(k_enc_len, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, kw, N, len, err);
     }
-    rc = scan_counts(ctx, len, pos, N, scan_off);
+    rc = scan_counts(ctx, len, pos, ng, scan_off);  // pos = group byte bases (pos[ng] = total)
     if (rc) return rc;
     if (N)
       hipLaunchKernelGGL(k_enc_write, dim3(grid_for(N)), dim3(256), 0, ctx->stream, d_v, d_off, kw, N, pos, out, err);
-    hipLaunchKernelGGL(k_list_pos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_off, n, pos, lo);
+    hipLaunchKernelGGL(k_list_bpos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_v, d_off, kw, n, N, pos, err,
+                       lo);
   }
   SG_HIP(hipGetLastError());
   uint32_t herr = 0;
@@ -236,14 +323,17 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
 // (capacity cap); h_off (host, n+1) gets the value offsets.  Scratch in ws.
 int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n, uint64_t nb, uint32_t* d_vals,
                uint64_t cap, uint64_t* h_off, uint64_t* d_voff) {
+  const uint64_t nblk = (nb + 31) / 32;
   WsPlan p;
-  const size_t o_t = p.add(nb * 4), o_vi = p.add((nb + 1) * 8), o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8),
-               o_err = p.add(8), o_hd = p.add((nb + 31) / 32 * 4), o_kwv = p.add((nb + 31) / 32 * 8);
+  const size_t o_tm = p.add(nblk * 4 + 4), o_tc = p.add(nblk * 4 + 4), o_vb = p.add((nblk + 1) * 8),
+               o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8), o_err = p.add(8), o_hd = p.add(nblk * 4 + 4),
+               o_kwv = p.add(nblk * 8);
   const size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nb));
   if (rc) return rc;
-  uint32_t* term = (uint32_t*)ws_at(ctx, o_t);
-  uint64_t* vidx = (uint64_t*)ws_at(ctx, o_vi);
+  uint32_t* tmask = (uint32_t*)ws_at(ctx, o_tm);
+  uint32_t* tcnt = (uint32_t*)ws_at(ctx, o_tc);
+  uint64_t* vbase = (uint64_t*)ws_at(ctx, o_vb);
   uint32_t* delta = (uint32_t*)ws_at(ctx, o_d);
   uint64_t* excl = (uint64_t*)ws_at(ctx, o_x);
   uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
@@ -251,10 +341,11 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   uint64_t* kwv = (uint64_t*)ws_at(ctx, o_kwv);  // N <= nb
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   ScopedTimer tm(ctx, "rpc_decode");
-  if (nb) hipLaunchKernelGGL(k_dec_term, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, nb, term);
-  rc = scan_counts(ctx, term, vidx, nb, scan_off);
+  if (nb) hipLaunchKernelGGL(k_dec_count, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, nb, tmask, tcnt);
+  rc = scan_counts(ctx, tcnt, vbase, nblk, scan_off);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_list_pos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vidx, d_voff);
+  hipLaunchKernelGGL(k_list_vpos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vbase, tmask,
+                     d_voff);
   SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint64_t N = h_off[n];
@@ -263,9 +354,9 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
     return SG_EINVAL;
   }
   if (nb) {
-    SG_HIP(hipMemsetAsync(heads, 0, (nb + 31) / 32 * 4, ctx->stream));
+    SG_HIP(hipMemsetAsync(heads, 0, nblk * 4 + 4, ctx->stream));
     hipLaunchKernelGGL(k_byte_heads, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_in_off, n, heads);
-    hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nb)), dim3(256), 0, ctx->stream, d_in, heads, nb, vidx, delta, err);
+    hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, heads, nb, vbase, delta, err);
   }
   rc = scan_counts(ctx, delta, excl, N, scan_off);
   if (rc) return rc;

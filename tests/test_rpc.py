@@ -108,3 +108,40 @@ def test_sancov_batch_vs_oracle(ctx):
     assert len(files) == len(covs)
     for k, c in enumerate(covs):
         assert files[k] == O.sancov(c), k
+
+
+@pytest.mark.gpu
+def test_delta_decode_corrupted_payloads_vs_oracle(ctx):
+    """Decode accepts / rejects exactly what binary.Uvarint + a running sum do
+    (oracle), on payloads with flipped high bits and cut ends, including runs
+    that cross the decoder's 32-byte blocks and list boundaries."""
+    from syzkaller_amd import cover as C
+    from syzkaller_amd._lib import SyzSigError
+
+    rng = np.random.default_rng(7)
+    for t in range(120):
+        parts = []
+        for _ in range(int(rng.integers(1, 4))):
+            m = int(rng.integers(0, 60))
+            v = np.sort(rng.integers(0, 1 << 32, size=m, dtype=np.uint64)).astype(np.uint32)
+            parts.append(bytearray(O.delta_encode(v)))
+        for p in parts:
+            if p and rng.random() < 0.7:
+                for _ in range(int(rng.integers(1, 4))):
+                    p[int(rng.integers(0, len(p)))] ^= 0x80
+            if p and rng.random() < 0.2:
+                del p[int(rng.integers(0, len(p))):]
+        expect = []
+        try:
+            for p in parts:
+                expect.append(O.delta_decode(bytes(p)))
+        except ValueError:
+            expect = None
+        data = b"".join(bytes(p) for p in parts)
+        doff = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.uint64)
+        if expect is None:
+            with pytest.raises(SyzSigError):
+                C.delta_decode(data, doff, ctx=ctx)
+            continue
+        gv, go = C.delta_decode(data, doff, ctx=ctx)
+        assert [gv[int(go[k]):int(go[k + 1])].tolist() for k in range(len(parts))] == expect, t
