@@ -21,7 +21,9 @@ point (PCIe staging included), and the oracle on a bounded sample:
   f4  RPC payloads (pkg/rpctype/rpctype.go:8-63): delta-varint encode and
       decode of 64k canonical RpcInput.Signal lists, and their sancov files
       (tools/syz-execprog/execprog.go:159-177).
-Usage: python bench_rows.py [c1 c4 c5 a0 ipc f2 f4]
+  a2  batched Canonicalize (cover.go:28-40; fuzzer.go:601 before every
+      NewInput): 64k raw per-call signal lists (Zipf, duplicates, up to 1024).
+Usage: python bench_rows.py [c1 c4 c5 a0 ipc f2 f4 a2]
 """
 import json
 import os
@@ -331,11 +333,47 @@ def row_f4(ctx, rng):
     return {"row": "f4 RPC payloads", **res}
 
 
+def row_a2(ctx, rng):
+    """Canonicalize of 64Ki unsorted per-call signal lists with duplicates
+    (lengths uniform in [0, 1024], Zipf values): device time of the sort and
+    of the unique pass, parity with the oracle on a prefix."""
+    from oracle import pyoracle as O
+
+    nl = 65536
+    lens = rng.integers(0, 1025, size=nl)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    N = int(off[-1])
+    raw = zipf_vals(rng, N, s=1.1, nranks=1 << 22)
+    v = raw.copy()
+    C.canonicalize_batch(v[: int(off[64])], off[:65], ctx)  # warm
+    v = raw.copy()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    out_len = C.canonicalize_batch(v, off, ctx)
+    wall = time.perf_counter() - t0
+    kt = ktime(ctx, ["canon_sort", "canon_unique", "scan"])
+    ctx.timing(False)
+    m = 256
+    t0 = time.perf_counter()
+    ref = [O.canonicalize(raw[int(off[k]):int(off[k + 1])]) for k in range(m)]
+    cpu = time.perf_counter() - t0
+    parity = all(int(out_len[k]) == n and np.array_equal(v[int(off[k]):int(off[k]) + n], a[:n])
+                 for k, (a, n) in enumerate(ref))
+    dev = sum(x for k, x in kt.items() if k != "scan")
+    algo = 4 * N + 4 * int(out_len.sum()) + 16 * (nl + 1)
+    return {"row": "a2 batched Canonicalize", "lists": nl, "elements": N, "unique_out": int(out_len.sum()),
+            "kernels_ms": kt, "device_ms": dev, "end_to_end_ms": wall * 1e3,
+            "elements_per_s": N / (dev / 1e3) if dev else None,
+            "frac_hbm": algo / (dev / 1e3) / 1e9 / HBM if dev else None,
+            "byte_model": "4*(elements_in + elements_out) + 16*(lists+1)", "parity": bool(parity),
+            "parity_scope": f"first {m} lists vs the oracle", "cpu_oracle_s_sample": cpu}
+
+
 def main():
     import torch
 
     torch.cuda.set_device(0)
-    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc", "f2", "f4"]
+    rows = sys.argv[1:] or ["c1", "c4", "c5", "a0", "ipc", "f2", "f4", "a2"]
     ctx = C.Context(0)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(2026)
