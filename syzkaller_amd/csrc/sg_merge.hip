@@ -679,7 +679,22 @@ struct CanonArgs {
   uint64_t nchunks;
   uint32_t* out;
   uint64_t* out_len;
+  uint64_t* ks;  // ks[w] = segment of element min(64 w + 63, n - 1)
 };
+
+// Element u's segment lies between ks[w - 1] and ks[w] (w = u / 64; almost
+// always one segment), so the per-element search is one or two cached loads
+// instead of a chain of ~17 dependent ones over the whole offset table.
+__global__ void k_canon_segs(CanonArgs a) {
+  const uint64_t nw = (a.n + 63) / 64, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride)
+    a.ks[w] = sgd::seg_search(a.off, 0, a.nseg - 1, std::min<uint64_t>(64 * w + 63, a.n - 1));
+}
+
+__device__ __forceinline__ uint64_t canon_seg(const CanonArgs& a, uint64_t u) {
+  const uint64_t w = u >> 6;
+  return sgd::seg_search(a.off, w ? a.ks[w - 1] : 0, a.ks[w], u);
+}
 
 __global__ __launch_bounds__(kBlock) void k_unique_keep(CanonArgs a) {
   const int lane = threadIdx.x & 63;
@@ -689,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void k_unique_keep(CanonArgs a) {
   for (int q = 0; q < 4; q++) {
     uint64_t u = c * kChunk + lane * 4 + q;
     if (u >= a.n) continue;
-    uint64_t k = sgd::seg_search(a.off, 0, a.nseg - 1, u);
+    uint64_t k = canon_seg(a, u);
     const uint32_t* b = a.buf[a.parity[k]];
     uint32_t x = b[u];
     uint32_t last = u == a.off[k] ? kSent : b[u - 1];  // cover.go:31-37
@@ -713,7 +728,7 @@ __global__ void k_unique_len(CanonArgs a) {
 __global__ void k_unique_write(CanonArgs a) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < a.n; u += stride) {
-    uint64_t k = sgd::seg_search(a.off, 0, a.nseg - 1, u);
+    uint64_t k = canon_seg(a, u);
     const uint32_t* b = a.buf[a.parity[k]];
     uint32_t x = b[u];
     uint64_t s = a.off[k];
@@ -750,7 +765,7 @@ int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_
   size_t o_b0 = p.add(n * 4), o_b1 = p.add(n * 4), o_ch = p.add(chunks.size() * sizeof(SortChunk)),
          o_big = p.add(big.size() * sizeof(BigSeg)), o_vs = p.add(vs.size() * 8), o_off = p.add((nseg + 1) * 8),
          o_par = p.add(nseg), o_mask = p.add(nchunks * 32), o_cnt = p.add(nchunks * 4),
-         o_base = p.add((nchunks + 1) * 8), o_len = p.add(nseg * 8);
+         o_base = p.add((nchunks + 1) * 8), o_len = p.add(nseg * 8), o_ks = p.add((n + 63) / 64 * 8);
   size_t scan_off = p.total;
   int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nchunks));
   if (rc) return rc;
@@ -800,8 +815,12 @@ int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_
   a.nchunks = nchunks;
   a.out = d_vals;
   a.out_len = dlen;
+  a.ks = (uint64_t*)ws_at(ctx, o_ks);
   {
     ScopedTimer tm(ctx, "canon_unique");
+    if (n)
+      hipLaunchKernelGGL(k_canon_segs, dim3((uint32_t)std::min<uint64_t>(div_up((n + 63) / 64, 256), 16384)), dim3(256),
+                         0, ctx->stream, a);
     hipLaunchKernelGGL(k_unique_keep, dim3(div_up(nchunks, kBlock / 64)), dim3(kBlock), 0, ctx->stream, a);
     rc = scan_counts(ctx, a.cnt, a.base, nchunks, scan_off);
     if (rc) return rc;
