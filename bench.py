@@ -173,24 +173,29 @@ def step_bytes(a):
     return 4 * a["n_in"] + 4 * a["n_uniq"] + 12 * a["n_cand"] + 4 * a["n_diff"] + a["n_rec"] / 8
 
 
-def pmc_bytes_per_step(kernels):
-    """HBM bytes per step from the PMC summary committed under profiles/
-    (separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), summed over
-    the step's kernels, or None."""
+def pmc_bytes_per_step(kernels, workload):
+    """HBM bytes per step of `workload` ("c2", "steady", "from_traces") from the
+    PMC summary committed under profiles/ (separate FETCH_SIZE / WRITE_SIZE
+    passes over that workload's own timed launches, gfx950-corrected), summed
+    over the step's kernels, or None when the summary holds no measurement of
+    this workload or of another kernel set."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             d = json.load(f)
     except Exception:
         return None, None
-    per = d.get("kernels", {})
+    w = d.get("workloads", {}).get(workload)
+    if not w:
+        return None, None
+    per = w.get("kernels", {})
     tot, seen = 0.0, []
     for k in kernels:
         if k in per and per[k].get("hbm_bytes_per_launch") is not None:
-            tot += per[k]["hbm_bytes_per_launch"]
+            tot += per[k]["hbm_bytes_per_launch"] * per[k].get("launches_per_step", 1)
             seen.append(k)
         elif k not in ("scan", "bucket_spill"):  # a summary of another kernel set: stale
             return None, None
-    return (tot if seen else None), d.get("tag")
+    return (tot if seen else None), f"{d.get('tag')}/{workload}"
 
 
 class StepTimer:
@@ -207,6 +212,16 @@ class StepTimer:
     def spans(self):
         torch.cuda.synchronize()
         return [self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(len(self.ev) - 1)]
+
+
+def cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        return None
 
 
 def cpu_info():
@@ -226,7 +241,7 @@ def cpu_info():
     return model, os.cpu_count(), avail
 
 
-def cpu_baseline(m0_values, batch, calls, gpu_flags, budget_s, threads):
+def cpu_baseline(m0_values, batch, calls, gpu_flags, budget_s, threads, threads_nproc=None):
     """The oracle on a bounded prefix of one batch, from the same starting
     maxSignal: (i) single-threaded, the reference's per-exec structure
     (fuzzer.go:661-691 under signalMu), with a parity check against the GPU's
@@ -262,16 +277,24 @@ def cpu_baseline(m0_values, batch, calls, gpu_flags, budget_s, threads):
     parity = bool(np.array_equal(flags, gpu_flags[: flags.size])) if gpu_flags is not None else None
     queued_frac = float(flags.mean()) if flags.size else None
     del ms
-    # (ii) the same prefix with `threads` procs under the reader-writer lock
+    # (ii) the same prefix with P procs under the reader-writer lock: P =
+    # `threads` (the box's CPU share) and P = nproc (SURVEY.md §8(d) leg (ii))
     e1 = int(off[done_prog * calls])
     v = batch.vals[:e1].cpu().numpy().view(np.uint32)
     o = off[: done_prog * calls + 1].astype(np.uint64)
     pr = np.arange(0, done_prog * calls + 1, calls, dtype=np.uint64)
-    ms = O.OSet(m0_values)
-    t = time.perf_counter()
-    _, used = O.triage_procs(ms, None, v, o, pr, threads)
-    mt_s = time.perf_counter() - t
+
+    def procs_leg(p):
+        ms_ = O.OSet(m0_values)
+        t_ = time.perf_counter()
+        _, used_ = O.triage_procs(ms_, None, v, o, pr, p)
+        return time.perf_counter() - t_, used_
+
+    mt_s, used = procs_leg(threads)
+    legs_n = procs_leg(threads_nproc) if threads_nproc and threads_nproc != threads else None
     model, ncpu, avail = cpu_info()
+    structure = ("procs taking whole programs, maps under one pthread rwlock with the RLock->Lock upgrade of "
+                 "fuzzer.go:671-676 (racy, as the reference)")
     sample = (f"first {done_prog} programs ({done_prog * calls} call records, {nel} signal entries) of the first "
               f"timed batch vs the same {len(m0_values)}-entry maxSignal; C restatement of the Go reference "
               f"(oracle/sigoracle.c, Go maps mirrored by open-addressing hash sets), not Go; set build "
@@ -285,9 +308,12 @@ def cpu_baseline(m0_values, batch, calls, gpu_flags, budget_s, threads):
         "prefix_parity_vs_gpu": parity,
         "prefix_queued_frac": queued_frac,
         "all_cores": {"value": nel / mt_s if mt_s else None, "unit": "PCs/s", "cores": used,
-                      "structure": "procs taking whole programs, maps under one pthread rwlock with the "
-                                   "RLock->Lock upgrade of fuzzer.go:671-676 (racy, as the reference)"},
-        "host": {"cpu_model": model, "nproc": ncpu, "cpus_available": avail},
+                      "threads_used": used, "structure": structure},
+        "all_cores_nproc": ({"value": nel / legs_n[0] if legs_n[0] else None, "unit": "PCs/s", "cores": legs_n[1],
+                             "threads_used": legs_n[1], "structure": structure,
+                             "note": "P = nproc threads; the cgroup CPU quota (host.cpu_quota) bounds how many run "
+                                     "at once"} if legs_n else None),
+        "host": {"cpu_model": model, "nproc": ncpu, "cpus_available": avail, "cpu_quota": cpu_quota()},
     }
 
 
@@ -323,7 +349,7 @@ def account(ctx, maxsig, m0set, newsig, batches, calls, rec_new, diff_vals, diff
     return per
 
 
-def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world):
+def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world, tag=1):
     """K steps, each triaging its batch against its own copy of the starting
     maxSignal (made before the timed region: the state reset is not part of
     the reference's step, fuzzer.go:645-693).  maxsig ends as step 0's copy
@@ -336,13 +362,13 @@ def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world):
         dist.barrier()
     torch.cuda.synchronize()
     ctx.timing(True)
-    call("sg_ctx_marker", ctx.h, 0, 1)  # the timed region, for kernel traces (scripts/trace_summary.py)
+    call("sg_ctx_marker", ctx.h, 0, tag)  # the timed region, for kernel traces (scripts/trace_summary.py, pmc_summary.py)
     t0 = time.perf_counter()
     for st, b in zip(states, batches):
         tm.mark()
         triage(ctx, st, newsig, b, rec_new)
         tm.mark()
-    call("sg_ctx_marker", ctx.h, 1, 1)
+    call("sg_ctx_marker", ctx.h, 1, tag)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -362,17 +388,17 @@ def kernel_table(ctx, names, steps):
     return out
 
 
-def roofline(acct, step_ms, kernels):
+def roofline(acct, step_ms, kernels, workload="c2"):
     b = step_bytes(acct)
     ach = b / (step_ms / 1e3) / 1e9
-    traffic, tag = pmc_bytes_per_step(STEP_KERNELS)
+    traffic, tag = pmc_bytes_per_step(STEP_KERNELS, workload)
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "scope": "whole triage step (all its kernels, HIP events on the launch stream)",
             "algo_bytes_per_step": b, "step_ms_events": step_ms,
             "formula": "4N_in + 4N_uniq + 8N_cand + 4N_cand + 4N_out + N_rec/8 (SURVEY.md §8(d), N_uniq measured)",
-            "traffic_source": f"profiles/pmc_traffic.json ({tag}): FETCH_SIZE/WRITE_SIZE summed over the step's "
-                              f"kernels" if traffic is not None else None,
+            "traffic_source": f"profiles/pmc_traffic.json ({tag}): FETCH_SIZE/WRITE_SIZE of this workload's timed "
+                              f"launches, summed over the step's kernels" if traffic is not None else None,
             "traffic_over_algo": round(traffic / b, 3) if traffic else None}
 
 
@@ -413,7 +439,8 @@ def run_c2(ctx, args, cfg, rank):
         del diff_vals, diff_off
     if not args.no_cpu:
         m0_values = m0set.export()
-        res["cpu"] = cpu_baseline(m0_values, timed[0], calls, gpu_flags0, args.cpu_budget, args.cpu_threads)
+        res["cpu"] = cpu_baseline(m0_values, timed[0], calls, gpu_flags0, args.cpu_budget, args.cpu_threads,
+                                  os.cpu_count())
     del batches, timed
     torch.cuda.empty_cache()
     if args.from_traces:
@@ -425,11 +452,14 @@ def run_c2(ctx, args, cfg, rank):
 
 
 def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
-    """End to end from executor traces: each timed step runs the executor-exact
-    signal kernels (A0, executor.h:389-401 + :497-526) over the batch's raw PC
-    traces, resident in HBM, and triages the signal it produced (C2's seeds,
-    so the triage work is the timed C2 batches')."""
-    calls = cfg["calls"]
+    """End to end from executor traces (C2's seeds, so the triage work is the
+    timed C2 batches'): each timed step triages the batch's raw PC traces,
+    resident in HBM, with sg_triage_traces_dev -- the set-exact front stage
+    (edge signal computed in the partition's loads, executor.h:389-401) whose
+    flags and set updates equal the executor-exact signal's (include/syzsig.h,
+    tests/test_traces.py).  For comparison, the same steps through the
+    executor-exact kernels (A0, executor.h:389-401 + :497-526) and then the
+    triage of the signal they produce ("executor_exact")."""
     traces, offs = [], []
     for k in range(steps):
         call("sg_gen_zipf_traces_dev", ctx.h, UNIVERSE_SEED, 1_000 + args.warmup + k, cfg["zipf_s"], cfg["ranks"], 0,
@@ -444,7 +474,14 @@ def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
         e.record()
         ev.append(e)
 
-    def step(tr, so):
+    def step_set_exact(tr):
+        call("sg_set_copy", maxsig.h, m0set.h)
+        mark()
+        call("sg_triage_traces_dev", ctx.h, maxsig.h, newsig.h, tr.data_ptr(), g.call_off.data_ptr(), g.npcs,
+             g.ncalls, rec_new.data_ptr())
+        mark()
+
+    def step_exact(tr, so):
         call("sg_set_copy", maxsig.h, m0set.h)
         mark()
         call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
@@ -456,27 +493,44 @@ def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
         mark()
         return n
 
-    step(traces[0], offs[0])  # warm-up
+    # set-exact (the product's trace path)
+    step_set_exact(traces[0])  # warm-up
     torch.cuda.synchronize()
     ev.clear()
     ctx.timing(True)
     torch.cuda.synchronize()
+    call("sg_ctx_marker", ctx.h, 0, 3)
     t0 = time.perf_counter()
-    units = sum(step(tr, so) for tr, so in zip(traces, offs))
+    for tr in traces:
+        step_set_exact(tr)
+    call("sg_ctx_marker", ctx.h, 1, 3)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kernels = kernel_table(ctx, ["exec_signal", "exec_compact"] + STEP_KERNELS, steps)
+    kernels = kernel_table(ctx, STEP_KERNELS, steps)
     ctx.timing(False)
+    tri = [ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 2)]
+    # executor-exact, for comparison
+    ev.clear()
+    step_exact(traces[0], offs[0])
+    torch.cuda.synchronize()
+    ev.clear()
+    t1 = time.perf_counter()
+    units = sum(step_exact(tr, so) for tr, so in zip(traces, offs))
+    torch.cuda.synchronize()
+    wall_x = time.perf_counter() - t1
     ex = [ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 3)]
-    tri = [ev[i + 1].elapsed_time(ev[i + 2]) for i in range(0, len(ev), 3)]
+    tx = [ev[i + 1].elapsed_time(ev[i + 2]) for i in range(0, len(ev), 3)]
     del traces, offs
     torch.cuda.empty_cache()
-    return {"workload": "C2 from traces: the timed step is executor signal (exec_signal + exec_compact over "
-                        f"{g.npcs} resident raw PCs) + triage of the {units / steps:.0f} signal entries it yields, "
-                        "maxSignal restored before every step",
-            "value": g.npcs * steps / wall, "unit": "raw PCs/s", "signal_per_s": units / wall,
-            "ms_per_step": wall * 1e3 / steps, "steps": steps, "exec_ms_events": float(np.mean(ex)),
-            "triage_ms_events": float(np.mean(tri)), "kernels": kernels}
+    return {"workload": "C2 from traces: the timed step triages the batch's "
+                        f"{g.npcs} resident raw PCs (sg_triage_traces_dev, set-exact edge signal in the partition's "
+                        "loads), maxSignal restored before every step",
+            "value": g.npcs * steps / wall, "unit": "raw PCs/s", "ms_per_step": wall * 1e3 / steps, "steps": steps,
+            "triage_ms_events": float(np.mean(tri)), "kernels": kernels,
+            "executor_exact": {"value": g.npcs * steps / wall_x, "unit": "raw PCs/s",
+                               "ms_per_step": wall_x * 1e3 / steps, "signal_per_step": units / steps,
+                               "exec_ms_events": float(np.mean(ex)), "triage_ms_events": float(np.mean(tx)),
+                               "path": "sg_exec_signal_dev (executor-exact per-call lists) + sg_triage_batch_dev"}}
 
 
 def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
@@ -501,7 +555,7 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
         call("sg_set_copy", maxsig.h, m0set.h)
         triage(ctx, maxsig, newsig, b, rec_new)
     timed = batches[args.warmup:]
-    wall, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1)
+    wall, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1, tag=2)
     kernels = kernel_table(ctx, STEP_KERNELS, args.steps)
     ctx.timing(False)
     units = sum(b.nvals for b in timed)
@@ -517,7 +571,7 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
         diff_off = torch.empty(maxnrec + 1, dtype=torch.int64, device="cuda")
         acct = account(ctx, maxsig, m0set, newsig, timed, calls, rec_new, diff_vals, diff_off)
         out["accounting"] = acct
-        out["roofline"] = roofline(acct, float(np.mean(tri)), kernels)
+        out["roofline"] = roofline(acct, float(np.mean(tri)), kernels, "steady")
         del diff_vals, diff_off
     if not args.no_cpu:
         call("sg_set_copy", maxsig.h, m0set.h)
@@ -548,7 +602,8 @@ def main():
     ap.add_argument("--c3-two-phase", action="store_true",
                     help="measurement: the prefix protocol's two-phase path at one rank too")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of single-thread CPU baseline work")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-cores CPU leg")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the CPU-share leg (a second leg always runs nproc threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-account", action="store_true", help="skip the byte-accounting replay")
     args = ap.parse_args()

@@ -137,6 +137,24 @@ int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint3
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec, uint8_t* d_rec_new,
 			uint32_t* d_diff_vals, uint64_t* d_diff_off);
 
+/* The same triage fed with raw per-call u32 PC traces (the executor's KCOV
+ * buffers, executor/executor_linux.cc:262-313) instead of signal: record r =
+ * call r, its trace pcs[call_off[r] .. call_off[r+1]) (call_off[0] == 0),
+ * its edges sig = pc ^ hash(previous pc of the call), pc ^ 0 for the call's
+ * first pc (executor/executor.h:389-401, hash :497-505), zero edges dropped
+ * (dedup(0) reports seen, :507-526).  rec_new and the maxSignal / newSignal
+ * updates are exactly those of sg_exec_signal_dev followed by a flags-only
+ * sg_triage_batch_dev on its output: the executor writes every non-zero edge
+ * at its first occurrence in the program, so the first call holding each
+ * edge and the batch's union of edges -- all that decides the flags and the
+ * sets (fuzzer.go:665-691) -- do not depend on the edges its lossy dedup
+ * table drops or lets through again (set-exact mode).
+ * Calls need not be grouped into programs.  Limits as sg_triage_batch_dev. */
+int sg_triage_traces(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* pcs, const uint64_t* call_off,
+		     size_t ncalls, uint8_t* rec_new);
+int sg_triage_traces_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_pcs,
+			 const uint64_t* d_call_off, uint64_t npcs, uint64_t ncalls, uint8_t* d_rec_new);
+
 /* ---- one batch hash-sharded by signal across GPUs ------ */
 /* The sequential loop of sg_triage_batch (syz-fuzzer/fuzzer.go:645-693) over a
  * batch whose call records are split contiguously across G ranks, one GPU each

@@ -58,6 +58,8 @@ SIGNATURES = {
     "sg_triage_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64, P64]),
     "sg_triage_batch_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
                                     c_void_p, c_void_p, c_void_p]),
+    "sg_triage_traces": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t, P8]),
+    "sg_triage_traces_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p]),
     "sg_shard_of": (c_int, [c_uint32, c_uint32]),
     "sg_shard_candidates_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
                                         c_uint32, c_void_p, c_void_p]),

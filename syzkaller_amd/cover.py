@@ -275,6 +275,18 @@ def triage_batch(maxset, newset, vals, rec_off, want_diff=True, ctx=None):
     return rec_new, None, None
 
 
+def triage_traces(maxset, newset, pcs, call_off, ctx=None):
+    """fuzzer.go:645-693 over a batch given as raw per-call PC traces (set-exact
+    edge signal, executor.h:389-401): the per-call flags, sets updated."""
+    p, off = _u32(pcs), _u64(call_off)
+    ncalls = off.size - 1
+    rec_new = np.zeros(ncalls, dtype=np.uint8)
+    c = maxset.ctx if ctx is None else ctx
+    call("sg_triage_traces", c.h, maxset.h, newset.h if newset is not None else None, _p32(p), _p64(off), ncalls,
+         _p8(rec_new))
+    return rec_new
+
+
 def add_inputs(corpus, maxset, vals, off, ctx=None):
     """syz-fuzzer/fuzzer.go:467-489 addInput over a batch of inputs."""
     vals, off = _u32(vals), _u64(off)

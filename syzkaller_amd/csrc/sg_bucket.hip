@@ -174,14 +174,15 @@ __global__ void k_group_chunks(const uint32_t* __restrict__ goff1, uint32_t T, u
 
 // cbase = exclusive scan of nch (cbase[ng] = number of chunks G).  Writes the
 // chunk list (start, slice-group) for c < G, start = n for G <= c <= gmax (the
-// launch grids use gmax, an upper bound known on the host), and cfirst[d] =
-// first chunk of slice d (cfirst[256] = G).
+// launch grids use gmax, an upper bound known on the host; n = the pass-1
+// total, goff1[256 T], which is below the input count when a trace batch
+// drops zero edges), and cfirst[d] = first chunk of slice d (cfirst[256] = G).
 __global__ void k_chunk_list(const uint32_t* __restrict__ goff1, uint32_t T, uint32_t NG,
-                             const uint32_t* __restrict__ gt, uint64_t ng, uint32_t n,
+                             const uint32_t* __restrict__ gt, uint64_t ng,
                              const uint32_t* __restrict__ cbase, uint64_t gmax, uint32_t* __restrict__ cstart,
                              uint32_t* __restrict__ cgov, uint32_t* __restrict__ cfirst) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t G = cbase[ng];
+  const uint32_t G = cbase[ng], n = goff1[256ull * T];
   if (i < ng) {
     const uint32_t g0 = group_start(goff1, T, NG, gt, i), g1 = group_start(goff1, T, NG, gt, i + 1);
     uint32_t c = cbase[i];
@@ -408,6 +409,109 @@ __global__ __launch_bounds__(kHBThreads) void k_hist_bytes(const uint8_t* __rest
   }
 }
 
+// ------------------------------------------------ trace batches (set-exact) ---
+// A batch given as raw per-call PC traces (the executor's KCOV buffers) is
+// triaged with its edge signal computed in the pass-1 loads: entry e of a
+// call is sig = pc[e] ^ hash(pc[e - 1]), pc[e] ^ 0 for the call's first PC
+// (executor/executor.h:392-396), and a zero sig is not an entry (the
+// executor's dedup reports 0 as seen, executor.h:507-515).  The executor
+// also drops an edge its dedup table still holds; skipping that is exact for
+// the triage: every non-zero edge is written at its first occurrence in the
+// program (dedup returns false when no slot holds it, executor.h:516-525),
+// i.e. in its first call, so the first record holding s and the union of the
+// batch's signal -- all that decides the queued records and the set updates
+// (fuzzer.go:665-691) -- are the same with or without the repeats.  The
+// partition and the buckets are the sort and unique stage.
+//
+// Repeats inside a pass-1 tile (a hot edge recurs hundreds of times in one
+// program's trace; the executor's table drops most of those) are dropped
+// before the partition: each edge takes a 64-bit atomicMin of
+// (tile position << 32 | sig) on an LDS slot hashed from sig, and an edge
+// whose slot ends up holding the same sig at an earlier position is a
+// repeat.  Exact: the earlier copy's record is not larger, so the first
+// record holding sig and the union are unchanged; a slot taken by another
+// edge only leaves a repeat in.  The histogram and the scatter drop the
+// same entries (same positions, same hash).
+constexpr uint32_t kTraceDedup = 1024;  // slots (8 KiB of LDS)
+__device__ __forceinline__ uint32_t dedup_slot(uint32_t sig) { return (sig * 0x9E3779B1u) >> 22; }
+
+// Call starts inside a pass-1 tile: its <= kRecCap + 1 record offsets as an
+// LDS bitmap over the tile's positions.
+__device__ __forceinline__ void trace_starts(const uint64_t* __restrict__ rec_off, uint64_t nrec, uint32_t r0,
+                                             uint32_t s0, uint32_t s1, uint32_t* cs, int tid) {
+  const uint32_t wn = (uint32_t)(nrec + 1 - r0 < kRecCap + 1 ? nrec + 1 - r0 : kRecCap + 1);
+  for (uint32_t i = tid; i < wn; i += kPThreads) {
+    const uint64_t o = rec_off[r0 + i];
+    if (o >= s0 && o < s1) atomicOr(&cs[(o - s0) >> 5], 1u << ((o - s0) & 31));
+  }
+}
+
+// the previous PC of position e for lane-strided loads (x = this lane's PC,
+// xp = pcs[e - 1] loaded by lane 0 of the wave)
+__device__ __forceinline__ uint32_t trace_prev(uint32_t x, uint32_t xp) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)xp, (int)x, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t trace_sig(uint32_t pc, uint32_t prev, bool start) {
+  return pc ^ (start ? 0u : sgd::exec_hash(prev));
+}
+
+// Pass-1 histogram of a trace batch: b2 counts of the tile's non-zero edges.
+__global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __restrict__ pcs,
+                                                          const uint64_t* __restrict__ rec_off, uint64_t nrec,
+                                                          const uint32_t* __restrict__ tstart,
+                                                          const uint32_t* __restrict__ trec, uint32_t T,
+                                                          uint32_t* __restrict__ hist) {
+  __shared__ uint32_t rc[256 * 32];
+  __shared__ uint32_t cs[kPT / 32];
+  __shared__ unsigned long long dd[kTraceDedup];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t t = xcd_tile(blockIdx.x, T), s0 = tstart[t], s1 = tstart[t + 1];
+  constexpr int kS = kPT / kPThreads;
+  uint32_t x[kS], xp[kS];
+#pragma unroll
+  for (int k = 0; k < kS; k++) {
+    const uint32_t e = s0 + k * kPThreads + tid;
+    x[k] = e < s1 ? pcs[e] : 0u;
+    xp[k] = lane == 0 && e < s1 && e > 0 ? pcs[e - 1] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 256 * 32 / 4 / kPThreads; k++)
+    reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < kPT / 32; i += kPThreads) cs[i] = 0;
+  for (int i = tid; i < (int)kTraceDedup; i += kPThreads) dd[i] = ~0ull;
+  __syncthreads();
+  trace_starts(rec_off, nrec, trec[t], s0, s1, cs, tid);
+  __syncthreads();
+  uint32_t live = 0;
+#pragma unroll
+  for (int k = 0; k < kS; k++) {
+    const uint32_t p = k * kPThreads + tid, e = s0 + p;
+    x[k] = trace_sig(x[k], trace_prev(x[k], xp[k]), (cs[p >> 5] >> (p & 31)) & 1u);
+    if (e < s1 && x[k] != 0) {
+      live |= 1u << k;
+      atomicMin(&dd[dedup_slot(x[k])], ((unsigned long long)p << 32) | x[k]);
+    }
+  }
+  __syncthreads();
+  const uint32_t cp = tid & 31;
+#pragma unroll
+  for (int k = 0; k < kS; k++) {
+    const uint32_t p = k * kPThreads + tid;
+    if ((live >> k) & 1u) {
+      const unsigned long long v = dd[dedup_slot(x[k])];
+      if ((uint32_t)v != x[k] || (uint32_t)(v >> 32) == p) atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) sum += rc[tid * 32 + ((k + tid) & 31)];
+    hist[(uint64_t)tid * T + t] = sum;
+  }
+}
+
 // Counting sort of one tile held in registers (kSteps entries per lane) by an
 // 8-bit digit, through LDS: counts, a one-wave exclusive scan, then every
 // entry takes a slot with an LDS atomic (order within a digit is arbitrary).
@@ -540,9 +644,12 @@ struct P1Args {
 // values (1.85 -> 1.67 ms per C2 launch against keeping digits and keys in
 // registers; an unpredicated path for full tiles, as pass 2 has, was slower
 // here: 1.93 ms).
-template <bool kDbg>
+// kTrace: a.vals are raw per-call PC traces, each entry's signal computed here
+// (see k_hist_trace) and zero edges skipped.
+template <bool kDbg, bool kTrace>
 __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32_t* cnt, uint32_t* gbase,
-                                        uint16_t* win, SegLds<uint8_t>& L, uint32_t t, uint32_t s0, uint32_t s1) {
+                                        uint16_t* win, SegLds<uint8_t>& L, unsigned long long* dd, uint32_t t,
+                                        uint32_t s0, uint32_t s1) {
   uint8_t* sidx = reinterpret_cast<uint8_t*>(stage);  // record-in-tile index; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   uint64_t tk = kDbg ? clock64() : 0;
@@ -566,6 +673,10 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
     sv[k] = ok ? a.vals[e] : 0u;
     vmask |= (ok ? 1u : 0u) << k;
   }
+  // trace batches: the PC before the wave's first position (lane 0; the rest
+  // come from the wave itself)
+  const uint32_t xp0 = kTrace && lane == 0 && ebase < s1 && ebase > 0 ? a.vals[ebase - 1] : 0u;
+  const bool start0 = kTrace && a.rec_off[r0] == s0;  // does a call start at the tile's first position
   for (uint32_t i = tid; i < wn; i += kPThreads) {
     const uint64_t o = a.rec_off[r0 + i];
     win[i] = (uint16_t)(o <= s0 ? 0 : (o - s0 >= (uint64_t)kPT ? kPT : o - s0));
@@ -575,6 +686,8 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
     cnt[d] = a.hist1[(uint64_t)d * a.T + t];
   }
   seg_clear(L, tid);
+  if (kTrace)
+    for (int i = tid; i < (int)kTraceDedup; i += kPThreads) dd[i] = ~0ull;
   __syncthreads();
   stamp(0);
   const uint32_t nt = s1 - s0;
@@ -582,6 +695,31 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
       L, sidx, [&](uint32_t k) { return (uint32_t)win[k]; }, [](uint32_t k) { return k; }, wn, nt, tid);
   uint32_t rp[kSteps / 4] = {};
   const uint32_t el0 = ebase + lane - s0;
+  if (kTrace) {
+    // entries -> edge signals: the previous PC is the lane before's (lane 0:
+    // the previous step's lane 63, or xp0); a call start is a segment start
+    // (seg_build marks every non-empty record starting inside the tile)
+    uint32_t carry = xp0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint32_t p = el0 + k * 64, pc = sv[k];
+      const bool start = p ? ((L.sbits[p >> 5] >> (p & 31)) & 1u) != 0 : start0;
+      const uint32_t prev = trace_prev(pc, carry);
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)pc, 63);
+      sv[k] = trace_sig(pc, prev, start);
+      if (sv[k] == 0) vmask &= ~(1u << k);
+      if ((vmask >> k) & 1u) atomicMin(&dd[dedup_slot(sv[k])], ((unsigned long long)p << 32) | sv[k]);
+      asm volatile("" : "+v"(sv[k]));  // one step at a time (registers)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSteps; k++)
+      if ((vmask >> k) & 1u) {  // a repeat of an earlier position of the tile
+        const uint32_t p = el0 + k * 64;
+        const unsigned long long v = dd[dedup_slot(sv[k])];
+        if ((uint32_t)v == sv[k] && (uint32_t)(v >> 32) != p) vmask &= ~(1u << k);
+      }
+  }
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t r = ((vmask >> k) & 1u) ? seg_lookup(L, sidx, el0 + k * 64) : 0u;  // record in tile
@@ -601,17 +739,18 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
   if (kDbg && tid == 0) atomicAdd(&a.dbg[5], 1ull);
 }
 
-template <bool kDbg>
+template <bool kDbg, bool kTrace>
 __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_p1_scatter(P1Args a) {
   __shared__ uint32_t stage[kPT];
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
   __shared__ SegLds<uint8_t> L;
+  __shared__ unsigned long long dd[kTrace ? kTraceDedup : 1];
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
   if (s0 >= s1) return;
-  p1_tile<kDbg>(a, stage, cnt, gbase, win, L, t, s0, s1);
+  p1_tile<kDbg, kTrace>(a, stage, cnt, gbase, win, L, dd, t, s0, s1);
 }
 
 // ---------------------------------------------------------------- pass 2 ---
@@ -1582,7 +1721,7 @@ static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
 // bucket descriptors and the list of non-empty buckets, in the workspace from
 // ws_base (reserved by the caller when `reserved`).  n > 0, nrec > 0.
 static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n, uint64_t nrec,
-                         size_t ws_base, bool reserved, BucketPlan& bp) {
+                         size_t ws_base, bool reserved, BucketPlan& bp, bool trace = false) {
   if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
     set_error("bucket triage: batch too large");
     return SG_EINVAL;
@@ -1632,7 +1771,10 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
                      gt);
   {
     ScopedTimer tm(ctx, "p1_hist");
-    if (((uintptr_t)d_vals & 15) == 0)
+    if (trace)
+      hipLaunchKernelGGL(k_hist_trace, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals, d_off, nrec,
+                         (const uint32_t*)tstart, (const uint32_t*)trec, T, hist1);
+    else if (((uintptr_t)d_vals & 15) == 0)
       hipLaunchKernelGGL(k_hist_rep<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
                          (const uint32_t*)tstart, (const uint4*)nullptr, T, (const uint32_t*)nullptr, hist1);
     else
@@ -1651,10 +1793,14 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   }
   {
     ScopedTimer tm(ctx, "p1_scatter");
-    if (dbg)
-      hipLaunchKernelGGL(k_p1_scatter<true>, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+    if (dbg && trace)
+      hipLaunchKernelGGL((k_p1_scatter<true, true>), dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+    else if (dbg)
+      hipLaunchKernelGGL((k_p1_scatter<true, false>), dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+    else if (trace)
+      hipLaunchKernelGGL((k_p1_scatter<false, true>), dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
     else
-      hipLaunchKernelGGL(k_p1_scatter<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
+      hipLaunchKernelGGL((k_p1_scatter<false, false>), dim3(T), dim3(kPThreads), 0, ctx->stream, a1);
   }
   if (dbg) {
     unsigned long long h[8];
@@ -1670,7 +1816,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   rc = scan32(ctx, nch, cbase, bp.ng, scr);
   if (rc) return rc;
   hipLaunchKernelGGL(k_chunk_list, dim3(div_up((bp.ng > bp.gmax ? bp.ng : bp.gmax) + 1, 256)), dim3(256), 0,
-                     ctx->stream, (const uint32_t*)goff1, T, NG, (const uint32_t*)gt, bp.ng, (uint32_t)n,
+                     ctx->stream, (const uint32_t*)goff1, T, NG, (const uint32_t*)gt, bp.ng,
                      (const uint32_t*)cbase, bp.gmax, cstart, cgov, cfirst);
   hipLaunchKernelGGL(k_chunk_desc, dim3(div_up(bp.gmax, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)cstart,
                      (const uint32_t*)cgov, gcount, bp.gmax, (const uint32_t*)goff1, T, NG, (const uint32_t*)gt,
@@ -1821,14 +1967,14 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
 // when ws_base != 0).
 static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
                              const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new,
-                             const EmitArgs* emit = nullptr, size_t ws_base = 0) {
+                             const EmitArgs* emit = nullptr, size_t ws_base = 0, bool trace = false) {
   if (n == 0) return SG_OK;
   if (nrec == 0) {
     set_error("bucket triage: signal entries without records");
     return SG_EINVAL;
   }
   BucketPlan bp(n, nrec);
-  int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp);
+  int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp, trace);
   if (rc) return rc;
   return buckets_one(ctx, bp, mwords, nwords, d_rec_new, emit, n, nrec);
 }
@@ -1912,14 +2058,15 @@ static int read_off(sg_ctx* ctx, const uint64_t* d_off, uint64_t r, uint64_t* v)
 constexpr uint64_t kSliceEntries = 1ull << 30;
 
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
-                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new) {
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new, bool trace) {
   if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
     set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
     return SG_EINVAL;
   }
   if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
   const uint64_t m = ctx->max_launch_recs;
-  if (nrec <= m && n <= kSliceEntries) return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new);
+  if (nrec <= m && n <= kSliceEntries)
+    return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new, nullptr, 0, trace);
   if (ctx->slice_off_cap < m + 1) {
     SG_HIP(hipStreamSynchronize(ctx->stream));
     if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
@@ -1957,7 +2104,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     }
     hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1, e0,
                        roff);
-    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e0, roff, e1 - e0, r1 - r0, d_rec_new + r0);
+    // (a slice starts at a record boundary: a trace slice's first entry is a call start)
+    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e0, roff, e1 - e0, r1 - r0, d_rec_new + r0, nullptr, 0, trace);
     if (rc) return rc;
     SG_HIP(hipStreamSynchronize(ctx->stream));  // the next slice's offsets overwrite roff
     r0 = r1;

@@ -30,14 +30,7 @@ namespace sg {
 
 constexpr uint32_t kDedupSize = 8192;  // executor.h:506
 
-__device__ __forceinline__ uint32_t exec_hash(uint32_t a) {  // executor.h:497-505
-  a = (a ^ 61) ^ (a >> 16);
-  a = a + (a << 3);
-  a = a ^ (a >> 4);
-  a = a * 0x27d4eb2du;
-  a = a ^ (a >> 15);
-  return a;
-}
+using sgd::exec_hash;  // executor.h:497-505
 
 // The speculative pass, per edge j of the window (positions start..nvalid-1
 // of up to 128 edges: lane l holds positions l and 64 + l), all deciding

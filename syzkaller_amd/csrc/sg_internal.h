@@ -184,9 +184,10 @@ struct OwnerJob {
 int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint64_t* d_cmask, uint64_t* d_dmask,
                         uint32_t* d_tile_rec, uint8_t* d_seg_flag, uint32_t* set_a, uint32_t* set_b);
 
-// Partitioned flags-only triage (sg_bucket.hip); ctx lock held.
+// Partitioned flags-only triage (sg_bucket.hip); ctx lock held.  trace:
+// d_vals are raw per-call PC traces, triaged by their edge signal.
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
-                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new);
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new, bool trace = false);
 // Candidate emission of the partitioned path (sharded triage, sg_shard.hip):
 // each distinct s not in the snapshot, once per launch, as {s, rec_base +
 // first record}, counted per owning shard.
@@ -234,6 +235,18 @@ __host__ __device__ __forceinline__ uint32_t set_sig(uint32_t p) {  // inverse o
 __host__ __device__ __forceinline__ uint32_t set_word(uint32_t ws) {
   return (((ws >> 3) & 0xFFFFu) << 11) | ((ws >> 19) << 3) | (ws & 7u);
 }
+// The executor's edge hash (executor/executor.h:497-505): an edge's signal
+// is pc ^ hash(previous pc of the call), 0 before the call's first pc
+// (executor.h:392-396).
+__host__ __device__ __forceinline__ uint32_t exec_hash(uint32_t a) {
+  a = (a ^ 61) ^ (a >> 16);
+  a = a + (a << 3);
+  a = a ^ (a >> 4);
+  a = a * 0x27d4eb2du;
+  a = a ^ (a >> 15);
+  return a;
+}
+
 __device__ __forceinline__ bool test_bit(const uint32_t* words, uint32_t s) {
   return (words[set_pos(s) >> 5] >> (s & 31)) & 1u;
 }

@@ -525,6 +525,63 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
   return SG_OK;
 }
 
+int sg_triage_traces_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* d_pcs,
+                         const uint64_t* d_call_off, uint64_t npcs, uint64_t ncalls, uint8_t* d_rec_new) {
+  if (!ctx || !maxsig || !d_call_off || (ncalls && !d_rec_new) || (npcs && !d_pcs)) {
+    set_error("sg_triage_traces_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  if (maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {
+    set_error("sg_triage_traces_dev: set belongs to another context");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = check_alloc(ctx);
+  if (rc) return rc;
+  return bucket_triage(ctx, maxsig->words, newsig ? newsig->words : nullptr, d_pcs, d_call_off, npcs, ncalls,
+                       d_rec_new, true);
+}
+
+int sg_triage_traces(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* pcs, const uint64_t* call_off,
+                     size_t ncalls, uint8_t* rec_new) {
+  if (!ctx || !maxsig || !call_off || (ncalls && !rec_new)) {
+    set_error("sg_triage_traces: invalid argument");
+    return SG_EINVAL;
+  }
+  if (call_off[0] != 0) {
+    set_error("sg_triage_traces: call_off[0] must be 0");
+    return SG_EINVAL;
+  }
+  for (size_t r = 0; r < ncalls; r++)
+    if (call_off[r + 1] < call_off[r]) {
+      set_error("sg_triage_traces: call_off not non-decreasing at %zu", r);
+      return SG_EINVAL;
+    }
+  const uint64_t npcs = call_off[ncalls];
+  if (npcs && !pcs) return SG_EINVAL;
+  const size_t b_pcs = (npcs * 4 + 255) & ~size_t(255), b_off = ((ncalls + 1) * 8 + 255) & ~size_t(255),
+               b_flag = (ncalls + 256) & ~size_t(255);
+  char* stage = nullptr;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int rc = check_alloc(ctx);
+    if (rc) return rc;
+    rc = dstage_reserve(ctx, b_pcs + b_off + b_flag + 256);
+    if (rc) return rc;
+    stage = (char*)ctx->dstage;
+  }
+  uint32_t* dp = (uint32_t*)stage;
+  uint64_t* doff = (uint64_t*)(stage + b_pcs);
+  uint8_t* dflag = (uint8_t*)(stage + b_pcs + b_off);
+  if (npcs) SG_HIP(hipMemcpyAsync(dp, pcs, npcs * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(doff, call_off, (ncalls + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  int rc = sg_triage_traces_dev(ctx, maxsig, newsig, dp, doff, npcs, ncalls, dflag);
+  if (rc) return rc;
+  if (ncalls) SG_HIP(hipMemcpyAsync(rec_new, dflag, ncalls, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
 int sg_set_diff(sg_set* set, const uint32_t* sig, size_t n, uint32_t* out, size_t* nout) {
   if (!set || !nout || (n && (!sig || !out))) return SG_EINVAL;
   *nout = 0;
