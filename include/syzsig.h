@@ -109,6 +109,11 @@ void* sg_set_device_words(sg_set* set);
 int sg_set_wrap_dev(sg_ctx* ctx, void* d_words, sg_set** out);
 /* set |= words (device pointer to 2^27 uint32 words). */
 int sg_set_or_dev(sg_set* set, const uint32_t* d_words);
+/* set |= words & ~exclude (device pointer to 2^27 uint32 words; exclude a set
+ * of the same context): the new signal of a batch whose total was computed
+ * against an older maxSignal (fuzzer.go:674 adds to newSignal only what
+ * maxSignal lacks). */
+int sg_set_or_new_dev(sg_set* set, const uint32_t* d_words, sg_set* exclude);
 /* dst = src (both sets of the same context). */
 int sg_set_copy(sg_set* dst, sg_set* src);
 /* *out = number of the n device-resident values not in set (duplicates

@@ -54,6 +54,7 @@ SIGNATURES = {
     "sg_set_wrap_dev": (c_int, [c_void_p, c_void_p, POINTER(c_void_p)]),
     "sg_set_or_dev": (c_int, [c_void_p, c_void_p]),
     "sg_set_copy": (c_int, [c_void_p, c_void_p]),
+    "sg_set_or_new_dev": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sg_set_count_missing_dev": (c_int, [c_void_p, c_void_p, c_uint64, P64]),
     "sg_triage_batch": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t, P8, P32, P64, P64]),
     "sg_triage_batch_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,

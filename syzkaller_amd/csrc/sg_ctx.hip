@@ -32,10 +32,18 @@ int hip_fail(hipError_t e, const char* what) {
 int ensure_device(sg_ctx* ctx) {
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  // hipGetLastError after our launches must see only our errors: drop one
-  // left on this thread by another library (seen: torch's "invalid device
-  // ordinal" after spawning multiprocess workers)
-  (void)hipGetLastError();
+  // hipGetLastError after our launches must see only our errors.  The one
+  // known stale code left on this thread by another library (torch's
+  // "invalid device ordinal" after spawning multiprocess workers) is dropped
+  // silently; any other pending error belongs to the caller's own HIP work,
+  // so it is reported on stderr before it is cleared, not hidden.
+  const hipError_t stale = hipPeekAtLastError();
+  if (stale != hipSuccess) {
+    if (stale != hipErrorInvalidDevice)
+      fprintf(stderr, "libsyzsig: clearing a pending HIP error of the calling thread: %d (%s)\n", (int)stale,
+              hipGetErrorString(stale));
+    (void)hipGetLastError();
+  }
   return SG_OK;
 }
 
@@ -293,6 +301,21 @@ __global__ void k_set_or(uint32_t* __restrict__ words, const uint32_t* __restric
     a.y |= b.y;
     a.z |= b.z;
     a.w |= b.w;
+    reinterpret_cast<uint4*>(words)[i] = a;
+  }
+}
+
+// words |= other & ~exclude
+__global__ void k_set_or_new(uint32_t* __restrict__ words, const uint32_t* __restrict__ other,
+                             const uint32_t* __restrict__ exclude) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kSetWords / 4; i += stride) {
+    uint4 a = reinterpret_cast<uint4*>(words)[i];
+    const uint4 b = reinterpret_cast<const uint4*>(other)[i], x = reinterpret_cast<const uint4*>(exclude)[i];
+    a.x |= b.x & ~x.x;
+    a.y |= b.y & ~x.y;
+    a.z |= b.z & ~x.z;
+    a.w |= b.w & ~x.w;
     reinterpret_cast<uint4*>(words)[i] = a;
   }
 }
@@ -644,6 +667,17 @@ int sg_set_or_dev(sg_set* set, const uint32_t* d_words) {
   int rc = ensure_device(ctx);
   if (rc) return rc;
   hipLaunchKernelGGL(k_set_or, dim3(4096), dim3(256), 0, ctx->stream, set->words, d_words);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_set_or_new_dev(sg_set* set, const uint32_t* d_words, sg_set* exclude) {
+  if (!set || !d_words || !exclude || exclude->ctx != set->ctx) return SG_EINVAL;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_set_or_new, dim3(4096), dim3(256), 0, ctx->stream, set->words, d_words, exclude->words);
   SG_HIP(hipGetLastError());
   return SG_OK;
 }

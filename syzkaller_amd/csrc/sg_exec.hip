@@ -32,6 +32,10 @@ constexpr uint32_t kDedupSize = 8192;  // executor.h:506
 
 using sgd::exec_hash;  // executor.h:497-505
 
+__device__ __forceinline__ unsigned long long mark_load(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // The speculative pass, per edge j of the window (positions start..nvalid-1
 // of up to 128 edges: lane l holds positions l and 64 + l), all deciding
 // against the table as it stands:
@@ -185,10 +189,12 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #endif
             // (one wave: its LDS operations complete in issue order, so the
-            // reads below see every lane's atomicMin without a fence)
+            // reads below see every lane's atomicMin without a fence; they are
+            // relaxed atomic loads, not plain reads of locations other lanes
+            // update atomically, so the memory model allows no reordering)
             __builtin_amdgcn_wave_barrier();
-            const unsigned long long a0 = markA[d0 & (kMarkN - 1)], b0 = markB[d0 >> 4];
-            const unsigned long long a1 = markA[d1 & (kMarkN - 1)], b1 = markB[d1 >> 4];
+            const unsigned long long a0 = mark_load(&markA[d0 & (kMarkN - 1)]), b0 = mark_load(&markB[d0 >> 4]);
+            const unsigned long long a1 = mark_load(&markA[d1 & (kMarkN - 1)]), b1 = mark_load(&markB[d1 >> 4]);
 #if SG_EXEC_FENCE
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 #endif

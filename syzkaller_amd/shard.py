@@ -37,14 +37,19 @@ from ._lib import call, lib
 
 class Comm:
     """The collectives of the protocol over a torch.distributed group (or a
-    single rank when torch.distributed is not initialised)."""
+    single rank when torch.distributed is not initialised).
 
-    def __init__(self, group=None):
+    At one rank every exchange is a local copy, unless `collectives` is set:
+    then the group's collectives run anyway (a one-rank RCCL group executes the
+    same device-tensor, async and side-stream code as N ranks; tests)."""
+
+    def __init__(self, group=None, collectives=False):
         self.group = group
         self.on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         self.host = self.on and dist.get_backend(group) != "nccl"  # gloo: host-staged
+        self.local = self.world == 1 and not (collectives and self.on)  # exchanges are copies
 
     def _stage(self, t):
         return t.cpu() if self.host and t.is_cuda else t
@@ -53,7 +58,7 @@ class Comm:
         """[values of rank 0, values of rank 1, ...] for a short int64 list."""
         dev = "cpu" if (self.host or not torch.cuda.is_available()) else "cuda"
         t = torch.tensor(values, dtype=torch.int64, device=dev)
-        if self.world == 1:
+        if self.local:
             return [values]
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
@@ -61,7 +66,7 @@ class Comm:
 
     def exchange_counts(self, counts):
         """counts[k] goes to rank k; returns what every rank sent here."""
-        if self.world == 1:
+        if self.local:
             return list(counts)
         dev = "cpu" if self.host else "cuda"
         s = torch.tensor(counts, dtype=torch.int64, device=dev)
@@ -71,7 +76,7 @@ class Comm:
 
     def all_to_all(self, send, send_splits, recv_splits):
         """all_to_all_single with variable splits (element counts)."""
-        if self.world == 1:
+        if self.local:
             return send[: send_splits[0]]
         dev = send.device
         recv = torch.empty(sum(recv_splits), dtype=send.dtype, device="cpu" if self.host else dev)
@@ -81,7 +86,7 @@ class Comm:
     def all_to_all_equal(self, out, t):
         """Dense all_to_all_single: part k of t (equal parts) goes to rank k,
         out's part j comes from rank j."""
-        if self.world == 1:
+        if self.local:
             out.copy_(t)
             return out
         if self.host:
@@ -94,7 +99,7 @@ class Comm:
 
     def all_gather_equal(self, out, t):
         """out = the t of every rank, concatenated in rank order."""
-        if self.world == 1:
+        if self.local:
             out.copy_(t)
             return out
         if self.host:
@@ -107,7 +112,7 @@ class Comm:
 
     def start_all_to_all_equal(self, out, t):
         """all_to_all_equal left running on RCCL's stream (see start_all_gather_equal)."""
-        if self.world == 1 or self.host:
+        if self.local or self.host:
             self.all_to_all_equal(out, t)
             return _Done()
         return dist.all_to_all_single(out, t, group=self.group, async_op=True)
@@ -115,14 +120,14 @@ class Comm:
     def start_all_gather_equal(self, out, t):
         """all_gather_equal left running on RCCL's stream; wait() on the handle
         orders the current stream after it (under gloo: done on return)."""
-        if self.world == 1 or self.host:
+        if self.local or self.host:
             self.all_gather_equal(out, t)
             return _Done()
         return dist.all_gather_into_tensor(out, t, group=self.group, async_op=True)
 
     def all_gather_var(self, t, n):
         """The first n elements of t from every rank, concatenated."""
-        if self.world == 1:
+        if self.local:
             return t[:n]
         counts = [c[0] for c in self.all_gather_i64([n])]
         m = max(counts)
@@ -194,6 +199,10 @@ class HipStages:
 
     def or_words(self, sset, t):
         call("sg_set_or_dev", sset.h, ctypes.c_void_p(t.data_ptr()))
+
+    def or_new_words(self, sset, t, exclude):
+        """sset |= t & ~exclude."""
+        call("sg_set_or_new_dev", sset.h, ctypes.c_void_p(t.data_ptr()), exclude.h)
 
     def prefix_or(self, parts, nparts, words, prefix, total):
         call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
@@ -435,11 +444,16 @@ class PrefixTriage:
             if "side_done" in pend:
                 torch.cuda.current_stream().wait_event(pend["side_done"])
             pend["got_p"].wait()
+            pend["got_t"].wait()
+            # newSignal gains the batch's signal that maxSignal lacks now
+            # (fuzzer.go:674): T was computed against the maxSignal of start(),
+            # which an overlapped batch finished since may have grown, and
+            # newSignal may have been drained (the Poll, fuzzer.go:358-364) in
+            # between -- so T & ~maxSignal, before step 3 changes maxSignal
+            if newsig is not None:
+                st.or_new_words(newsig, b["T"], maxsig)
             st.prefix_end(maxsig, b["P"], None, pend["rec_new"], slot)
             # 4. the replicated state after the whole batch
-            pend["got_t"].wait()
             st.or_words(maxsig, b["T"])
-            if newsig is not None:
-                st.or_words(newsig, b["T"])
         self.last = pend["last"]
         return pend["nrec_total"]

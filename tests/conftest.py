@@ -14,6 +14,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: a larger case (tens of millions of entries)")
 
 
+HIP_ERROR_INVALID_DEVICE = 101  # hipErrorInvalidDevice
+
+
+@pytest.fixture(autouse=True)
+def _stale_hip_error(request):
+    """Before each GPU test: drop the "invalid device ordinal" error that tests
+    spawning worker processes leave pending on this process's main thread
+    (torch's allocator would report it at the next test's first allocation).
+    Any other pending error is left in place, to fail where it shows."""
+    if request.node.get_closest_marker("gpu"):
+        import ctypes
+
+        try:
+            hip = ctypes.CDLL("libamdhip64.so")
+        except OSError:
+            hip = None
+        if hip is not None and hip.hipPeekAtLastError() == HIP_ERROR_INVALID_DEVICE:
+            hip.hipGetLastError()
+    yield
+
+
 @pytest.fixture(scope="session")
 def ctx():
     from syzkaller_amd.cover import Context, default_context

@@ -73,3 +73,49 @@ def test_c2_full_batch_steady_state_vs_oracle(ctx):
     ns.close()
     ms.close()
     call("sg_ctx_reset_stream", ctx.h)
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_fresh_batch_sets_vs_oracle(ctx):
+    """The headline configuration itself (bench.py's recipe): a fresh Zipf
+    batch of 64Ki programs x 16 calls x 1024 PCs against a >= 16M-entry
+    maxSignal taken from a warm batch's first programs.  Every record is
+    queued (each carries a never-seen edge), so the check that matters is the
+    ~200M new signals: maxSignal and newSignal after the batch, exported and
+    compared whole with the oracle's sequential loop, plus the flags."""
+    from syzkaller_amd._lib import call
+    from syzkaller_amd.cover import SignalSet
+
+    nprog, calls, pcs = 65536, 16, 1024
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    trace = torch.empty(nprog * calls * pcs, dtype=torch.int32, device="cuda")
+    # maxSignal: the warm batch's (seed 2_000_000) first 4608 programs
+    nwarm = 4608
+    call("sg_gen_zipf_traces_dev", ctx.h, UNIVERSE_SEED, 2_000_000, 1.1, 1 << 20, 0, nwarm, calls, pcs, trace.data_ptr())
+    wsig, woff = _signal(call, ctx, trace, nwarm, calls, pcs)
+    m0 = np.unique(wsig.cpu().numpy().view(np.uint32))
+    del wsig, woff
+    assert m0.size >= 16 << 20
+    # the bench's first timed batch (seed 1000 + warmup 2)
+    call("sg_gen_zipf_traces_dev", ctx.h, UNIVERSE_SEED, 1_002, 1.1, 1 << 20, 0, nprog, calls, pcs, trace.data_ptr())
+    sig, off = _signal(call, ctx, trace, nprog, calls, pcs)
+    del trace
+    nvals, nrec = sig.numel(), off.numel() - 1
+    ms, ns = SignalSet(ctx), SignalSet(ctx)
+    call("sg_set_add_dev", ms.h, torch.from_numpy(m0.view(np.int32)).cuda().data_ptr(), m0.size)
+    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
+         None, None)
+    torch.cuda.synchronize()
+    got = rec_new.cpu().numpy()
+    om, on = O.OSet(m0), O.OSet()
+    exp = O.triage_flags_only(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
+    assert np.array_equal(got, exp)
+    gn, en = ns.export(), on.export()
+    assert gn.size > 100_000_000 and gn.size == en.size  # ~208M new signals
+    assert np.array_equal(gn, en)
+    del gn, en
+    assert np.array_equal(ms.export(), om.export())
+    ns.close()
+    ms.close()
+    call("sg_ctx_reset_stream", ctx.h)

@@ -61,6 +61,9 @@ class NumpyPrefixStages:
     def or_words(self, s, t):
         s.w |= t.numpy().view(np.uint32)[:WORDS]
 
+    def or_new_words(self, s, t, exclude):
+        s.w |= t.numpy().view(np.uint32)[:WORDS] & ~exclude.w
+
     def prefix_or(self, parts, nparts, words, prefix, total):
         p = parts.numpy().view(np.uint32)[: nparts * words].reshape(nparts, words)
         pre = prefix.numpy().view(np.uint32)[: nparts * words].reshape(nparts, words)
@@ -117,7 +120,7 @@ M0 = np.arange(0, 3000, 5, dtype=np.uint32)
 BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
 
 
-def _worker(rank, world, port, q, pipelined, gather):
+def _worker(rank, world, port, q, pipelined, gather, drain=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -127,7 +130,15 @@ def _worker(rank, world, port, q, pipelined, gather):
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
+        drained = []  # drain: newSignal after each batch's finish, then cleared (the Poll, fuzzer.go:358-364)
         pend = None
+
+        def finish(pd):
+            assert tri.finish(pd[0]) == pd[1]
+            if drain:
+                drained.append(ns.export())
+                ns.w[:] = 0
+
         for seed, nrec in BATCHES:
             vals, off = batch(seed, nrec)
             r0, r1 = split(nrec, world, seed)[rank]
@@ -143,25 +154,32 @@ def _worker(rank, world, port, q, pipelined, gather):
             # lacks this batch's total) before the previous one is finished
             p = tri.start(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new, nrec_total=nrec)
             if pend is not None:
-                assert tri.finish(pend[0]) == pend[1]
+                finish(pend)
             pend = (p, nrec)
         if pend is not None:
-            assert tri.finish(pend[0]) == pend[1]
-        q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(), ns.export()))
+            finish(pend)
+        q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(),
+               drained if drain else ns.export()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,pipelined,gather", [(2, False, False), (4, False, False), (2, True, False),
-                                                    (4, True, False), (2, True, True), (4, False, True)])
-def test_prefix_triage_equals_sequential_loop(world, pipelined, gather):
+@pytest.mark.parametrize("world,pipelined,gather,drain", [(2, False, False, False), (4, False, False, False),
+                                                          (2, True, False, False), (4, True, False, False),
+                                                          (2, True, True, False), (4, False, True, False),
+                                                          (2, True, False, True), (4, True, True, True)])
+def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain):
+    """drain: newSignal is read and cleared after every finish() while the next
+    batch is already started -- each drained set must be exactly that batch's
+    new signal (fuzzer.go:674: only what maxSignal lacked), not a re-report of
+    the previous batch's."""
     from oracle import pyoracle as O
 
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather, drain)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -172,9 +190,13 @@ def test_prefix_triage_equals_sequential_loop(world, pipelined, gather):
         p.join(timeout=60)
         assert p.exitcode == 0
     om, on = O.OSet(M0), O.OSet()
+    per_batch_new = []
     for b, (seed, nrec) in enumerate(BATCHES):
         vals, off = batch(seed, nrec)
+        if drain:
+            on = O.OSet()
         ef = O.triage_flags_only(om, on, vals, off)
+        per_batch_new.append(on.export().tolist())
         got = np.zeros(nrec, np.uint8)
         for r in range(world):
             r0, fl = res[r][0][b]
@@ -184,4 +206,7 @@ def test_prefix_triage_equals_sequential_loop(world, pipelined, gather):
             assert 0 < ef.sum() < nrec  # mixed flags
     for r in range(world):  # the replicated state is the sequential loop's on every rank
         assert res[r][1] == om.export().tolist()
-        assert res[r][2] == on.export().tolist()
+        if drain:
+            assert res[r][2] == per_batch_new
+        else:
+            assert res[r][2] == on.export().tolist()

@@ -190,7 +190,7 @@ def test_shard_owners_and_flags_vs_numpy(ctx):
         assert np.array_equal(got.cpu().numpy(), exp.numpy()), (rec_lo, nrec)
 
 
-def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
+def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=False):
     from syzkaller_amd import cover as C
     from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
     from tests.test_shard import split
@@ -205,10 +205,12 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs"):
         side_ctx = C.Context(ctx_dev)
         with torch.cuda.stream(side):
             side_st = HipStages(side_ctx)
-        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=True, side_stages=side_st, side_stream=side,
-                           gather=False)
+        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=True, side_stages=side_st,
+                           side_stream=side, gather=False)
+    elif proto == "prefix":
+        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=collectives)
     else:
-        tri = (PrefixTriage if proto == "prefix" else ShardedTriage)(HipStages(ctx), Comm())
+        tri = ShardedTriage(HipStages(ctx), Comm(collectives=collectives))
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
     C.SignalAdd(ms, m0)
     out, pend = [], None
@@ -271,13 +273,17 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, proto):
+def _worker(rank, world, port, q, proto, backend="gloo"):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank on the box's one GPU, its collectives forced on
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _run_protocol(0, world, rank, BATCHES, M0, proto)))
+        q.put((rank, _run_protocol(0, world, rank, BATCHES, M0, proto, collectives=backend == "nccl")))
     finally:
         dist.destroy_process_group()
 
@@ -310,3 +316,29 @@ def test_sharded_protocol_two_ranks_one_gpu(proto):
         assert np.array_equal(got, ef[b]), b
     for r in range(world):
         assert res[r][1] == em and res[r][2] == en
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
+def test_sharded_protocol_rccl_one_rank(proto):
+    """The RCCL branch of Comm (syzkaller_amd/shard.py): a one-rank "nccl"
+    group with the collectives forced on, so the device-tensor
+    all_to_all_single / all_gather_into_tensor run through RCCL, the async
+    handles are waited on, and (prefix_pipelined) the prefix-OR runs on the
+    side stream between them; flags and sets equal the oracle's sequential
+    loop.  (Two or more RCCL ranks need one GPU each: the driver's multi-GPU
+    runs.)"""
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    p = mctx.Process(target=_worker, args=(0, 1, port, q, proto, "nccl"))
+    p.start()
+    r, (out, m, n) = q.get(timeout=280)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    ef, em, en = _expected()
+    for b, (r0, fl) in enumerate(out):
+        assert np.array_equal(np.array(fl, np.uint8), ef[b]), b
+    assert m == em and n == en
