@@ -109,7 +109,7 @@ def row_c4(ctx, rng):
     t0 = time.perf_counter()
     sel = C.minimize_csr(vals, off, order, ctx=ctx)
     wall = time.perf_counter() - t0
-    kt = ktime(ctx, ["tile_rec", "triage_claim", "triage_resolve", "scan", "emit"])
+    kt = ktime(ctx, ["min_claim", "min_owners", "scan", "emit"])
     ctx.timing(False)
     dev_ms = sum(kt.values())
     N = int(vals.size)
@@ -187,7 +187,8 @@ def row_f2(ctx, rng):
         t0 = time.perf_counter()
         fv, fo = C.union_fold(vals, off, grp, ng, ctx=ctx)
         wall = time.perf_counter() - t0
-        kt = ktime(ctx, ["union_fold", "merge_small", "merge_keep", "merge_scatter", "scan"])
+        kt = ktime(ctx, ["union_fold", "fold_keys", "fold_sort", "fold_unique", "merge_small", "merge_keep",
+                         "merge_scatter", "scan"])
         ctx.timing(False)
         dev = kt.get("union_fold", 0.0)
         algo = 4 * (vals.size + fv.size)  # every input element read once, every fold element written once

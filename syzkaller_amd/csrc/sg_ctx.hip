@@ -249,6 +249,11 @@ size_t scan_ws_bytes(uint64_t n) {
   return b + 512;
 }
 
+__global__ void k_copy_u64(const uint64_t* __restrict__ in, uint64_t n, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+
 static int scan_u64_inplace(sg_ctx* ctx, uint64_t* data, uint64_t n, char* scratch) {
   // exclusive in-place scan of n u64 values (used for tile sums)
   if (n == 0) return SG_OK;
@@ -276,7 +281,9 @@ int scan_counts(sg_ctx* ctx, const uint32_t* d_in, uint64_t* d_out, uint64_t n, 
     return SG_OK;
   }
   hipLaunchKernelGGL(k_scan_tile, dim3((uint32_t)nt), dim3(kBlock), 0, ctx->stream, d_in, n, d_out, sums);
-  SG_HIP(hipMemcpyAsync(bases, sums, nt * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  // (a copy kernel: a device-to-device hipMemcpyAsync between two kernels
+  // leaves the stream idle around it)
+  hipLaunchKernelGGL(k_copy_u64, dim3(div_up(nt, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)sums, nt, bases);
   int rc = scan_u64_inplace(ctx, bases, nt, next);
   if (rc) return rc;
   if (nt > 1) hipLaunchKernelGGL(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_out, n, bases);

@@ -10,9 +10,18 @@
 // seen a and b times and drops 0xFFFFFFFF (cover.go:97), so a fold is: every
 // value with its largest count over the folded lists, ascending, sentinel
 // dropped -- associative and commutative.  The reference walks the inputs one
-// after another, O(inputs x |cov|) element copies; here the lists of every
-// group are merged pairwise in a balanced tree, one batched Union launch per
-// level over all groups (merge_dev, sg_merge.hip), O(N log inputs).
+// after another, O(inputs x |cov|) element copies.
+//
+// Here: one k-way segmented sort + unique.  Element i of list k (group g)
+// gets its copy index j = i - (start of its run of equal values in the list;
+// lists are sorted); the fold of g is then the distinct (g, v, j), sorted:
+// a value with largest count c over the lists comes with j = 0 .. c - 1.  So
+// each element becomes one 64-bit key g << (32 + jb) | v << jb | j (jb = the
+// bits of the largest j, 0 for canonical covers), the keys are radix-sorted
+// (sg_sort.hip), and the first key of each run is kept unless v is the
+// sentinel.  A group's output starts at the number of kept keys before its
+// first key.  Where g, v and j do not fit 64 bits the lists are merged
+// pairwise in a balanced tree instead (merge_dev, sg_merge.hip).
 #include "sg_internal.h"
 
 #include <algorithm>
@@ -22,6 +31,9 @@ namespace sg {
 int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint32_t* dout, const uint64_t* a_beg,
               const uint64_t* a_len, const uint64_t* b_beg, const uint64_t* b_len, const uint64_t* out_beg,
               size_t npair, uint64_t* out_len);
+size_t radix_sort_ws(uint64_t n);
+int radix_sort_u64(sg_ctx* ctx, uint64_t* a, uint64_t* b, uint64_t n, size_t ws_used, uint64_t** sorted,
+                   uint64_t vary = 0);
 
 namespace {
 
@@ -38,6 +50,213 @@ __global__ void k_fold_pack(const uint32_t* __restrict__ src, const uint64_t* __
 struct Item {
   uint64_t beg, len;
 };
+
+// One wave per list: the copy index of each element (its position in its run
+// of equal values), by a wave max-scan of run starts carried across chunks.
+// kKeys: write the element's key; else the largest index into stats[0] and
+// the AND / OR of the values into stats[1] / stats[2] (the key bits that vary).
+template <bool kKeys>
+__global__ void k_fold_runs(const uint32_t* __restrict__ vals, const uint64_t* __restrict__ off, uint64_t n,
+                            const uint32_t* __restrict__ group, uint32_t jb, unsigned long long* __restrict__ stats,
+                            uint64_t* __restrict__ keys) {
+  const uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t b = off[k], e = off[k + 1];
+  const uint64_t gtop = kKeys ? (uint64_t)(group ? group[k] : 0u) << (32 + jb) : 0;
+  int carry = -1;  // the last run start (list-relative) before this chunk
+  uint32_t mj = 0, va = 0xFFFFFFFFu, vo = 0;
+  for (uint64_t c = b; c < e; c += 64) {
+    const uint64_t i = c + lane;
+    const bool live = i < e;
+    const uint32_t v = live ? vals[i] : 0u;
+    const bool start = live && (i == b || vals[i - 1] != v);
+    const int rs = max(sgd::wave_incl_max(start ? (int)(i - b) : -1), carry);
+    const uint32_t j = (uint32_t)((int)(i - b) - rs);
+    if (live) {
+      if (kKeys)
+        keys[i] = gtop | ((uint64_t)v << jb) | j;
+      else {
+        mj = max(mj, j);
+        va &= v;
+        vo |= v;
+      }
+    }
+    carry = __builtin_amdgcn_readlane(rs, 63);
+  }
+  if (!kKeys) {
+    for (int d = 32; d; d >>= 1) {
+      mj = max(mj, (uint32_t)__shfl_xor((int)mj, d));
+      va &= (uint32_t)__shfl_xor((int)va, d);
+      vo |= (uint32_t)__shfl_xor((int)vo, d);
+    }
+    // (read-checked: an atomic only when it changes the word -- every wave's
+    // atomic on the same three words cost ~1 ms per 50K lists)
+    if (lane == 0) {
+      if (mj > __hip_atomic_load(&stats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&stats[0], (unsigned long long)mj);
+      const unsigned long long a = __hip_atomic_load(&stats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((a & va) != a) atomicAnd(&stats[1], (unsigned long long)va);
+      const unsigned long long o = __hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((o | vo) != o) atomicOr(&stats[2], (unsigned long long)vo);
+    }
+  }
+}
+
+// The unique pass over the sorted keys, as a tile compaction (tiles of 8192
+// keys, 512 threads, wave w owning positions [1024 w, +1024) as 16 steps of
+// 64): a key is kept when it starts its run and its value is not the sentinel
+// (cover.go:97).  k_fold_count counts a tile's kept keys; k_fold_write, after
+// a scan of those counts, writes the kept values in order and, at each
+// group's first key, the group's output start (the kept keys before it).
+constexpr int kFuThreads = 512, kFuSteps = 16;
+constexpr uint32_t kFuTile = kFuThreads * kFuSteps;
+
+__device__ __forceinline__ bool fold_kept(const uint64_t* keys, uint64_t i, uint32_t jb) {
+  const uint64_t k = keys[i];
+  return (i == 0 || keys[i - 1] != k) && (uint32_t)(k >> jb) != 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(kFuThreads) void k_fold_count(const uint64_t* __restrict__ keys, uint64_t n, uint32_t jb,
+                                                           uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t ws[kFuThreads / 64];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint64_t base = (uint64_t)blockIdx.x * kFuTile + (uint64_t)w * (64 * kFuSteps);
+  uint32_t c = 0;
+  for (int s = 0; s < kFuSteps; s++) {
+    const uint64_t i = base + s * 64 + lane;
+    c += (uint32_t)__popcll(__ballot(i < n && fold_kept(keys, i, jb)));
+  }
+  if (lane == 0) ws[w] = c;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int j = 0; j < kFuThreads / 64; j++) t += ws[j];
+    tcnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kFuThreads) void k_fold_write(const uint64_t* __restrict__ keys, uint64_t n, uint32_t jb,
+                                                           const uint64_t* __restrict__ tpos, uint32_t* __restrict__ out,
+                                                           uint64_t* __restrict__ first) {
+  __shared__ uint32_t ws[kFuThreads / 64];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint64_t base = (uint64_t)blockIdx.x * kFuTile + (uint64_t)w * (64 * kFuSteps);
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t c = 0;
+  for (int s = 0; s < kFuSteps; s++) {
+    const uint64_t i = base + s * 64 + lane;
+    c += (uint32_t)__popcll(__ballot(i < n && fold_kept(keys, i, jb)));
+  }
+  if (lane == 0) ws[w] = c;
+  __syncthreads();
+  uint64_t pos = tpos[blockIdx.x];
+  for (int j = 0; j < w; j++) pos += ws[j];
+  for (int s = 0; s < kFuSteps; s++) {
+    const uint64_t i = base + s * 64 + lane;
+    const bool live = i < n;
+    const uint64_t k = live ? keys[i] : 0ull;
+    const uint64_t prev = live && i ? keys[i - 1] : ~k;
+    const bool kept = live && prev != k && (uint32_t)(k >> jb) != 0xFFFFFFFFu;
+    const uint64_t m = __ballot(kept);
+    const uint64_t at = pos + (uint64_t)__popcll(m & lt);
+    if (kept) out[at] = (uint32_t)(k >> jb);
+    const uint64_t g = k >> (32 + jb);
+    if (live && (i == 0 || (prev >> (32 + jb)) != g)) first[g] = at;  // this group's first key
+    pos += (uint64_t)__popcll(m);
+  }
+}
+
+constexpr int SG_EOVERFLOW_FOLD = 1;  // internal: the keys do not fit 64 bits
+
+static uint32_t bits_for(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+
+// The sort + unique fold (ctx lock held; arguments checked, N > 0).
+static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, const uint32_t* group,
+                       size_t ngroups, uint32_t* out_vals, size_t cap, uint64_t* out_off) {
+  const uint64_t N = off[n];
+  const uint32_t gb = bits_for(ngroups - 1);
+  if (gb + 32 > 64) return SG_EOVERFLOW_FOLD;
+  // inputs: values, offsets, groups (device staging)
+  const size_t b_v = (N * 4 + 255) & ~size_t(255), b_o = ((n + 1) * 8 + 255) & ~size_t(255),
+               b_g = (n * 4 + 255) & ~size_t(255);
+  int rc = dstage_reserve(ctx, b_v + b_o + b_g + 256);
+  if (rc) return rc;
+  uint32_t* dv = (uint32_t*)ctx->dstage;
+  uint64_t* doff = (uint64_t*)((char*)ctx->dstage + b_v);
+  uint32_t* dgrp = group ? (uint32_t*)((char*)ctx->dstage + b_v + b_o) : nullptr;
+  // workspace: keys (2 buffers), keep flags, their scan, group first indices / positions, max j
+  WsPlan p;
+  const uint64_t ntile = (N + kFuTile - 1) / kFuTile;
+  const size_t oA = p.add(N * 8), oB = p.add(N * 8), oK = p.add(ntile * 4), oP = p.add((ntile + 1) * 8),
+               oF = p.add(ngroups * 8), oJ = p.add(24);
+  const size_t sort_at = p.total, need = p.total + std::max(radix_sort_ws(N), scan_ws_bytes(ntile));
+  rc = ws_reserve(ctx, need);
+  if (rc) return rc;
+  uint64_t *ka = (uint64_t*)ws_at(ctx, oA), *kb = (uint64_t*)ws_at(ctx, oB), *tpos = (uint64_t*)ws_at(ctx, oP);
+  uint32_t* tcnt = (uint32_t*)ws_at(ctx, oK);
+  uint64_t* first = (uint64_t*)ws_at(ctx, oF);
+  unsigned long long* stats = (unsigned long long*)ws_at(ctx, oJ);  // max j, AND and OR of the values
+  SG_HIP(hipMemcpyAsync(dv, vals, N * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  if (group) SG_HIP(hipMemcpyAsync(dgrp, group, n * 4, hipMemcpyHostToDevice, ctx->stream));
+  unsigned long long st[3] = {0, 0xFFFFFFFFull, 0};
+  SG_HIP(hipMemcpyAsync(stats, st, 24, hipMemcpyHostToDevice, ctx->stream));
+  const dim3 lgrid(div_up(n, 4));
+  {
+    ScopedTimer tm(ctx, "union_fold");
+    hipLaunchKernelGGL(k_fold_runs<false>, lgrid, dim3(256), 0, ctx->stream, dv, doff, (uint64_t)n, dgrp, 0u, stats,
+                       nullptr);
+  }
+  SG_HIP(hipMemcpyAsync(st, stats, 24, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  const uint32_t jb = bits_for(st[0]);
+  if (gb + 32 + jb > 64) return SG_EOVERFLOW_FOLD;
+  // the key bits that vary: the group's, the values' (AND vs OR), the copy index's
+  const uint64_t vary = ((gb ? ((1ull << gb) - 1) : 0ull) << (32 + jb)) | ((st[1] ^ st[2]) << jb) |
+                        (jb ? (1ull << jb) - 1 : 0ull);
+  uint64_t* sorted = nullptr;
+  uint32_t* dout = nullptr;
+  {
+    ScopedTimer tm(ctx, "union_fold");
+    {
+      ScopedTimer tk(ctx, "fold_keys");
+      hipLaunchKernelGGL(k_fold_runs<true>, lgrid, dim3(256), 0, ctx->stream, dv, doff, (uint64_t)n, dgrp, jb, stats,
+                         ka);
+    }
+    {
+      ScopedTimer ts(ctx, "fold_sort");
+      rc = radix_sort_u64(ctx, ka, kb, N, sort_at, &sorted, vary);
+      if (rc) return rc;
+    }
+    ScopedTimer tu(ctx, "fold_unique");
+    SG_HIP(hipMemsetAsync(first, 0xFF, ngroups * 8, ctx->stream));
+    hipLaunchKernelGGL(k_fold_count, dim3((uint32_t)ntile), dim3(kFuThreads), 0, ctx->stream, (const uint64_t*)sorted, N,
+                       jb, tcnt);
+    rc = scan_counts(ctx, tcnt, tpos, ntile, sort_at);
+    if (rc) return rc;
+    dout = (uint32_t*)(sorted == ka ? kb : ka);  // the other key buffer, free now
+    hipLaunchKernelGGL(k_fold_write, dim3((uint32_t)ntile), dim3(kFuThreads), 0, ctx->stream, (const uint64_t*)sorted, N,
+                       jb, (const uint64_t*)tpos, dout, first);
+    SG_HIP(hipGetLastError());
+  }
+  std::vector<uint64_t> f(ngroups);
+  uint64_t total = 0;
+  SG_HIP(hipMemcpyAsync(f.data(), first, ngroups * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipMemcpyAsync(&total, tpos + ntile, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  out_off[ngroups] = total;
+  for (size_t gi = ngroups; gi-- > 0;) out_off[gi] = f[gi] == ~0ull ? out_off[gi + 1] : f[gi];
+  if (total > cap) {
+    set_error("sg_union_fold: %llu values, capacity %zu", (unsigned long long)total, cap);
+    return SG_EINVAL;
+  }
+  if (total == 0) return SG_OK;
+  if (!out_vals) return SG_EINVAL;
+  SG_HIP(hipMemcpyAsync(out_vals, dout, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
 
 }  // namespace
 }  // namespace sg
@@ -63,14 +282,19 @@ int sg_union_fold(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t
     }
   }
   const uint64_t N = off[n];
-  // the lists of each group, in input order (the order does not change the result)
-  std::vector<std::vector<Item>> items(ngroups);
-  for (size_t k = 0; k < n; k++) items[group ? group[k] : 0].push_back({off[k], off[k + 1] - off[k]});
   std::fill(out_off, out_off + ngroups + 1, 0);
   if (N == 0) return SG_OK;
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
+  rc = fold_sorted(ctx, vals, off, n, group, ngroups, out_vals, cap, out_off);
+  if (rc != SG_EOVERFLOW_FOLD) return rc;
+  // (g, v, j) does not fit 64 bits: a balanced tree of batched Unions, one
+  // launch per level over all groups
+  std::fill(out_off, out_off + ngroups + 1, 0);
+  // the lists of each group, in input order (the order does not change the result)
+  std::vector<std::vector<Item>> items(ngroups);
+  for (size_t k = 0; k < n; k++) items[group ? group[k] : 0].push_back({off[k], off[k + 1] - off[k]});
   // two ping-pong buffers of N values: a level's results never exceed its inputs
   const size_t b_v = (N * 4 + 255) & ~size_t(255);
   rc = dstage_reserve(ctx, 2 * b_v + 4 * ((ngroups + 1) * 8 + 256));

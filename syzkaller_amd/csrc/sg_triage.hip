@@ -317,6 +317,51 @@ __global__ __launch_bounds__(kBlock) void k_add_flagged_segs(const uint32_t* __r
   }
 }
 
+// ---- Minimize (cover.go:120-146) -----------------------------------------------
+// One workgroup per input: its elements all carry its rank key, so there is
+// no per-element item search.  Each element lowers owner[v] to the key
+// (read-checked atomicMin, the same first-owner rule as k_claim).  An element
+// that reads a key of an older generation (>= key_end: no element of this
+// call has written v yet) also sets v's bit in the touched bitmap (2^32 bits,
+// the set layout), so about one global atomicOr per distinct value: the
+// first current-generation writer of v always sets it.  The owners are then
+// flagged from the touched bitmap alone (k_min_owners, one read of 512 MiB)
+// instead of re-reading the corpus (k_resolve).
+__global__ __launch_bounds__(kBlock) void k_min_claim(const uint32_t* __restrict__ vals, const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ rank, uint32_t key_lo,
+                                                      uint32_t key_end, uint32_t* __restrict__ owner,
+                                                      uint32_t* __restrict__ touched) {
+  const uint64_t k = blockIdx.x;
+  const uint64_t b = off[k], e = off[k + 1];
+  const uint32_t key = key_lo + rank[k];
+  for (uint64_t i = b + threadIdx.x; i < e; i += kBlock) {
+    const uint32_t v = vals[i];
+    uint32_t* p = owner + v;
+    const uint32_t o = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o > key) {
+      atomicMin(p, key);
+      if (o >= key_end) sgd::set_bit(touched, v);
+    }
+  }
+}
+
+// flag[order[owner rank]] for every touched value (bit q of word w is signal
+// set_sig(32 w + q))
+__global__ void k_min_owners(const uint32_t* __restrict__ touched, const uint32_t* __restrict__ owner, uint32_t key_lo,
+                             const uint32_t* __restrict__ order, uint8_t* __restrict__ flag) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w4 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w4 < kSetWords / 4; w4 += stride) {
+    const uint4 q = reinterpret_cast<const uint4*>(touched)[w4];
+    const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      for (uint32_t m = ws[j]; m; m &= m - 1) {
+        const uint32_t v = sgd::set_sig((uint32_t)((w4 * 4 + j) << 5) | (uint32_t)__builtin_ctz(m));
+        flag[order[owner[v] - key_lo]] = 1;
+      }
+  }
+}
+
 __global__ void k_invert_perm(const uint32_t* __restrict__ order, uint64_t n, uint32_t* __restrict__ rank) {
   uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) rank[order[k]] = (uint32_t)k;
@@ -757,16 +802,15 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   int rc = check_alloc(ctx);
   if (rc) return rc;
   WsPlan p;
-  size_t o[5];
   size_t o_in = p.add(nv * 4), o_off = p.add((n + 1) * 8), o_ord = p.add(n * 4), o_rank = p.add(n * 4),
          o_flag = p.add(n), o_fr = p.add(n), o_out = p.add(n * 4), o_m = p.add(((n + kTile - 1) / kTile) * kTile / 8),
-         o_c = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 4), o_b = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 8 + 8);
-  size_t scan_b = scratch_plan(p, nv, o);
+         o_c = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 4), o_b = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 8 + 8),
+         o_t = p.add(kSetBytes);
   size_t scan_off = p.total;
   size_t scan_b2 = scan_ws_bytes(((n + kTile - 1) / kTile) * kChunksPerTile);
-  rc = ws_reserve(ctx, p.total + std::max(scan_b, scan_b2));
+  rc = ws_reserve(ctx, p.total + scan_b2);
   if (rc) return rc;
-  Scratch s = scratch_bind(ctx, nv, o);
+  uint32_t* dtouch = (uint32_t*)ws_at(ctx, o_t);  // touched values (set layout)
   uint32_t* din = (uint32_t*)ws_at(ctx, o_in);
   uint64_t* doff = (uint64_t*)ws_at(ctx, o_off);
   uint32_t* dord = (uint32_t*)ws_at(ctx, o_ord);
@@ -782,17 +826,22 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   uint32_t key_lo;
   rc = owner_keys(ctx, n, &key_lo);
   if (rc) return rc;
-  PipeArgs a{};
-  a.vals = din;
-  a.n = nv;
-  a.off = doff;
-  a.nseg = n;
-  a.filter = nullptr;  // covered starts empty (cover.go:130)
-  a.rank = drank;
-  a.key_lo = key_lo;
-  a.seg_flag = dflag;
-  rc = run_pipe(ctx, a, s);
-  if (rc) return rc;
+  // the owner table: every element lowers its value's owner to its input's
+  // rank key (covered starts empty, cover.go:130); the inputs owning some
+  // value are the selected ones (cover.go:133-141)
+  {
+    ScopedTimer tm(ctx, "min_claim");
+    SG_HIP(hipMemsetAsync(dtouch, 0, kSetBytes, ctx->stream));
+    hipLaunchKernelGGL(k_min_claim, dim3((uint32_t)n), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
+                       (const uint64_t*)doff, (const uint32_t*)drank, key_lo, (uint32_t)(key_lo + n), ctx->owner,
+                       dtouch);
+  }
+  {
+    ScopedTimer tm(ctx, "min_owners");
+    hipLaunchKernelGGL(k_min_owners, dim3(4096), dim3(256), 0, ctx->stream, (const uint32_t*)dtouch,
+                       (const uint32_t*)ctx->owner, key_lo, (const uint32_t*)dord, dflag);
+  }
+  SG_HIP(hipGetLastError());
   // selected indices in processing order: compact order[k] where flag[order[k]]
   hipLaunchKernelGGL(k_gather_flag, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, dord, (uint64_t)n, dflag, dfr);
   Scratch s2;

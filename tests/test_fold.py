@@ -65,3 +65,48 @@ def test_union_fold_vs_oracle(ctx, multiset):
     # nothing at all
     gv, go = C.union_fold(np.zeros(0, np.uint32), np.zeros(3, np.uint64), ctx=ctx)
     assert gv.size == 0 and not go.any()
+
+
+@pytest.mark.gpu
+def test_union_fold_key_width_edges(ctx):
+    """The sort path packs (group, value, copy index) into 64 bits: 2^20
+    groups (20 bits) with a value repeated 4096 times (copy index 4095: 12
+    bits) fill them exactly; 8192 repeats need 13 bits, so that fold takes the
+    merge-tree path.  Both equal the oracle's left fold."""
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(55)
+    ng = 1 << 20
+    for reps in (4096, 8192):
+        covs = [np.sort(rng.integers(0, 1 << 32, size=int(rng.integers(0, 50)), dtype=np.uint64).astype(np.uint32))
+                for _ in range(300)]
+        covs[7] = np.concatenate([covs[7][:3], np.full(reps, 0xC0FFEE, np.uint32)])
+        covs[7].sort()
+        covs[9] = np.array([0xC0FFEE] * 5 + [0xFFFFFFFF] * 3, np.uint32)
+        vals, off = C.to_csr(covs)
+        grp = rng.integers(0, ng, size=len(covs)).astype(np.uint32)
+        grp[9] = grp[7]
+        grp[10] = ng - 1
+        gv, go = C.union_fold(vals, off, grp, ng, ctx=ctx)
+        ev, eo = O.union_fold(vals, off, grp, ng)
+        assert np.array_equal(go, eo) and np.array_equal(gv, ev), reps
+
+
+@pytest.mark.gpu
+def test_union_fold_zipf_corpus(ctx):
+    """A bench-like corpus (canonical Zipf covers, many groups) against the
+    oracle: values sharing their top byte, so the sort skips digits."""
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(56)
+    n = 4000
+    lens = np.clip(np.exp(rng.normal(np.log(300), 0.8, size=n)), 1, 4000).astype(np.int64)
+    ranks = np.minimum(rng.zipf(1.05, size=int(lens.sum())), 1 << 21) - 1
+    raw = (0x81000000 + 16 * ranks).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(lens)])
+    covs = [np.unique(raw[off[k]:off[k + 1]]) for k in range(n)]
+    vals, off = C.to_csr(covs)
+    for grp, ng in ((rng.integers(0, 300, size=n).astype(np.uint32), 300), (None, 1)):
+        gv, go = C.union_fold(vals, off, grp, ng, ctx=ctx)
+        ev, eo = O.union_fold(vals, off, grp, ng)
+        assert np.array_equal(go, eo) and np.array_equal(gv, ev)
