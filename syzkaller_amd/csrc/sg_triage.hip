@@ -327,13 +327,17 @@ __global__ __launch_bounds__(kBlock) void k_add_flagged_segs(const uint32_t* __r
 // first current-generation writer of v always sets it.  The owners are then
 // flagged from the touched bitmap alone (k_min_owners, one read of 512 MiB)
 // instead of re-reading the corpus (k_resolve).
+// Workgroups run in processing order (block b = the input of rank b, key
+// key_lo + b): the early ranks claim the corpus's common values first, so a
+// later element's read-check mostly finds a smaller key and issues no atomic,
+// and the longest inputs (sort.Sort puts them first, cover.go:157) start first.
 __global__ __launch_bounds__(kBlock) void k_min_claim(const uint32_t* __restrict__ vals, const uint64_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ rank, uint32_t key_lo,
+                                                      const uint32_t* __restrict__ order, uint32_t key_lo,
                                                       uint32_t key_end, uint32_t* __restrict__ owner,
                                                       uint32_t* __restrict__ touched) {
-  const uint64_t k = blockIdx.x;
+  const uint64_t k = order[blockIdx.x];
   const uint64_t b = off[k], e = off[k + 1];
-  const uint32_t key = key_lo + rank[k];
+  const uint32_t key = key_lo + blockIdx.x;
   for (uint64_t i = b + threadIdx.x; i < e; i += kBlock) {
     const uint32_t v = vals[i];
     uint32_t* p = owner + v;
@@ -802,7 +806,7 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   int rc = check_alloc(ctx);
   if (rc) return rc;
   WsPlan p;
-  size_t o_in = p.add(nv * 4), o_off = p.add((n + 1) * 8), o_ord = p.add(n * 4), o_rank = p.add(n * 4),
+  size_t o_in = p.add(nv * 4), o_off = p.add((n + 1) * 8), o_ord = p.add(n * 4),
          o_flag = p.add(n), o_fr = p.add(n), o_out = p.add(n * 4), o_m = p.add(((n + kTile - 1) / kTile) * kTile / 8),
          o_c = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 4), o_b = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 8 + 8),
          o_t = p.add(kSetBytes);
@@ -814,7 +818,6 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   uint32_t* din = (uint32_t*)ws_at(ctx, o_in);
   uint64_t* doff = (uint64_t*)ws_at(ctx, o_off);
   uint32_t* dord = (uint32_t*)ws_at(ctx, o_ord);
-  uint32_t* drank = (uint32_t*)ws_at(ctx, o_rank);
   uint8_t* dflag = (uint8_t*)ws_at(ctx, o_flag);
   uint8_t* dfr = (uint8_t*)ws_at(ctx, o_fr);
   uint32_t* dout = (uint32_t*)ws_at(ctx, o_out);
@@ -822,7 +825,6 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   SG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(dord, order, n * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemsetAsync(dflag, 0, n, ctx->stream));
-  hipLaunchKernelGGL(k_invert_perm, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, dord, (uint64_t)n, drank);
   uint32_t key_lo;
   rc = owner_keys(ctx, n, &key_lo);
   if (rc) return rc;
@@ -833,7 +835,7 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
     ScopedTimer tm(ctx, "min_claim");
     SG_HIP(hipMemsetAsync(dtouch, 0, kSetBytes, ctx->stream));
     hipLaunchKernelGGL(k_min_claim, dim3((uint32_t)n), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
-                       (const uint64_t*)doff, (const uint32_t*)drank, key_lo, (uint32_t)(key_lo + n), ctx->owner,
+                       (const uint64_t*)doff, (const uint32_t*)dord, key_lo, (uint32_t)(key_lo + n), ctx->owner,
                        dtouch);
   }
   {
