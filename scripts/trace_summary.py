@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
 """Timed-step launches of the triage kernels from a rocprofv3 --kernel-trace
 CSV: the launches between the REGION-th k_mark_begin / k_mark_end pair
-(bench.py brackets each timed region with sg_ctx_marker; region 0 = C2,
-1 = the steady state), their durations and launch resources.
+(bench.py brackets each timed region with sg_ctx_marker; in run order region
+0 = C2, 1 = C2 from traces, 2 = the steady state), their durations and launch
+resources.
 usage: trace_summary.py KERNEL_TRACE_CSV COMMAND OUT_JSON [REGION]"""
 import csv
 import json
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_hist_rep<false>", "k_p1_scatter<false>", "k_hist_bytes", "k_p2_scatter", "k_bucket<false, false>",
+KERNELS = ["k_hist_rep<false>", "k_hist_trace", "k_p1_scatter<false", "k_hist_bytes", "k_p2_scatter", "k_bucket<false, false>",
            "k_bucket_direct<false>", "k_bucket_groups", "k_chunk_desc", "k_cuts", "k_scan32_reduce", "k_scan32_apply",
            "k_set_copy"]
 
