@@ -147,9 +147,19 @@ def row_c5(ctx, rng):
     t0 = time.perf_counter()
     got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites, ctx=ctx)
     wall = time.perf_counter() - t0
-    kt = ktime(ctx, ["report_index", "report_first", "report_del", "report_sites"])
-    kt["report_query"] = kt.get("report_first", 0.0) + kt.get("report_del", 0.0)
+    qkeys = ("report_sorted_q", "report_count_q", "report_scatter_q", "report_chunks", "report_first", "report_del")
+    kt = ktime(ctx, ["report_index", *qkeys, "report_sites"])
+    kt["report_query"] = sum(kt.get(k) or 0.0 for k in qkeys)
     ctx.timing(False)
+    # the same queries in PC order (a canonical cover, as html.go:177-189 passes): no regrouping
+    qs = np.sort(q)
+    ctx.timing(True)
+    got_sorted = C.cover_uncovered(qs, 0xffffffff, starts, ends, sites, ctx=ctx)
+    kts = ktime(ctx, ["report_index", *qkeys, "report_sites"])
+    kts["report_query"] = sum(kts.get(k) or 0.0 for k in qkeys)
+    ctx.timing(False)
+    pc_order = {"kernels_ms": kts, "frac_hbm_query": 16 * nq / (kts["report_query"] / 1e3) / 1e9 / HBM,
+                "same_result": bool(np.array_equal(np.sort(got_sorted), np.sort(got)))}
     sample = 2_000_000
     t1 = time.perf_counter()
     ref = O.cover_uncovered(q[:sample], 0xffffffff, starts, ends, sites)
@@ -164,7 +174,8 @@ def row_c5(ctx, rng):
             "query_GBs_algo": algo / (kt["report_query"] / 1e3) / 1e9 if kt.get("report_query") else None,
             "frac_hbm_query": algo / (kt["report_query"] / 1e3) / 1e9 / HBM if kt.get("report_query") else None,
             "frac_hbm_all": algo / (dev / 1e3) / 1e9 / HBM,
-            "parity_2M_prefix": bool(np.array_equal(got_s, ref)), "cpu_oracle_s_2M": cpu, "cpu_cores": 1}
+            "parity_2M_prefix": bool(np.array_equal(got_s, ref)), "cpu_oracle_s_2M": cpu, "cpu_cores": 1,
+            "pc_order": pc_order}
 
 
 def row_f2(ctx, rng):

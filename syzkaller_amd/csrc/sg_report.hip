@@ -17,13 +17,21 @@
 // (two radix-indexed searches, first-query atomicMin per symbol, last-delete
 // atomicMax per call site), per symbol group (the first query per start
 // decides which symbol's range is added), per call site (final verdict), then
-// an ordered compaction.  The per-query pass is split in two (k_rep_first,
-// k_rep_del) so that each runs in the query order its read-check needs.  Symbols must be sorted by start with non-decreasing
+// an ordered compaction.  The per-query work runs grouped by chunks of call
+// sites (k_q_count / k_q_scatter / k_q_chunk: every lookup and both
+// reductions in LDS); past 16M call sites it is two passes of radix-indexed
+// global searches (k_rep_first, k_rep_del), each in the query order its
+// read-check needs.  Symbols must be sorted by start with non-decreasing
 // ends (the condition under which the reference's binary search over ends is
 // meaningful).
 #include "sg_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
+
+#ifndef SG_REPORT_DIAG
+#define SG_REPORT_DIAG 0
+#endif
 
 namespace sg {
 
@@ -162,6 +170,443 @@ __global__ __launch_bounds__(256) void k_rep_del(RepArgs a) {
   }
 }
 
+// ---- chunked query path --------------------------------------------------
+// The two per-query reductions (first query per symbol: a minimum; last
+// deleting query per call site: a maximum) do not depend on the order in
+// which queries are visited, so the queries can be regrouped freely.  The
+// call sites are cut into chunks of kSites consecutive sites (32 KiB of u64
+// PCs); a query belongs to the chunk that holds lower_bound(sites, pc), i.e.
+// the chunk c with bnd[c-1] < pc <= bnd[c] (bnd[c] = the chunk's last site;
+// chunk nch = above every site).  The queries are counted and scattered by
+// chunk (k_q_count, k_q_scatter: chunk found by a search over bnd in LDS),
+// then each chunk's queries run against its sites, and the symbols its PC
+// range can land in, held in LDS (k_q_chunk): every lookup is an LDS search,
+// the two reductions are LDS atomics, flushed once per (tile, chunk).
+constexpr uint32_t kSites = 4096;        // call sites per chunk
+constexpr uint32_t kMaxChunks = 4096;    // chunk bounds held in LDS (16M sites)
+constexpr uint32_t kChunkIdx = 8192;     // radix buckets over the chunk bounds
+constexpr uint32_t kSiteIdx = 1024;      // radix buckets over one chunk's sites
+constexpr uint32_t kSymCap = 1024;       // symbols of a chunk held in LDS
+constexpr int kQT = 1024;                // threads of the count / scatter kernels
+constexpr int kQPer = 16;                // queries per thread there (kSQPer when staged)
+constexpr int kSQPer = 8;
+constexpr int kCT = 512;                 // threads of the chunk kernel
+constexpr uint32_t kCTile = 16384;       // grouped queries per chunk-kernel tile
+
+struct ChunkArgs {
+  const uint32_t* cov;
+  uint64_t ncov;
+  uint64_t hi32;           // base << 32
+  const uint64_t* pcs;     // call sites, sorted
+  uint64_t npcs;
+  const uint64_t* sstart;
+  const uint64_t* send;
+  uint64_t nsym;
+  RadixIdx iend;           // over send (chunks whose symbols exceed kSymCap)
+  uint32_t nch;            // chunks with sites; chunk nch: above every site
+  uint32_t csh;            // radix shift of the chunk index (over pc - bnd[0])
+  uint64_t* bnd;           // [nch] last site of each chunk
+  uint16_t* cidx;          // [kChunkIdx + 1] bounds below bnd[0] + (k << csh)
+  uint2* symr;             // [nch + 1] symbol range a chunk's queries can land in (lo, hi inclusive)
+  uint32_t* ssh;           // [nch] radix shift of each chunk's site index
+  uint16_t* sidx;          // [nch][kSiteIdx + 1] the chunk's sites below first + (k << ssh)
+  uint32_t* ssym;          // [npcs] upper_bound(send, site): the symbol a query at the site lands in
+  uint32_t ntiles;         // query tiles of the count / scatter kernels
+  uint32_t tw;             // width of a chunk's row of tiles: 8 ceil(ntiles / 8)
+  uint32_t* tcount;        // [nch + 1][tw] queries per (chunk, tile), tiles at tile_col
+  uint64_t* toff;          // [(nch + 1) tw + 1] exclusive scan of tcount: each (chunk, tile)'s first slot
+  uint32_t* jparts;        // [nch + 1] chunk-kernel jobs per chunk
+  uint64_t* jstart;        // [nch + 2] scan of jparts
+  uint64_t* qoff;          // [nch + 2] each chunk's first slot
+  uint2* grouped;          // [ncov] (cov, query index) grouped by chunk
+  uint32_t* first_q;
+  uint32_t* last_del;
+};
+
+__device__ __forceinline__ uint64_t query_pc(uint64_t hi32, uint32_t cov) { return hi32 + (uint64_t)cov - 5; }
+
+// Column of tile t in a chunk's row of the count table: the tiles that run on
+// one XCD (blockIdx % 8, round-robin dispatch: speed only) side by side, so
+// the runs that neighbouring tiles of one XCD write for a chunk share cache
+// lines in that XCD's L2 instead of leaving partial lines in several.
+__device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tw) { return (t & 7u) * (tw >> 3) + (t >> 3); }
+
+// chunk bounds and, per chunk, the range of upper_bound(send, pc) over its PCs
+__global__ void k_chunk_prep(ChunkArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > a.nch) return;
+  uint64_t lo = 0, hi = a.nsym;
+  if (c > 0) lo = ub64(a.send, a.nsym, a.pcs[c * kSites - 1]);
+  if (c < a.nch) {
+    const uint64_t last = a.pcs[min<uint64_t>((c + 1) * kSites, a.npcs) - 1];
+    a.bnd[c] = last;
+    hi = ub64(a.send, a.nsym, last);
+    const uint64_t span = last - a.pcs[c * kSites];
+    uint32_t sh = 0;
+    while (sh < 63 && (span >> sh) >= kSiteIdx) sh++;
+    a.ssh[c] = sh;
+  }
+  a.symr[c] = make_uint2((uint32_t)lo, (uint32_t)hi);
+}
+
+// per site, the symbol a query at it lands in (cover.go:278)
+__global__ void k_site_sym(ChunkArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < a.npcs) a.ssym[j] = (uint32_t)ub64(a.send, a.nsym, a.pcs[j]);
+}
+
+// per chunk, a radix index over its sites: sidx[c][k] = sites of chunk c
+// below first + (k << ssh[c]) (saturated at the top of u64)
+__global__ void k_site_index(ChunkArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(t / (kSiteIdx + 1)), k = (uint32_t)(t % (kSiteIdx + 1));
+  if (c >= a.nch) return;
+  const uint64_t* ps = a.pcs + (uint64_t)c * kSites;
+  const uint32_t m = (uint32_t)min<uint64_t>(kSites, a.npcs - (uint64_t)c * kSites);
+  const uint64_t s0 = ps[0], x0 = s0 + ((uint64_t)k << a.ssh[c]), x = x0 < s0 ? ~0ull : x0;
+  uint32_t lo = 0, hi = m;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ps[mid] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  a.sidx[t] = (uint16_t)lo;
+}
+
+// chunk index: cidx[k] = number of chunk bounds below bnd[0] + (k << csh)
+__global__ void k_chunk_index(ChunkArgs a) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > kChunkIdx) return;
+  const uint64_t b0 = a.pcs[kSites - 1 < a.npcs ? kSites - 1 : a.npcs - 1];  // bnd[0]
+  const uint64_t d = (uint64_t)k << a.csh;
+  const uint64_t x = (a.csh < 64 && (d >> a.csh) == k && b0 + d >= b0) ? b0 + d : ~0ull;
+  // bnd[c] = pcs[min((c+1) kSites, n) - 1]: search over c
+  uint32_t lo = 0, hi = a.nch;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.pcs[min<uint64_t>((uint64_t)(mid + 1) * kSites, a.npcs) - 1] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  a.cidx[k] = (uint16_t)lo;
+}
+
+// number of b[lo..hi) below x plus lo (b sorted), b in LDS
+__device__ __forceinline__ uint32_t lds_lb(const uint64_t* b, uint32_t lo, uint32_t hi, uint64_t x) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (b[mid] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+struct ChunkLds {
+  uint64_t bnd[kMaxChunks];
+  uint16_t idx[kChunkIdx + 1];
+};
+
+__device__ __forceinline__ void load_chunks(const ChunkArgs& a, ChunkLds& L) {
+  for (uint32_t i = threadIdx.x; i < a.nch; i += blockDim.x) L.bnd[i] = a.bnd[i];
+  for (uint32_t i = threadIdx.x; i <= kChunkIdx; i += blockDim.x) L.idx[i] = a.cidx[i];
+}
+
+// chunk of pc: the number of chunk bounds below it
+__device__ __forceinline__ uint32_t chunk_of(const ChunkArgs& a, const ChunkLds& L, uint64_t pc) {
+  const uint64_t b0 = L.bnd[0];
+  if (pc <= b0) return 0;
+  const uint64_t k = (pc - b0) >> a.csh;
+  if (k >= kChunkIdx) return lds_lb(L.bnd, L.idx[kChunkIdx], a.nch, pc);
+  return lds_lb(L.bnd, L.idx[k], L.idx[k + 1], pc);
+}
+
+template <int kPer>
+__global__ __launch_bounds__(kQT) void k_q_count(ChunkArgs a) {
+  __shared__ ChunkLds L;
+  __shared__ uint32_t hist[kMaxChunks + 1];
+  load_chunks(a, L);
+  for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
+  __syncthreads();
+  const uint64_t q0 = (uint64_t)blockIdx.x * kQT * kPer + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = q0 + (uint64_t)k * kQT;
+    if (i < a.ncov) atomicAdd(&hist[chunk_of(a, L, query_pc(a.hi32, a.cov[i]))], 1u);
+  }
+  __syncthreads();
+  const uint32_t col = tile_col(blockIdx.x, a.tw);
+  for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) a.tcount[(uint64_t)i * a.tw + col] = hist[i];
+}
+
+// each chunk's first slot (the scan at its first tile) and the total
+__global__ void k_q_chunk_off(ChunkArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c <= (uint64_t)a.nch + 1) a.qoff[c] = a.toff[c * a.tw];
+  if (c <= a.nch) a.jparts[c] = (uint32_t)((a.toff[(c + 1) * a.tw] - a.toff[c * a.tw] + kCTile - 1) / kCTile);
+}
+
+// (cov, query index) into the chunk's range: per workgroup a rank per chunk
+// (LDS atomics) on top of the (chunk, tile) offset from the scan.  kStaged:
+// the tile is staged in LDS in chunk order, then written out slot by slot, so
+// a wave's stores are runs of consecutive addresses (the LDS it needs leaves
+// one workgroup per CU); otherwise every query is one 8-B store.
+template <int kPer, bool kStaged>
+__global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
+  constexpr uint32_t kT = kQT * kPer;
+  __shared__ ChunkLds L;
+  __shared__ uint32_t hist[kMaxChunks + 1];  // counts, then the tile's chunk offsets
+  __shared__ uint2 stage[kStaged ? kT : 1];
+  __shared__ uint16_t cid[kStaged ? kT : 1];
+  __shared__ uint32_t wsum[kQT / 64 + 1];
+  load_chunks(a, L);
+  for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kT;
+  const uint64_t q0 = t0 + threadIdx.x;
+  uint32_t cv[kPer], ch[kPer], rk[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = q0 + (uint64_t)k * kQT;
+    ch[k] = 0xFFFFFFFFu;
+    if (i < a.ncov) {
+      cv[k] = a.cov[i];
+      ch[k] = chunk_of(a, L, query_pc(a.hi32, cv[k]));
+      rk[k] = atomicAdd(&hist[ch[k]], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* base = reinterpret_cast<uint32_t*>(L.bnd);  // (the bounds are no longer needed)
+  if (!kStaged) {
+    for (uint32_t c = threadIdx.x; c <= a.nch; c += kQT)
+      base[c] = hist[c] ? (uint32_t)a.toff[(uint64_t)c * a.tw + tile_col(blockIdx.x, a.tw)] : 0u;
+    __syncthreads();
+#if SG_REPORT_DIAG
+    // diagnostics: linear stores (the scatter's pattern removed; results wrong)
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (ch[k] != 0xFFFFFFFFu) a.grouped[q0 + (uint64_t)k * kQT] = make_uint2(cv[k], base[ch[k]] + rk[k]);
+#else
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (ch[k] != 0xFFFFFFFFu) a.grouped[base[ch[k]] + rk[k]] = make_uint2(cv[k], (uint32_t)(q0 + (uint64_t)k * kQT));
+#endif
+    return;
+  }
+  // per thread kPerT consecutive chunks: the (chunk, tile) base and the
+  // exclusive scan of the counts (the chunk's first staging slot)
+  constexpr uint32_t kPerT = (kMaxChunks + 1 + kQT - 1) / kQT;
+  const uint32_t c0 = threadIdx.x * kPerT;
+  uint32_t h[kPerT], run = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPerT; j++) {
+    const uint32_t c = c0 + j;
+    h[j] = c <= a.nch ? hist[c] : 0u;
+    run += h[j];
+  }
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t incl = sgd::wave_incl_add(run);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t x = threadIdx.x < kQT / 64 ? wsum[threadIdx.x] : 0u;
+    const uint32_t xi = sgd::wave_incl_add(x);
+    if (threadIdx.x < kQT / 64) wsum[threadIdx.x] = xi - x;
+  }
+  __syncthreads();
+  uint32_t off = wsum[wv] + incl - run;
+#pragma unroll
+  for (uint32_t j = 0; j < kPerT; j++) {
+    const uint32_t c = c0 + j;
+    if (c <= a.nch) {
+      base[c] = h[j] ? (uint32_t)a.toff[(uint64_t)c * a.tw + tile_col(blockIdx.x, a.tw)] : 0u;
+      hist[c] = off;
+    }
+    off += h[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (ch[k] != 0xFFFFFFFFu) {
+      const uint32_t slot = hist[ch[k]] + rk[k];
+      stage[slot] = make_uint2(cv[k], (uint32_t)(q0 + (uint64_t)k * kQT));
+      cid[slot] = (uint16_t)ch[k];
+    }
+  __syncthreads();
+  const uint32_t nv = (uint32_t)min<uint64_t>(kT, a.ncov - t0);
+  for (uint32_t i = threadIdx.x; i < nv; i += kQT) {
+    const uint32_t c = cid[i];
+    a.grouped[base[c] + (i - hist[c])] = stage[i];
+  }
+}
+
+// Queries in PC order (a canonical cover.Cover, as html.go:177-189 passes:
+// one input's cover or a cover.Union): every chunk's queries are already a
+// contiguous range, found by a search, and nothing is regrouped.
+// k_q_sorted: flag = 1 if some query's PC is below its predecessor's (16
+// consecutive queries per thread: four 16-B loads and the predecessor's).
+__global__ void k_q_sorted(ChunkArgs a, uint32_t* flag) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+  const bool al = ((uintptr_t)a.cov & 15) == 0;
+  bool bad = false;
+  for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i0 < a.ncov; i0 += stride) {
+    uint32_t v[16];
+    if (al && i0 + 16 <= a.ncov) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 x = reinterpret_cast<const uint4*>(a.cov + i0)[q];
+        v[4 * q] = x.x;
+        v[4 * q + 1] = x.y;
+        v[4 * q + 2] = x.z;
+        v[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; q++) v[q] = i0 + q < a.ncov ? a.cov[i0 + q] : a.cov[a.ncov - 1];
+    }
+    uint64_t prev = i0 ? query_pc(a.hi32, a.cov[i0 - 1]) : 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint64_t pc = query_pc(a.hi32, v[q]);
+      bad |= pc < prev;
+      prev = pc;
+    }
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(flag, 1u);  // (one atomic per workgroup)
+}
+
+// sorted queries: qoff[c] = queries with pc <= bnd[c - 1], and the jobs per chunk
+__global__ void k_q_direct_off(ChunkArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > (uint64_t)a.nch + 1) return;
+  uint64_t q = a.ncov;
+  if (c == 0) {
+    q = 0;
+  } else if (c <= a.nch) {
+    const uint64_t x = a.bnd[c - 1];
+    uint64_t lo = 0, hi = a.ncov;  // first query with pc > x
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (query_pc(a.hi32, a.cov[mid]) <= x)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    q = lo;
+  }
+  a.qoff[c] = q;
+}
+
+__global__ void k_q_parts(ChunkArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c <= a.nch) a.jparts[c] = (uint32_t)((a.qoff[c + 1] - a.qoff[c] + kCTile - 1) / kCTile);
+}
+
+// last chunk c with qoff[c] <= p (qoff non-decreasing, qoff[0] = 0; also the
+// chunk of job p over jstart)
+__device__ __forceinline__ uint32_t chunk_of_pos(const uint64_t* qoff, uint32_t nch, uint64_t p) {
+  uint32_t lo = 0, hi = nch;  // chunks 0 .. nch
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (qoff[mid] <= p)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+// One job per kCTile grouped queries of one chunk: the chunk's sites,
+// their symbols and the chunk's radix index over them, and the symbols its PC
+// range can land in, into LDS.  Each query finds its call site through the
+// index (the delete, cover.go:299); a query at a call site takes the site's
+// symbol (cover.go:278-285), any other searches the held symbols.  First
+// query per symbol and last deleting query per site are LDS atomics, flushed
+// with one global atomic per touched symbol / site.
+template <bool kDirect>
+__global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
+  __shared__ uint64_t site[kSites];
+  __shared__ uint32_t ldel[kSites];
+  __shared__ uint16_t srel[kSites];  // site's symbol - the chunk's first held symbol (0xFFFF: none)
+  __shared__ uint16_t sidx[kSiteIdx + 1];
+  __shared__ uint64_t s_end[kSymCap], s_start[kSymCap];
+  __shared__ uint32_t fq[kSymCap];
+  // job: part `part` (kCTile queries) of chunk c
+  const uint32_t j = blockIdx.x;
+  if (j >= a.jstart[a.nch + 1]) return;
+  const uint32_t c = chunk_of_pos(a.jstart, a.nch, j);
+  {
+    const uint64_t p = a.qoff[c] + (uint64_t)(j - a.jstart[c]) * kCTile;
+    const uint64_t e = min<uint64_t>(a.qoff[c + 1], p + kCTile);
+    const uint64_t sbase = (uint64_t)c * kSites;
+    const uint32_t m = c < a.nch ? (uint32_t)min<uint64_t>(kSites, a.npcs - sbase) : 0u;
+    const uint2 sr = a.symr[c];
+    const uint32_t shi = sr.y < a.nsym ? sr.y : (uint32_t)a.nsym - 1;  // last symbol held
+    const uint32_t nsl = sr.x <= shi && sr.x < a.nsym ? shi - sr.x + 1 : 0u;
+    const bool sym_lds = nsl <= kSymCap;
+    const uint64_t s0 = m ? a.pcs[sbase] : 0;
+    const uint32_t ssh = m ? a.ssh[c] : 0;
+    for (uint32_t i = threadIdx.x; i < m; i += kCT) {
+      site[i] = a.pcs[sbase + i];
+      ldel[i] = 0;
+      const uint32_t y = a.ssym[sbase + i];
+      srel[i] = sym_lds && y < a.nsym ? (uint16_t)(y - sr.x) : (uint16_t)0xFFFF;
+    }
+    if (m)
+      for (uint32_t k = threadIdx.x; k <= kSiteIdx; k += kCT) sidx[k] = a.sidx[(uint64_t)c * (kSiteIdx + 1) + k];
+    if (sym_lds)
+      for (uint32_t i = threadIdx.x; i < nsl; i += kCT) {
+        s_end[i] = a.send[sr.x + i];
+        s_start[i] = a.sstart[sr.x + i];
+        fq[i] = 0xFFFFFFFFu;
+      }
+    __syncthreads();
+    for (uint64_t i = p + threadIdx.x; i < e; i += kCT) {
+      const uint2 g = kDirect ? make_uint2(a.cov[i], (uint32_t)i) : a.grouped[i];
+      const uint64_t pc = query_pc(a.hi32, g.x);
+      uint32_t j = 0;
+      bool exact = false;
+      if (m && pc >= s0) {
+        const uint64_t k = (pc - s0) >> ssh;
+        if (k < kSiteIdx) {  // (past the index: above the chunk's last site)
+          j = lds_lb(site, sidx[k], sidx[k + 1], pc);
+          exact = j < m && site[j] == pc;
+        }
+      }
+      bool hit;
+      if (sym_lds) {
+        uint32_t k;
+        if (exact) {
+          k = srel[j];
+        } else {
+          // upper_bound(send, pc) lies in [sr.x, sr.y]; within the held symbols
+          // it is sr.x + (held ends <= pc), and sr.y (maybe nsym) past them
+          k = 0;
+          for (uint32_t step = 1u << (31 - __builtin_clz(nsl | 1)); step; step >>= 1)
+            if (k + step <= nsl && s_end[k + step - 1] <= pc) k += step;
+        }
+        hit = k < nsl && pc >= s_start[k];  // (pc < end: pc <= end holds)
+        if (hit && fq[k] > g.y) atomicMin(&fq[k], g.y);
+      } else {
+        const uint64_t idx = exact ? a.ssym[sbase + j] : ub_idx(a.send, a.nsym, a.iend, pc);
+        hit = idx < a.nsym && pc >= a.sstart[idx] && pc <= a.send[idx];
+        if (hit && a.first_q[idx] > g.y) atomicMin(&a.first_q[idx], g.y);
+      }
+      if (hit && exact && ldel[j] < g.y + 1) atomicMax(&ldel[j], g.y + 1);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += kCT)
+      if (ldel[i]) atomicMax(&a.last_del[sbase + i], ldel[i]);
+    if (sym_lds)
+      for (uint32_t i = threadIdx.x; i < nsl; i += kCT)
+        if (fq[i] != 0xFFFFFFFFu) atomicMin(&a.first_q[sr.x + i], fq[i]);
+  }
+}
+
 __global__ void k_rep_group(RepArgs a) {
   uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.nsym) return;
@@ -276,8 +721,25 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   plan_idx(nsym, sym_end[0], sym_end[nsym - 1], iend);
   plan_idx(nall, all_pcs[0], all_pcs[nall - 1], ipcs);
   const size_t o_ie = p.add(((uint64_t)iend.nb + 1) * 4), o_ip = p.add(((uint64_t)ipcs.nb + 1) * 4);
+  // chunked query path (k_q_*) up to kMaxChunks chunks of call sites;
+  // SG_REPORT_DIRECT=1 forces the per-query search passes (k_rep_first / k_rep_del)
+  const char* direct_env = getenv("SG_REPORT_DIRECT");
+  const bool chunked = nall <= (uint64_t)kSites * kMaxChunks && !(direct_env && atoi(direct_env));
+  const uint32_t nch = div_up(nall, kSites);
+  // query tiles: 16K queries (8K staged) per count / scatter workgroup
+  const char* staged_env = getenv("SG_REPORT_STAGED");
+  const bool staged = !staged_env || atoi(staged_env);  // (SG_REPORT_STAGED=0: one store per query)
+  const uint32_t ntq = div_up(ncov, (uint64_t)kQT * (staged ? kSQPer : kQPer));
+  const uint32_t tw = 8 * div_up(ntq, 8);
+  const uint64_t ntc = chunked ? ((uint64_t)nch + 1) * tw : 1;
+  const size_t o_bnd = p.add((uint64_t)nch * 8), o_sr = p.add(((uint64_t)nch + 1) * 8),
+               o_qo = p.add(((uint64_t)nch + 2) * 8), o_gq = p.add(chunked ? ncov * 8 : 8),
+               o_ci = p.add(((uint64_t)kChunkIdx + 1) * 2), o_sh = p.add((uint64_t)nch * 4),
+               o_si = p.add((uint64_t)nch * (kSiteIdx + 1) * 2), o_sy = p.add(chunked ? nall * 4 : 4),
+               o_tc = p.add(ntc * 4), o_to = p.add((ntc + 1) * 8), o_jp = p.add(((uint64_t)nch + 1) * 4),
+               o_js = p.add(((uint64_t)nch + 2) * 8), o_srt = p.add(4);
   size_t scan_off = p.total;
-  rc = ws_reserve(ctx, p.total + scan_ws_bytes(nchunks));
+  rc = ws_reserve(ctx, p.total + std::max(scan_ws_bytes(nchunks), scan_ws_bytes(ntc)));
   if (rc) return rc;
   RepArgs a{};
   a.cov = (uint32_t*)ws_at(ctx, o_cov);
@@ -316,14 +778,106 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     hipLaunchKernelGGL(k_radix_index, dim3(div_up((uint64_t)ipcs.nb + 1, 256)), dim3(256), 0, ctx->stream, a.pcs,
                        (uint64_t)nall, ipcs.lo, ipcs.sh, ipcs.nb, (uint32_t*)ipcs.r);
   }
-  const dim3 qgrid((uint32_t)std::min<uint64_t>(div_up(ncov, 256), 16384));
-  {
-    ScopedTimer tm(ctx, "report_first");
-    hipLaunchKernelGGL(k_rep_first, qgrid, dim3(256), 0, ctx->stream, a);
-  }
-  {
-    ScopedTimer tm(ctx, "report_del");
-    hipLaunchKernelGGL(k_rep_del, qgrid, dim3(256), 0, ctx->stream, a);
+  if (chunked) {
+    ChunkArgs k{};
+    k.cov = a.cov;
+    k.ncov = ncov;
+    k.hi32 = (uint64_t)base << 32;
+    k.pcs = a.pcs;
+    k.npcs = nall;
+    k.sstart = a.sstart;
+    k.send = a.send;
+    k.nsym = nsym;
+    k.iend = iend;
+    k.nch = nch;
+    k.bnd = (uint64_t*)ws_at(ctx, o_bnd);
+    k.cidx = (uint16_t*)ws_at(ctx, o_ci);
+    k.ssh = (uint32_t*)ws_at(ctx, o_sh);
+    k.sidx = (uint16_t*)ws_at(ctx, o_si);
+    k.ssym = (uint32_t*)ws_at(ctx, o_sy);
+    {  // radix shift over [bnd[0], bnd[nch - 1]]
+      const uint64_t b0 = all_pcs[std::min<uint64_t>(kSites, nall) - 1], span = all_pcs[nall - 1] - b0;
+      uint32_t sh = 0;
+      while (sh < 63 && (span >> sh) >= kChunkIdx) sh++;
+      k.csh = sh;
+    }
+    k.symr = (uint2*)ws_at(ctx, o_sr);
+    k.ntiles = ntq;
+    k.tw = tw;
+    k.jparts = (uint32_t*)ws_at(ctx, o_jp);
+    k.jstart = (uint64_t*)ws_at(ctx, o_js);
+    k.tcount = (uint32_t*)ws_at(ctx, o_tc);
+    k.toff = (uint64_t*)ws_at(ctx, o_to);
+    k.qoff = (uint64_t*)ws_at(ctx, o_qo);
+    k.grouped = (uint2*)ws_at(ctx, o_gq);
+    k.first_q = a.first_q;
+    k.last_del = a.last_del;
+    // queries in PC order (the reference's canonical covers) need no regrouping
+    uint32_t* dsorted = (uint32_t*)ws_at(ctx, o_srt);
+    uint32_t unsorted = 1;
+    {
+      ScopedTimer tm(ctx, "report_sorted_q");
+      SG_HIP(hipMemsetAsync(dsorted, 0, 4, ctx->stream));
+      hipLaunchKernelGGL(k_q_sorted, dim3(std::min<uint32_t>(div_up(ncov, 256 * 16), 8192)), dim3(256), 0, ctx->stream,
+                         k, dsorted);
+      SG_HIP(hipMemcpyAsync(&unsorted, dsorted, 4, hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    if (!unsorted) {
+      ScopedTimer tm(ctx, "report_count_q");
+      hipLaunchKernelGGL(k_chunk_prep, dim3(div_up((uint64_t)nch + 1, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_site_sym, dim3(div_up(nall, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_site_index, dim3(div_up((uint64_t)nch * (kSiteIdx + 1), 256)), dim3(256), 0, ctx->stream,
+                         k);
+      hipLaunchKernelGGL(k_q_direct_off, dim3(div_up((uint64_t)nch + 2, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_q_parts, dim3(div_up((uint64_t)nch + 1, 256)), dim3(256), 0, ctx->stream, k);
+      rc = scan_counts(ctx, k.jparts, k.jstart, (uint64_t)nch + 1, scan_off);
+      if (rc) return rc;
+    }
+    if (unsorted) {
+      ScopedTimer tm(ctx, "report_count_q");
+      hipLaunchKernelGGL(k_chunk_prep, dim3(div_up((uint64_t)nch + 1, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_chunk_index, dim3(div_up((uint64_t)kChunkIdx + 1, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_site_sym, dim3(div_up(nall, 256)), dim3(256), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_site_index, dim3(div_up((uint64_t)nch * (kSiteIdx + 1), 256)), dim3(256), 0, ctx->stream,
+                         k);
+      if (tw != ntq) SG_HIP(hipMemsetAsync(k.tcount, 0, ntc * 4, ctx->stream));  // (the padding columns)
+      if (staged)
+        hipLaunchKernelGGL(k_q_count<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      else
+        hipLaunchKernelGGL(k_q_count<kQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      rc = scan_counts(ctx, k.tcount, k.toff, ntc, scan_off);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_q_chunk_off, dim3(div_up((uint64_t)nch + 2, 256)), dim3(256), 0, ctx->stream, k);
+      rc = scan_counts(ctx, k.jparts, k.jstart, (uint64_t)nch + 1, scan_off);
+      if (rc) return rc;
+    }
+    if (unsorted) {
+      ScopedTimer tm(ctx, "report_scatter_q");
+      if (staged)
+        hipLaunchKernelGGL((k_q_scatter<kSQPer, true>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      else
+        hipLaunchKernelGGL((k_q_scatter<kQPer, false>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+    }
+    {
+      ScopedTimer tm(ctx, "report_chunks");
+      // jobs: sum over chunks of ceil(count / kCTile) <= ncov / kCTile + nch + 1
+      const dim3 jgrid(div_up(ncov, kCTile) + nch + 1);
+      if (unsorted)
+        hipLaunchKernelGGL(k_q_chunk<false>, jgrid, dim3(kCT), 0, ctx->stream, k);
+      else
+        hipLaunchKernelGGL(k_q_chunk<true>, jgrid, dim3(kCT), 0, ctx->stream, k);
+    }
+  } else {
+    const dim3 qgrid((uint32_t)std::min<uint64_t>(div_up(ncov, 256), 16384));
+    {
+      ScopedTimer tm(ctx, "report_first");
+      hipLaunchKernelGGL(k_rep_first, qgrid, dim3(256), 0, ctx->stream, a);
+    }
+    {
+      ScopedTimer tm(ctx, "report_del");
+      hipLaunchKernelGGL(k_rep_del, qgrid, dim3(256), 0, ctx->stream, a);
+    }
   }
   {
     ScopedTimer tm(ctx, "report_sites");

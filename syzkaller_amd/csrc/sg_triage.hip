@@ -25,6 +25,7 @@
 #include "sg_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace sg {
@@ -363,6 +364,166 @@ __global__ void k_min_owners(const uint32_t* __restrict__ touched, const uint32_
         const uint32_t v = sgd::set_sig((uint32_t)((w4 * 4 + j) << 5) | (uint32_t)__builtin_ctz(m));
         flag[order[owner[v] - key_lo]] = 1;
       }
+  }
+}
+
+// Filtered claim for the later ranks.  The values of the first R inputs in
+// processing order (the longest ones, cover.go:157: they hold the corpus's
+// common values) are owned by ranks < R, so a later element of one of them can
+// never lower its owner: it is skipped without touching the owner table.  A
+// subset of those values -- an open-addressing set of kFilt slots, each value
+// at most kFiltProbe slots from its home (values that find no slot there are
+// simply left out) -- is loaded into each persistent workgroup's LDS once; the
+// elements of ranks >= R stream through in rank order (windows of the virtual
+// concatenation, taken by ticket) and only the ones the set does not hold
+// make the read-checked claim.  Exact for any subset the set holds.
+constexpr uint32_t kFilt = 16384, kFiltProbe = 8, kFiltEmpty = 0xFFFFFFFFu;
+// Phase A: the first R = kFiltRanks inputs in processing order, claimed one
+// workgroup per input.  The filter's values: those of input 0 that inputs 1 ..
+// R - 1 also hold -- the values common to the longest covers, i.e.
+// the corpus's most common ones (a value one long cover holds is as likely
+// rare).
+constexpr uint32_t kFiltRanks = 4;
+constexpr uint32_t kFirstSlots = 1u << 16;  // set of input 0's values (bounded probes: extras left out)
+constexpr int kFT = 1024;              // persistent claim workgroup
+constexpr uint32_t kFWin = 4 * kFT;    // elements per window
+__device__ __forceinline__ uint32_t filt_home(uint32_t v) { return (v * 0x9E3779B1u) >> 18; }  // 14 bits
+__device__ __forceinline__ uint32_t first_home(uint32_t v) { return (v * 0x85EBCA6Bu) >> 16; }  // 16 bits
+
+__device__ __forceinline__ void set_insert(uint32_t* tab, uint32_t mask, uint32_t h, uint32_t v, uint32_t probes) {
+  for (uint32_t d = 0; d < probes; d++) {
+    uint32_t* slot = &tab[(h + d) & mask];
+    const uint32_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == v) return;
+    if (cur == kFiltEmpty) {
+      const uint32_t old = atomicCAS(slot, kFiltEmpty, v);
+      if (old == kFiltEmpty || old == v) return;
+    }
+  }
+}
+
+// input 0's values into the first-values set
+__global__ __launch_bounds__(kBlock) void k_min_first(const uint32_t* __restrict__ vals,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ order, uint32_t* __restrict__ first) {
+  const uint64_t k = order[0];
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = off[k] + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < off[k + 1]; i += stride) {
+    const uint32_t v = vals[i];
+    if (v != kFiltEmpty) set_insert(first, kFirstSlots - 1, first_home(v), v, 16);  // (the empty marker: never filtered)
+  }
+}
+
+// values of inputs 1 .. R - 1 (phase A) that the first-values set holds into the filter
+__global__ __launch_bounds__(kBlock) void k_min_filter(const uint32_t* __restrict__ vals,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ first, uint32_t* __restrict__ filt) {
+  const uint64_t k = order[1 + blockIdx.y];
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = off[k] + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < off[k + 1]; i += stride) {
+    const uint32_t v = vals[i];
+    if (v == kFiltEmpty) continue;
+    const uint32_t h = first_home(v);
+    bool in = false;
+    for (uint32_t d = 0; d < 16; d++) {
+      const uint32_t c = first[(h + d) & (kFirstSlots - 1)];
+      if (c == v) in = true;
+      if (c == v || c == kFiltEmpty) break;
+    }
+    if (in) set_insert(filt, kFilt - 1, filt_home(v), v, kFiltProbe);
+  }
+}
+
+// phase B's geometry: lengths and starts of ranks R.. (in processing order)
+__global__ void k_min_ranks(const uint64_t* __restrict__ off, const uint32_t* __restrict__ order, uint64_t R,
+                            uint64_t nr, uint32_t* __restrict__ lens, uint64_t* __restrict__ soff) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nr) return;
+  const uint32_t k = order[R + j];
+  soff[j] = off[k];
+  lens[j] = (uint32_t)(off[k + 1] - off[k]);
+}
+
+// each window's first rank: last r with roff[r] <= w kFWin
+__global__ void k_min_wrank(const uint64_t* __restrict__ roff, uint64_t nr, uint64_t nwin,
+                            uint32_t* __restrict__ wrank) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwin) return;
+  const uint64_t p = w * kFWin;
+  uint64_t lo = 0, hi = nr - 1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (roff[mid] <= p)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  wrank[w] = (uint32_t)lo;
+}
+
+struct MinClaimF {
+  const uint32_t* vals;
+  const uint64_t* roff;   // [n - R + 1] element offsets of ranks R.. in the virtual concatenation
+  const uint64_t* soff;   // [n - R] where rank R + j's elements start in vals
+  uint64_t nr;            // ranks in this phase
+  uint64_t nel;           // their elements
+  uint32_t key0;          // key of rank R
+  uint32_t key_end;
+  uint32_t* owner;
+  uint32_t* touched;
+  const uint32_t* filt;
+  const uint32_t* wrank;  // [windows] rank (relative to R) holding each window's first element
+};
+
+__global__ __launch_bounds__(kFT) void k_min_claim_f(MinClaimF a) {
+  __shared__ uint32_t fs[kFilt];
+  for (uint32_t i = threadIdx.x; i < kFilt; i += kFT) fs[i] = a.filt[i];
+  __syncthreads();
+  const uint64_t nwin = (a.nel + kFWin - 1) / kFWin;
+  // windows blockIdx.x, + gridDim.x, ...: the grid sweeps them in rank order
+  constexpr int kE = kFWin / kFT;  // elements per thread per window, loads in flight together
+  for (uint64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
+    uint64_t r = a.wrank[w], rend = a.roff[r + 1];
+    int64_t base = (int64_t)a.soff[r] - (int64_t)a.roff[r];  // vals index = base + position
+    const uint64_t p0 = w * kFWin + threadIdx.x, p1 = min<uint64_t>((w + 1) * kFWin, a.nel);
+    uint32_t v[kE], rk[kE];
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const uint64_t p = p0 + (uint64_t)e * kFT;
+      rk[e] = 0xFFFFFFFFu;
+      if (p < p1) {
+        while (rend <= p) {
+          rend = a.roff[++r + 1];
+          base = (int64_t)a.soff[r] - (int64_t)a.roff[r];
+        }
+        v[e] = a.vals[base + (int64_t)p];
+        rk[e] = (uint32_t)r;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      if (rk[e] == 0xFFFFFFFFu) continue;
+      const uint32_t x = v[e];
+      bool held = false;
+      if (x != kFiltEmpty) {
+        const uint32_t h = filt_home(x);
+#pragma unroll
+        for (uint32_t d = 0; d < kFiltProbe; d++) {
+          const uint32_t c = fs[(h + d) & (kFilt - 1)];
+          if (c == x) held = true;
+          if (c == x || c == kFiltEmpty) break;
+        }
+      }
+      if (held) continue;
+      const uint32_t key = a.key0 + rk[e];
+      uint32_t* q = a.owner + x;
+      const uint32_t o = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (o > key) {
+        atomicMin(q, key);
+        if (o >= a.key_end) sgd::set_bit(a.touched, x);
+      }
+    }
   }
 }
 
@@ -809,9 +970,10 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   size_t o_in = p.add(nv * 4), o_off = p.add((n + 1) * 8), o_ord = p.add(n * 4),
          o_flag = p.add(n), o_fr = p.add(n), o_out = p.add(n * 4), o_m = p.add(((n + kTile - 1) / kTile) * kTile / 8),
          o_c = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 4), o_b = p.add(((n + kTile - 1) / kTile) * kChunksPerTile * 8 + 8),
-         o_t = p.add(kSetBytes);
+         o_t = p.add(kSetBytes), o_fs = p.add(kFilt * 4), o_ro = p.add((n + 1) * 8), o_so = p.add(n * 8),
+         o_tk = p.add((nv / kFWin + 2) * 4), o_ct = p.add(((size_t)kFirstSlots + n) * 4);
   size_t scan_off = p.total;
-  size_t scan_b2 = scan_ws_bytes(((n + kTile - 1) / kTile) * kChunksPerTile);
+  size_t scan_b2 = std::max(scan_ws_bytes(((n + kTile - 1) / kTile) * kChunksPerTile), scan_ws_bytes(n));
   rc = ws_reserve(ctx, p.total + scan_b2);
   if (rc) return rc;
   uint32_t* dtouch = (uint32_t*)ws_at(ctx, o_t);  // touched values (set layout)
@@ -831,12 +993,59 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   // the owner table: every element lowers its value's owner to its input's
   // rank key (covered starts empty, cover.go:130); the inputs owning some
   // value are the selected ones (cover.go:133-141)
+  // phase A: ranks < R (the first ~kFiltElems elements in processing order)
+  // claim one workgroup per input and fill the filter set; phase B: the rest
+  // through the persistent filtered claim (k_min_claim_f)
+  const char* filt_env = getenv("SG_MINIMIZE_FILTER");
+  const bool use_filt = !filt_env || atoi(filt_env);
+  // phase A: the first kFiltRanks inputs (SG_MINIMIZE_FILTER_RANKS: tests
+  // raise it past the filter's values' inputs)
+  const char* fr_env = getenv("SG_MINIMIZE_FILTER_RANKS");
+  const uint64_t R = use_filt && n > kFiltRanks ? std::min<uint64_t>(n - 1, std::max<uint64_t>(
+                                                       kFiltRanks, fr_env ? (uint64_t)atoll(fr_env) : 0))
+                                                 : n;
   {
     ScopedTimer tm(ctx, "min_claim");
     SG_HIP(hipMemsetAsync(dtouch, 0, kSetBytes, ctx->stream));
-    hipLaunchKernelGGL(k_min_claim, dim3((uint32_t)n), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
+    hipLaunchKernelGGL(k_min_claim, dim3((uint32_t)R), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
                        (const uint64_t*)doff, (const uint32_t*)dord, key_lo, (uint32_t)(key_lo + n), ctx->owner,
                        dtouch);
+    if (R < n) {
+      uint32_t* dfilt = (uint32_t*)ws_at(ctx, o_fs);
+      uint64_t* droff = (uint64_t*)ws_at(ctx, o_ro);
+      uint64_t* dsoff = (uint64_t*)ws_at(ctx, o_so);
+      uint32_t* dwr = (uint32_t*)ws_at(ctx, o_tk);
+      uint32_t* dfirst = (uint32_t*)ws_at(ctx, o_ct);
+      uint32_t* dlens = dfirst + kFirstSlots;
+      const uint64_t nr = n - R;
+      uint64_t nel = nv;
+      for (uint64_t r = 0; r < R; r++) nel -= off[order[r] + 1] - off[order[r]];
+      const uint64_t nwin = (nel + kFWin - 1) / kFWin;
+      hipLaunchKernelGGL(k_min_ranks, dim3(div_up(nr, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)doff,
+                         (const uint32_t*)dord, R, nr, dlens, dsoff);
+      rc = scan_counts(ctx, dlens, droff, nr, scan_off);
+      if (rc) return rc;
+      if (nwin)
+        hipLaunchKernelGGL(k_min_wrank, dim3(div_up(nwin, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)droff,
+                           nr, nwin, dwr);
+      SG_HIP(hipMemsetAsync(dfilt, 0xFF, kFilt * 4, ctx->stream));
+      SG_HIP(hipMemsetAsync(dfirst, 0xFF, kFirstSlots * 4, ctx->stream));
+      hipLaunchKernelGGL(k_min_first, dim3(16), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
+                         (const uint64_t*)doff, (const uint32_t*)dord, dfirst);
+      hipLaunchKernelGGL(k_min_filter, dim3(16, (uint32_t)R - 1), dim3(kBlock), 0, ctx->stream, (const uint32_t*)din,
+                         (const uint64_t*)doff, (const uint32_t*)dord, (const uint32_t*)dfirst, dfilt);
+      MinClaimF f{(const uint32_t*)din, droff, dsoff, nr, nel, (uint32_t)(key_lo + R), (uint32_t)(key_lo + n),
+                  ctx->owner, dtouch, dfilt, dwr};
+      if (nel) {
+      int per_cu = 0, cus = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_min_claim_f, kFT, 0) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+        cus = 256;
+      hipLaunchKernelGGL(k_min_claim_f, dim3((uint32_t)(per_cu * cus)), dim3(kFT), 0, ctx->stream, f);
+      }
+    }
   }
   {
     ScopedTimer tm(ctx, "min_owners");

@@ -191,6 +191,47 @@ def test_minimize_vs_oracle(C):
         assert np.array_equal(C.minimize_csr(rv, ro, order), O.minimize(rv, ro, order)), n
 
 
+def test_minimize_filtered_claim(C, monkeypatch):
+    """Minimize's filtered claim (sg_triage.hip k_min_claim_f): the values
+    common to the first inputs in processing order fill an LDS set, and later
+    elements found in it skip the owner table.  Phase A (the inputs claimed
+    one workgroup each) is the first 4 inputs, or more
+    (SG_MINIMIZE_FILTER_RANKS); Zipf values (most later elements held),
+    sentinels, empty inputs, inputs longer than a claim window, any
+    processing order, and the unfiltered path (SG_MINIMIZE_FILTER=0)."""
+    rng = np.random.default_rng(108)
+
+    def corpus(n, med, hi, s=1.1):
+        lens = np.clip(np.exp(rng.normal(np.log(med), 1.0, size=n)), 0, 20000).astype(np.int64)
+        lens[rng.integers(0, n, size=n // 20)] = 0
+        covs = []
+        for L in lens:
+            v = (np.minimum(rng.zipf(s, size=int(L)), hi) - 1).astype(np.uint64)
+            v = (0x81000000 + 16 * v).astype(np.uint32)
+            if rng.random() < 0.05 and L:
+                v[0] = SENT
+            covs.append(C.Canonicalize(v))
+        return C.to_csr(covs)
+
+    for n, med, hi, budget in [(3000, 40, 5000, "4"), (5000, 300, 1 << 20, "60"), (2500, 3000, 1 << 16, "1")]:
+        vals, off = corpus(n, med, hi)
+        monkeypatch.setenv("SG_MINIMIZE_FILTER_RANKS", budget)
+        order = C.minimize_order(off)
+        got = C.minimize_csr(vals, off, order)
+        monkeypatch.delenv("SG_MINIMIZE_FILTER_RANKS")
+        assert np.array_equal(got, O.minimize(vals, off, order)), (n, budget)
+        perm = rng.permutation(n).astype(np.uint32)
+        monkeypatch.setenv("SG_MINIMIZE_FILTER_RANKS", budget)
+        got = C.minimize_csr(vals, off, perm)
+        monkeypatch.delenv("SG_MINIMIZE_FILTER_RANKS")
+        assert np.array_equal(got, O.minimize(vals, off, perm)), (n, budget)
+    vals, off = corpus(12000, 200, 1 << 22)  # the default phase A
+    order = C.minimize_order(off)
+    assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order))
+    monkeypatch.setenv("SG_MINIMIZE_FILTER", "0")
+    assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order))
+
+
 # ---- signal sets (map replacements) --------------------------------------------
 def test_signal_set_ops(C):
     rng = np.random.default_rng(107)
@@ -643,6 +684,47 @@ def test_cover_uncovered_radix_edges(C):
     got = C.cover_uncovered(q, 0, s3, e3, p3)
     exp = O.cover_uncovered(q, 0, s3, e3, p3)
     assert np.array_equal(got, exp)
+
+
+def test_cover_uncovered_chunk_edges(C, monkeypatch):
+    """The chunked query path (sg_report.hip k_q_*): a chunk whose PC range
+    spans more symbols than it holds in LDS (many site-less symbols: global
+    symbol search), queries below the first and above the last call site,
+    site counts at and around the 4096-site chunk size; the same queries in
+    PC order (no regrouping), with one store per query (SG_REPORT_STAGED=0)
+    and through the direct per-query passes (SG_REPORT_DIRECT=1)."""
+    rng = np.random.default_rng(143)
+    hi32 = np.uint64(0xffffffff) << np.uint64(32)
+    base = np.uint64(0xffffffff81000000)
+    # 6000 adjacent 16-byte symbols, a call site in every 5th: chunk 0 spans all of them
+    starts = base + 16 * np.arange(6000, dtype=np.uint64)
+    ends = starts + np.uint64(16)
+    sites = starts[::5] + np.uint64(5)
+    cases = [(starts, ends, sites)]
+    for nsites in (4095, 4096, 4097, 8192 + 3):
+        s, e, p = _symtab(rng, 3 * nsites)
+        cases.append((s, e, p[:nsites]))
+    for starts, ends, sites in cases:
+        q = (rng.choice(sites, size=30000) + np.uint64(5) - hi32).astype(np.uint32)
+        lo = int(starts[0] + np.uint64(5) - hi32)
+        q = np.concatenate([q, rng.integers(0, 1 << 32, size=2000, dtype=np.uint64).astype(np.uint32),
+                            np.arange(lo - 40, lo + 40, dtype=np.uint32),
+                            (np.uint32(int(ends[-1] + np.uint64(5) - hi32)) + np.arange(20, dtype=np.uint32))])
+        exp = O.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        assert np.array_equal(got, exp), sites.size
+        # in PC order (a canonical cover, as html.go passes): no regrouping
+        qs = np.sort(q)
+        assert np.array_equal(C.cover_uncovered(qs, 0xffffffff, starts, ends, sites),
+                              O.cover_uncovered(qs, 0xffffffff, starts, ends, sites)), sites.size
+        monkeypatch.setenv("SG_REPORT_STAGED", "0")  # one store per query
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        monkeypatch.delenv("SG_REPORT_STAGED")
+        assert np.array_equal(got, exp), sites.size
+        monkeypatch.setenv("SG_REPORT_DIRECT", "1")
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        monkeypatch.delenv("SG_REPORT_DIRECT")
+        assert np.array_equal(got, exp), sites.size
 
 
 def test_cover_uncovered_partial_functions(C):
