@@ -457,11 +457,14 @@ __device__ __forceinline__ uint32_t trace_sig(uint32_t pc, uint32_t prev, bool s
 }
 
 // Pass-1 histogram of a trace batch: b2 counts of the tile's non-zero edges.
+// It also records which entries are kept (non-zero, not an in-tile repeat):
+// one ballot word per 64 tile positions (keep[t][p / 64], bit p % 64), which
+// the scatter reads instead of repeating the dedup.
 __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __restrict__ pcs,
                                                           const uint64_t* __restrict__ rec_off, uint64_t nrec,
                                                           const uint32_t* __restrict__ tstart,
                                                           const uint32_t* __restrict__ trec, uint32_t T,
-                                                          uint32_t* __restrict__ hist) {
+                                                          uint32_t* __restrict__ hist, uint64_t* __restrict__ keep) {
   __shared__ uint32_t rc[256 * 32];
   __shared__ uint32_t cs[kPT / 32];
   __shared__ unsigned long long dd[kTraceDedup];
@@ -498,10 +501,14 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
 #pragma unroll
   for (int k = 0; k < kS; k++) {
     const uint32_t p = k * kPThreads + tid;
+    bool kept = false;
     if ((live >> k) & 1u) {
       const unsigned long long v = dd[dedup_slot(x[k])];
-      if ((uint32_t)v != x[k] || (uint32_t)(v >> 32) == p) atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
+      kept = (uint32_t)v != x[k] || (uint32_t)(v >> 32) == p;
+      if (kept) atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
     }
+    const uint64_t b = __ballot(kept);  // positions k kPThreads + 64 (tid / 64) ..
+    if (lane == 0) keep[(uint64_t)t * (kPT / 64) + (p >> 6)] = b;
   }
   __syncthreads();
   if (tid < 256) {
@@ -637,6 +644,7 @@ struct P1Args {
   uint32_t* out;           // s << 8 | rec_in_tile
   uint8_t* top;            // out's top bytes (the pass-2 digits)
   unsigned long long* dbg; // diagnostics (k_p1_scatter<true>): cycles per phase, summed over blocks
+  const uint64_t* keep;    // trace batches: k_hist_trace's kept-entry words
 };
 
 // One tile.  Only the values and their records (four 8-bit records per
@@ -648,7 +656,7 @@ struct P1Args {
 // (see k_hist_trace) and zero edges skipped.
 template <bool kDbg, bool kTrace>
 __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32_t* cnt, uint32_t* gbase,
-                                        uint16_t* win, SegLds<uint8_t>& L, unsigned long long* dd, uint32_t t,
+                                        uint16_t* win, SegLds<uint8_t>& L, uint32_t t,
                                         uint32_t s0, uint32_t s1) {
   uint8_t* sidx = reinterpret_cast<uint8_t*>(stage);  // record-in-tile index; stage is free until the rank
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -686,8 +694,6 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
     cnt[d] = a.hist1[(uint64_t)d * a.T + t];
   }
   seg_clear(L, tid);
-  if (kTrace)
-    for (int i = tid; i < (int)kTraceDedup; i += kPThreads) dd[i] = ~0ull;
   __syncthreads();
   stamp(0);
   const uint32_t nt = s1 - s0;
@@ -707,18 +713,16 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
       const uint32_t prev = trace_prev(pc, carry);
       carry = (uint32_t)__builtin_amdgcn_readlane((int)pc, 63);
       sv[k] = trace_sig(pc, prev, start);
-      if (sv[k] == 0) vmask &= ~(1u << k);
-      if ((vmask >> k) & 1u) atomicMin(&dd[dedup_slot(sv[k])], ((unsigned long long)p << 32) | sv[k]);
       asm volatile("" : "+v"(sv[k]));  // one step at a time (registers)
     }
-    __syncthreads();
+    // kept entries (non-zero, not an in-tile repeat): the histogram's words,
+    // one per 64 positions -- wave w's step k is positions w kPerWave + 64 k ..
+    const uint64_t* kw = a.keep + (uint64_t)t * (kPT / 64) + __builtin_amdgcn_readfirstlane(w) * (kPerWave / 64);
 #pragma unroll
-    for (int k = 0; k < kSteps; k++)
-      if ((vmask >> k) & 1u) {  // a repeat of an earlier position of the tile
-        const uint32_t p = el0 + k * 64;
-        const unsigned long long v = dd[dedup_slot(sv[k])];
-        if ((uint32_t)v == sv[k] && (uint32_t)(v >> 32) != p) vmask &= ~(1u << k);
-      }
+    for (int k = 0; k < kSteps; k++) {
+      const uint64_t b = kw[k];
+      if (!((b >> lane) & 1ull)) vmask &= ~(1u << k);
+    }
   }
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
@@ -746,11 +750,10 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(8, 8)
   __shared__ uint32_t gbase[256];
   __shared__ uint16_t win[kRecCap + 1];  // tile-relative record starts, clamped to [0, kPT]
   __shared__ SegLds<uint8_t> L;
-  __shared__ unsigned long long dd[kTrace ? kTraceDedup : 1];
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t s0 = a.tstart[t], s1 = a.tstart[t + 1];
   if (s0 >= s1) return;
-  p1_tile<kDbg, kTrace>(a, stage, cnt, gbase, win, L, dd, t, s0, s1);
+  p1_tile<kDbg, kTrace>(a, stage, cnt, gbase, win, L, t, s0, s1);
 }
 
 // ---------------------------------------------------------------- pass 2 ---
@@ -1652,7 +1655,7 @@ struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, NG, ng, gmax;
   WsPlan p;
   size_t oTS, oTR, oGT, oH1, oO1, oV1, oB1, oNC, oCB, oCS, oCG, oCF, oCD, oDT, oBD, oGB, oH2, oO2, oV2, oSP, oTK, oBN, oBP,
-      oLB, oLQ, oSC;
+      oLB, oLQ, oSC, oKM;
   BucketPlan(uint64_t n_, uint64_t nrec_) : n(n_), nrec(nrec_) {
     nA = (n + kPT - 1) / kPT;
     nB = nrec ? (nrec - 1) / kRecCap : 0;
@@ -1686,10 +1689,11 @@ struct BucketPlan {
     oLB = p.add((uint64_t)kNumBuckets * 4);
     oLQ = p.add((uint64_t)kNumBuckets * 16);
     oSC = p.add(scan32_ws(256 * (gmax > T ? gmax : T)));
+    oKM = p.add(T * (kPT / 8));  // trace batches: kept-entry words
   }
   void rebase(size_t b) {
     for (size_t* o : {&oTS, &oTR, &oGT, &oH1, &oO1, &oV1, &oB1, &oNC, &oCB, &oCS, &oCG, &oCF, &oCD, &oDT, &oBD, &oGB, &oH2,
-                      &oO2, &oV2, &oSP, &oTK, &oBN, &oBP, &oLB, &oLQ, &oSC})
+                      &oO2, &oV2, &oSP, &oTK, &oBN, &oBP, &oLB, &oLQ, &oSC, &oKM})
       *o += b;
   }
 };
@@ -1773,7 +1777,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
     ScopedTimer tm(ctx, "p1_hist");
     if (trace)
       hipLaunchKernelGGL(k_hist_trace, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals, d_off, nrec,
-                         (const uint32_t*)tstart, (const uint32_t*)trec, T, hist1);
+                         (const uint32_t*)tstart, (const uint32_t*)trec, T, hist1, (uint64_t*)ws_at(ctx, bp.oKM));
     else if (((uintptr_t)d_vals & 15) == 0)
       hipLaunchKernelGGL(k_hist_rep<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
                          (const uint32_t*)tstart, (const uint4*)nullptr, T, (const uint32_t*)nullptr, hist1);
@@ -1783,7 +1787,7 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
-  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, b1, nullptr};
+  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, b1, nullptr, (const uint64_t*)ws_at(ctx, bp.oKM)};
   const bool dbg = ctx->debug_part;
   unsigned long long* p1dbg = nullptr;
   if (dbg) {
@@ -1880,7 +1884,14 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
     ba.nshards = emit->nshards;
     ba.shard_cnt = emit->shard_cnt;
   }
-  const uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, false>, kBThreads);
+  uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, false>, kBThreads);
+  // diagnostics: SG_BUCKET_BLOCKS caps the persistent grid (leaves CUs to
+  // kernels on other streams)
+  static const uint32_t cap_blocks = [] {
+    const char* e = getenv("SG_BUCKET_BLOCKS");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  if (cap_blocks && cap_blocks < bgrid) bgrid = cap_blocks;
   uint64_t* ddbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&ddbg, (size_t)bgrid * 88));
