@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
                                                           const uint32_t* __restrict__ trec, uint32_t T,
                                                           uint32_t* __restrict__ hist, uint64_t* __restrict__ keep) {
   __shared__ uint32_t rc[256 * 32];
-  __shared__ uint32_t cs[kPT / 32];
+  __shared__ alignas(16) uint32_t cs[kPT / 32];
   __shared__ unsigned long long dd[kTraceDedup];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t t = xcd_tile(blockIdx.x, T), s0 = tstart[t], s1 = tstart[t + 1];
@@ -498,17 +498,25 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
   }
   __syncthreads();
   const uint32_t cp = tid & 31;
+  uint32_t kmask = 0;  // kept steps of this thread (no cross-lane step in this loop)
 #pragma unroll
   for (int k = 0; k < kS; k++) {
     const uint32_t p = k * kPThreads + tid;
-    bool kept = false;
     if ((live >> k) & 1u) {
       const unsigned long long v = dd[dedup_slot(x[k])];
-      kept = (uint32_t)v != x[k] || (uint32_t)(v >> 32) == p;
-      if (kept) atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
+      if ((uint32_t)v != x[k] || (uint32_t)(v >> 32) == p) {
+        kmask |= 1u << k;
+        atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
+      }
     }
-    const uint64_t b = __ballot(kept);  // positions k kPThreads + 64 (tid / 64) ..
-    if (lane == 0) keep[(uint64_t)t * (kPT / 64) + (p >> 6)] = b;
+  }
+  // the kept words through LDS (cs: the call starts are no longer needed),
+  // then one coalesced 2 KiB store per tile
+  unsigned long long* kw = reinterpret_cast<unsigned long long*>(cs);
+#pragma unroll
+  for (int k = 0; k < kS; k++) {
+    const uint64_t b = __ballot((kmask >> k) & 1u);  // positions k kPThreads + 64 (tid / 64) ..
+    if (lane == 0) kw[(k * kPThreads + tid) >> 6] = b;
   }
   __syncthreads();
   if (tid < 256) {
@@ -516,6 +524,7 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
 #pragma unroll
     for (int k = 0; k < 32; k++) sum += rc[tid * 32 + ((k + tid) & 31)];
     hist[(uint64_t)tid * T + t] = sum;
+    keep[(uint64_t)t * (kPT / 64) + tid] = kw[tid];
   }
 }
 
