@@ -225,6 +225,12 @@ def test_minimize_filtered_claim(C, monkeypatch):
         got = C.minimize_csr(vals, off, perm)
         monkeypatch.delenv("SG_MINIMIZE_FILTER_RANKS")
         assert np.array_equal(got, O.minimize(vals, off, perm)), (n, budget)
+    # just past phase A: one or two inputs left, empty inputs, all-sentinel inputs
+    for covs in ([[1, 2, 3], [2, 3], [3], [3, 4], [4, 5]], [[7, 8], [], [8], [], [SENT], [8, 9], []],
+                 [[SENT], [SENT], [SENT], [SENT], [SENT, 1], [1]]):
+        v, o = C.to_csr([np.array(c, np.uint32) for c in covs])
+        for order in (C.minimize_order(o), np.arange(len(covs), dtype=np.uint32)[::-1].copy()):
+            assert np.array_equal(C.minimize_csr(v, o, order), O.minimize(v, o, order)), covs
     vals, off = corpus(12000, 200, 1 << 22)  # the default phase A
     order = C.minimize_order(off)
     assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order))
