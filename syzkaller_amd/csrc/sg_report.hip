@@ -191,7 +191,7 @@ constexpr int kQT = 1024;                // threads of the count / scatter kerne
 constexpr int kQPer = 16;                // queries per thread there (kSQPer when staged)
 constexpr int kSQPer = 8;
 constexpr int kCT = 512;                 // threads of the chunk kernel
-constexpr uint32_t kCTile = 16384;       // grouped queries per chunk-kernel tile
+constexpr uint32_t kCTile = 32768;       // grouped queries per chunk-kernel tile
 
 struct ChunkArgs {
   const uint32_t* cov;
@@ -565,11 +565,12 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
         fq[i] = 0xFFFFFFFFu;
       }
     __syncthreads();
-    for (uint64_t i = p + threadIdx.x; i < e; i += kCT) {
-      const uint2 g = kDirect ? make_uint2(a.cov[i], (uint32_t)i) : a.grouped[i];
-      const uint64_t pc = query_pc(a.hi32, g.x);
-      uint32_t j = 0;
-      bool exact = false;
+    // a query's call site (exact: pc is site j) and symbol (hit: pc inside
+    // symbol sym -- an index into the held symbols, or a global index when
+    // they are not held)
+    auto lookup = [&](uint64_t pc, uint32_t& j, bool& exact, bool& hit, uint64_t& sym) {
+      j = 0;
+      exact = false;
       if (m && pc >= s0) {
         const uint64_t k = (pc - s0) >> ssh;
         if (k < kSiteIdx) {  // (past the index: above the chunk's last site)
@@ -577,7 +578,6 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
           exact = j < m && site[j] == pc;
         }
       }
-      bool hit;
       if (sym_lds) {
         uint32_t k;
         if (exact) {
@@ -590,13 +590,71 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
             if (k + step <= nsl && s_end[k + step - 1] <= pc) k += step;
         }
         hit = k < nsl && pc >= s_start[k];  // (pc < end: pc <= end holds)
-        if (hit && fq[k] > g.y) atomicMin(&fq[k], g.y);
+        sym = k;
       } else {
         const uint64_t idx = exact ? a.ssym[sbase + j] : ub_idx(a.send, a.nsym, a.iend, pc);
         hit = idx < a.nsym && pc >= a.sstart[idx] && pc <= a.send[idx];
-        if (hit && a.first_q[idx] > g.y) atomicMin(&a.first_q[idx], g.y);
+        sym = idx;
       }
-      if (hit && exact && ldel[j] < g.y + 1) atomicMax(&ldel[j], g.y + 1);
+    };
+    auto first_query = [&](uint64_t sym, uint32_t qi) {
+      if (sym_lds) {
+        if (fq[sym] > qi) atomicMin(&fq[sym], qi);
+      } else if (a.first_q[sym] > qi) {
+        atomicMin(&a.first_q[sym], qi);
+      }
+    };
+    if (!kDirect) {
+      for (uint64_t i = p + threadIdx.x; i < e; i += kCT) {
+        const uint2 g = a.grouped[i];
+        uint32_t j;
+        bool exact, hit;
+        uint64_t sym;
+        lookup(query_pc(a.hi32, g.x), j, exact, hit, sym);
+        if (hit) first_query(sym, g.y);
+        if (hit && exact && ldel[j] < g.y + 1) atomicMax(&ldel[j], g.y + 1);
+      }
+    } else {
+      // Queries in PC order: each thread takes a contiguous run, so a PC
+      // repeated by the next query reuses its lookup, a symbol's first query
+      // in the run is its only minimum candidate (symbols are non-decreasing
+      // in PC), and a site's last deleting query in the run is flushed once,
+      // when the PC moves on.
+      const uint64_t per = (e - p + kCT - 1) / kCT;
+      const uint64_t b0 = min<uint64_t>(p + threadIdx.x * per, e), b1 = min<uint64_t>(b0 + per, e);
+      uint64_t prev = 0, psym = ~0ull;
+      bool have = false, pdel = false;
+      uint32_t pj = 0, pmax = 0;
+      for (uint64_t i0 = b0; i0 < b1; i0 += 4) {
+        uint32_t cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) cv[u] = i0 + u < b1 ? a.cov[i0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (i0 + u >= b1) break;
+          const uint32_t qi = (uint32_t)(i0 + u);
+          const uint64_t pc = query_pc(a.hi32, cv[u]);
+          if (have && pc == prev) {
+            pmax = qi + 1;
+            continue;
+          }
+          if (pdel && ldel[pj] < pmax) atomicMax(&ldel[pj], pmax);
+          uint32_t j;
+          bool exact, hit;
+          uint64_t sym;
+          lookup(pc, j, exact, hit, sym);
+          if (hit && sym != psym) {
+            first_query(sym, qi);
+            psym = sym;
+          }
+          have = true;
+          prev = pc;
+          pdel = hit && exact;
+          pj = j;
+          pmax = qi + 1;
+        }
+      }
+      if (pdel && ldel[pj] < pmax) atomicMax(&ldel[pj], pmax);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < m; i += kCT)
