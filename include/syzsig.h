@@ -199,22 +199,27 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
 int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
 			    uint32_t* d_total);
 /* The two halves of sg_triage_batch_dev (flags and set updates, no diff) for
- * the prefix protocol.  Begin: the batch's partitions are built once and
- * kept in the context's slot (0 or 1: two batches can be kept, so one batch's
- * exchange runs while the next is partitioned), and marks |= every signal of
- * the batch not in base (the local new signal, fuzzer.go:666).  End: the sequential loop
- * (fuzzer.go:645-693) over the kept batch against maxsig | d_prefix (d_prefix:
- * nullable, 2^27 words in the set layout, e.g. another set's or an exchanged
- * bitmap), writing the flags of its nrec records to d_rec_new.  maxsig gains
- * the batch's new signal, and the words that gain bits also gain their
- * d_prefix bits (the prefix protocol ORs a superset of d_prefix into maxsig
- * afterwards); newsig (nullable) gains the new signal.  Only begin's launches
- * read the batch's buffers; other calls may run on the context between begin
- * and end (the slots have workspaces of their own).  End closes the slot. */
+ * the prefix protocol.  Begin: marks |= every signal of the batch not in base
+ * (the local new signal, fuzzer.go:666; base != marks), and each such signal's
+ * first record in the batch is kept in the context's slot (0 or 1: two batches
+ * can be kept, so one batch's exchange runs while the next is begun).  End: the
+ * sequential loop's flags (fuzzer.go:645-693) of the batch's nrec records
+ * against maxsig | d_prefix (d_prefix: nullable, 2^27 words in the set layout,
+ * e.g. another set's or an exchanged bitmap), written to d_rec_new; maxsig must
+ * contain begin's base.  End's set updates: newsig (nullable) gains the new
+ * signal (marks minus maxsig | d_prefix), and maxsig |= marks -- its new signal
+ * and bits of d_prefix (the prefix protocol ORs a superset of d_prefix into
+ * maxsig afterwards).  Flags: end without the set updates (maxsig is only
+ * read).  Marks must stay unchanged until end; only begin's launches read the
+ * batch's buffers, and other calls may run on the context between begin and
+ * end/flags (the slots have workspaces of their own).  End and flags close
+ * the slot. */
 int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks, const uint32_t* d_vals,
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec);
 int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
 		      uint8_t* d_rec_new);
+int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, const sg_set* maxsig, const uint32_t* d_prefix,
+			uint8_t* d_rec_new);
 
 /* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:
  * diff = SignalDiff(maxSignal, S_k); corpusSignal ∪= diff; maxSignal ∪= diff. */

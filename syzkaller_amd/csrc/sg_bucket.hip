@@ -870,14 +870,15 @@ struct BucketArgs {
   const uint4* blist_q;    // ... and their descriptors
   const uint32_t* nlist;   // device: their number
   uint64_t* dbg;           // diagnostics (k_bucket<true>): per block {start, end, buckets, rounds, 4 phase cycle sums}
-  // candidate emission (sharded triage, sg_shard.hip): instead of flagging
-  // records and setting bits, every distinct candidate s of the batch is
-  // written once, with its first record, as {s, rec_base + record}
+  // candidate emission (sharded triage, sg_shard.hip; the prefix protocol's
+  // begin): instead of flagging records and updating maxSignal, every
+  // distinct candidate s of the batch is written once, with its first
+  // record, as {s, rec_base + record}, and set in nwords when that is given
   uint2* pairs;
   unsigned long long* npairs;
   uint32_t rec_base;
-  uint32_t nshards;         // pairs are counted per owning shard (shard_of)
-  unsigned long long* shard_cnt;
+  uint32_t nshards;         // pairs are counted per owning shard (shard_of) ...
+  unsigned long long* shard_cnt;  // ... when this is given
 };
 
 // Owning shard of a signal in the hash-sharded multi-GPU triage: the murmur3
@@ -930,14 +931,15 @@ __device__ __forceinline__ void emit_pairs(const BucketArgs& a, const uint32_t (
   for (int k = 0; k < kPer; k++)
     if (rec[k] != kNone) {
       a.pairs[pos++] = make_uint2(sig[k], a.rec_base + rec[k]);
-      atomicAdd(&shcnt[shard_of(sig[k], a.nshards)], 1u);
+      if (a.shard_cnt) atomicAdd(&shcnt[shard_of(sig[k], a.nshards)], 1u);
     }
   __syncthreads();  // ewc / ebase are rewritten by the next call
 }
 
 __device__ __forceinline__ void flush_shard_counts(const BucketArgs& a, const uint32_t* shcnt) {
-  for (uint32_t i = threadIdx.x; i < a.nshards; i += blockDim.x)
-    if (shcnt[i]) atomicAdd(&a.shard_cnt[i], (unsigned long long)shcnt[i]);
+  if (a.shard_cnt)
+    for (uint32_t i = threadIdx.x; i < a.nshards; i += blockDim.x)
+      if (shcnt[i]) atomicAdd(&a.shard_cnt[i], (unsigned long long)shcnt[i]);
 }
 
 // non-empty flag per bucket (scanned into list positions)
@@ -1368,11 +1370,20 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
         for (int k = 0; k < kPer; k++) {
           const uint32_t i = (half * kPer + k) * kBThreads + tid;
           const uint32_t v = ht[i];
-          sig[k] = part_sig((b << 16) | map_signal(i, v));
+          const uint32_t sl = map_signal(i, v);
+          sig[k] = part_sig((b << 16) | sl);
           rec[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
           ht[i] = kEmpty;
+          if (a.nwords && v != kEmpty) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
         }
-        emit_pairs(a, sig, rec, shcnt);
+        emit_pairs(a, sig, rec, shcnt);  // (ends with a barrier)
+      }
+      if (a.nwords) {  // the candidates' bits: words kWPT tid .., written by this block alone
+        const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
+        uint32_t* ng = a.nwords + bucket_word(b, kWPT * tid);
+#pragma unroll
+        for (int j = 0; j < kWPT; j++)
+          if (nb[j]) ng[j] = ns[j] | nb[j];
       }
       reinterpret_cast<wvec*>(nbits)[tid] = wvec{};
     } else {
@@ -1499,6 +1510,9 @@ __global__ __launch_bounds__(kDThreads) void k_bucket_direct(BucketArgs a) {
         rec[k] = owner[i];
       }
       emit_pairs(a, sig, rec, shcnt);
+      if (a.nwords)
+        for (uint32_t i = tid; i < kQW; i += kDThreads)
+          if (nbits[i]) a.nwords[bucket_word(b, qq * kQW + i)] |= nbits[i];
     } else {
       for (uint32_t i = tid; i < kQ; i += kDThreads)
         if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
@@ -2172,10 +2186,20 @@ static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std:
   return SG_OK;
 }
 
-// Two-phase triage (the prefix protocol, syzkaller_amd/shard.py): begin
-// partitions every record slice of the batch once, keeping the partitions in
-// the workspace, and marks the batch's signal that is not in `base`; end runs
-// the bucket stage of each kept slice in order against the caller's maxSignal.
+// Two-phase triage (the prefix protocol, syzkaller_amd/shard.py).  Begin runs
+// the bucket stage of each record slice against base in emitting form: the
+// batch's signal not in base is set in marks, and each such s is kept once,
+// with its first record, as a pair in the slot's workspace.  Slice j is
+// tested against base | marks, so a signal of an earlier slice is not
+// re-emitted by a later one: the pairs are the first owners over the whole
+// batch.  End: record r is queued iff it owns a pair whose s is in neither
+// maxSignal nor the prefix (k_prefix_flags).  That is the sequential loop
+// against M = maxsig | prefix for any M containing base: every s of the batch
+// outside M is outside base, so its pair is kept, and its first owner is the
+// loop's (a record is queued iff it is the first to hold some s outside M).
+// SG_PREFIX_KEEP=1 selects the earlier form, kept for measurement: begin
+// keeps the partitions and marks the buckets (k_bucket_mark), end runs the
+// bucket stage against maxsig | prefix.
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // The slot's workspace stands in for the context's during one call (the
@@ -2212,6 +2236,53 @@ static int slot_reserve(sg_ctx* ctx, PrefixSlot& s, size_t bytes) {
   return SG_OK;
 }
 
+// flags of the kept pairs {s, record}: one pair per thread and step, coalesced;
+// a bucket's pairs are adjacent, so their bitmap words share cache lines
+constexpr int kFixT = 256;
+__global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict__ pairs,
+                                                        const unsigned long long* __restrict__ npairs,
+                                                        const uint32_t* __restrict__ mwords,
+                                                        const uint32_t* __restrict__ owords, uint8_t* __restrict__ rec_new) {
+  const uint64_t n = *npairs, stride = (uint64_t)gridDim.x * kFixT;
+  for (uint64_t i = (uint64_t)blockIdx.x * kFixT + threadIdx.x; i < n; i += stride) {
+    const uint2 p = pairs[i];
+    const uint32_t t = sgd::set_pos(p.x);
+    uint32_t w = mwords[t >> 5];
+    if (owords) w |= owords[t >> 5];
+    if (!((w >> (t & 31)) & 1u)) rec_new[p.y] = 1;
+  }
+}
+
+// end's set updates: newsig |= marks & ~(maxsig | prefix), maxsig |= marks
+__global__ void k_prefix_merge(const uint32_t* __restrict__ marks, uint32_t* __restrict__ mwords,
+                               const uint32_t* __restrict__ owords, uint32_t* __restrict__ nwords) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < kSetWords / 4; w += stride) {
+    const uint4 c = reinterpret_cast<const uint4*>(marks)[w];
+    if (!(c.x | c.y | c.z | c.w)) continue;
+    uint4 m = reinterpret_cast<uint4*>(mwords)[w];
+    if (nwords) {
+      uint4 o = owords ? reinterpret_cast<const uint4*>(owords)[w] : make_uint4(0, 0, 0, 0);
+      uint4 nw = reinterpret_cast<uint4*>(nwords)[w];
+      nw.x |= c.x & ~(m.x | o.x);
+      nw.y |= c.y & ~(m.y | o.y);
+      nw.z |= c.z & ~(m.z | o.z);
+      nw.w |= c.w & ~(m.w | o.w);
+      reinterpret_cast<uint4*>(nwords)[w] = nw;
+    }
+    m.x |= c.x;
+    m.y |= c.y;
+    m.z |= c.z;
+    m.w |= c.w;
+    reinterpret_cast<uint4*>(mwords)[w] = m;
+  }
+}
+
+static bool prefix_keep_mode() {  // read at each begin (tests switch it)
+  const char* e = getenv("SG_PREFIX_KEEP");
+  return e && atoi(e) != 0;
+}
+
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec) {
   if (slot >= kPrefixSlots) {
@@ -2225,9 +2296,44 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
   PrefixSlot& S = ctx->prefix[slot];
   S.slices.clear();
   S.open = false;
+  S.keep = prefix_keep_mode();
+  S.marks = marks_words;
+  S.n = n;
   std::vector<RecSlice> sl;
   int rc = nrec ? record_slices(ctx, d_off, nrec, sl) : SG_OK;
   if (rc) return rc;
+  if (!S.keep) {
+    // the pairs: a counter, then <= n pairs
+    rc = slot_reserve(ctx, S, 256 + n * 8);
+    if (rc) return rc;
+    unsigned long long* np = (unsigned long long*)S.ws;
+    uint2* pairs = (uint2*)((char*)S.ws + 256);
+    SG_HIP(hipMemsetAsync(np, 0, 8, ctx->stream));
+    size_t need = 0;
+    for (const RecSlice& x : sl)
+      if (x.e1 > x.e0)
+        need = std::max(need, align256(bucket_plan_bytes(x.e1 - x.e0, x.r1 - x.r0)) + align256((x.r1 - x.r0 + 1) * 8));
+    if (need) {
+      rc = ws_reserve(ctx, need);
+      if (rc) return rc;
+    }
+    for (const RecSlice& x : sl) {
+      if (x.e1 == x.e0) continue;
+      const uint64_t ns = x.e1 - x.e0, nr = x.r1 - x.r0;
+      BucketPlan bp(ns, nr);
+      uint64_t* roff = (uint64_t*)ws_at(ctx, align256(bucket_plan_bytes(ns, nr)));
+      hipLaunchKernelGGL(k_rebase, dim3(div_up(nr + 1, 256)), dim3(256), 0, ctx->stream, d_off + x.r0, nr + 1, x.e0,
+                         roff);
+      rc = partition_one(ctx, d_vals + x.e0, roff, ns, nr, 0, true, bp);
+      if (rc) return rc;
+      const EmitArgs e{pairs, np, (uint32_t)x.r0, 1, nullptr};
+      rc = buckets_one(ctx, bp, const_cast<uint32_t*>(base_words), marks_words, nullptr, &e, ns, nr, marks_words);
+      if (rc) return rc;
+    }
+    S.nrec = nrec;
+    S.open = true;
+    return SG_OK;
+  }
   size_t total = 0;
   for (const RecSlice& x : sl)
     if (x.e1 > x.e0) total += align256(bucket_plan_bytes(x.e1 - x.e0, x.r1 - x.r0)) + align256((x.r1 - x.r0 + 1) * 8);
@@ -2263,7 +2369,7 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
 }
 
 int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords,
-               uint8_t* d_rec_new) {
+               uint8_t* d_rec_new, bool update) {
   if (slot >= kPrefixSlots || !ctx->prefix[slot].open) {
     set_error("prefix triage: no batch begun in slot %u", slot);
     return SG_EINVAL;
@@ -2271,6 +2377,20 @@ int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owo
   PrefixSlot& S = ctx->prefix[slot];
   S.open = false;
   if (S.nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, S.nrec, ctx->stream));
+  if (!S.keep) {
+    if (S.n) {
+      ScopedTimer tm(ctx, "prefix_flags");
+      hipLaunchKernelGGL(k_prefix_flags, dim3((uint32_t)std::min<uint64_t>(div_up(S.n, kFixT), 8192)), dim3(kFixT), 0,
+                         ctx->stream, (const uint2*)((char*)S.ws + 256), (const unsigned long long*)S.ws, mwords,
+                         owords, d_rec_new);
+    }
+    if (update && S.n) {
+      ScopedTimer tm(ctx, "prefix_merge");
+      hipLaunchKernelGGL(k_prefix_merge, dim3(8192), dim3(256), 0, ctx->stream, S.marks, mwords, owords, nwords);
+    }
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+  }
   SlotWs guard(ctx, S);
   for (const PrefixSlice& x : S.slices) {
     if (x.e1 == x.e0) continue;

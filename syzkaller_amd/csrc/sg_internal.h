@@ -60,12 +60,16 @@ struct PrefixSlice {
   size_t ws_base;
 };
 
-// One kept batch of the two-phase triage: its record slices and their
-// partitions, in a workspace of its own (two slots, so one batch's exchange
-// can run while the next one is partitioned)
+// One kept batch of the two-phase triage: its first-owner pairs (or, with
+// SG_PREFIX_KEEP, its record slices and their partitions), in a workspace of
+// its own (two slots, so one batch's exchange can run while the next one is
+// partitioned)
 struct PrefixSlot {
   std::vector<PrefixSlice> slices;
   uint64_t nrec = 0;
+  uint64_t n = 0;              // signal entries of the batch (bounds the pairs)
+  uint32_t* marks = nullptr;   // begin's marks (end's set updates)
+  bool keep = false;           // partitions kept instead of pairs
   bool open = false;
   void* ws = nullptr;
   size_t ws_cap = 0;
@@ -200,13 +204,14 @@ struct EmitArgs {
 };
 // Workspace bytes of one partitioned launch over n entries / nrec records.
 size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
-// Two-phase triage (sg_bucket.hip): begin partitions the batch (kept in the
-// workspace) and ORs into marks_words its signal not in base_words; end
-// triages the kept partitions against mwords (flags, mwords / nwords updated).
-// Between the two only set operations may run on the context.
+// Two-phase triage (sg_bucket.hip): begin ORs into marks_words the batch's
+// signal not in base_words and keeps each such signal's first record in the
+// slot; end flags the records against mwords | owords and, with `update`,
+// ORs the marks into mwords (nwords gaining what mwords | owords lacked).
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec);
-int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new);
+int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new,
+               bool update);
 // One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch
 // at ws_base (reserved by the caller).
 int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,

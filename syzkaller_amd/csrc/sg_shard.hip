@@ -396,7 +396,8 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
 
 int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks, const uint32_t* d_vals,
                         const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec) {
-  if (!ctx || !base || !marks || base->ctx != ctx || marks->ctx != ctx || !d_rec_off || (nvals && !d_vals)) {
+  if (!ctx || !base || !marks || base == marks || base->ctx != ctx || marks->ctx != ctx || !d_rec_off ||
+      (nvals && !d_vals)) {
     set_error("sg_prefix_begin_dev: invalid argument");
     return SG_EINVAL;
   }
@@ -419,7 +420,23 @@ int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t
     set_error("sg_prefix_end_dev: no flag buffer");
     return SG_EINVAL;
   }
-  return prefix_end(ctx, slot, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new);
+  return prefix_end(ctx, slot, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new, true);
+}
+
+int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, const sg_set* maxsig, const uint32_t* d_prefix,
+                        uint8_t* d_rec_new) {
+  if (!ctx || !maxsig || maxsig->ctx != ctx) {
+    set_error("sg_prefix_flags_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  if (slot < kPrefixSlots && ctx->prefix[slot].nrec && !d_rec_new) {
+    set_error("sg_prefix_flags_dev: no flag buffer");
+    return SG_EINVAL;
+  }
+  return prefix_end(ctx, slot, maxsig->words, d_prefix, nullptr, d_rec_new, false);
 }
 
 int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {

@@ -1,7 +1,7 @@
 """The bitmap-prefix one-batch triage protocol (syzkaller_amd/shard.py
 PrefixTriage) on CPU: world size 2 and 4 over gloo, with the stages restated
 in numpy from their contracts (sg_triage_batch_dev, sg_prefix_begin_dev /
-sg_prefix_end_dev, sg_set_clear / or_dev, sg_bitmap_prefix_or_dev) over
+sg_prefix_end_dev / sg_prefix_flags_dev, sg_set_clear / or_dev, sg_bitmap_prefix_or_dev) over
 a 2^20-signal bitmap (the protocol is word-wise, so a smaller signal space
 exercises it fully; the full 2^32 space runs on the GPU in
 tests/test_shard_gpu.py).  The flags of every record and the final
@@ -77,17 +77,22 @@ class NumpyPrefixStages:
         v = vals[:nvals].numpy().view(np.uint32)
         if v.size:
             marks.add(v[~base.has(v)])
-        self.kept[slot] = (vals, off, nvals, nrec)
+        self.kept[slot] = (vals, off, nvals, nrec, marks)
+
+    def prefix_flags(self, maxset, prefix, rec_new, slot=0):
+        """The loop's flags against maxset | prefix (include/syzsig.h)."""
+        vals, off, nvals, nrec, _ = self.kept.pop(slot)
+        start = maxset.w | (prefix.numpy().view(np.uint32)[:WORDS] if prefix is not None else 0)
+        self.triage(BitSet(start.copy()), None, vals, off, nvals, nrec, rec_new)
 
     def prefix_end(self, maxset, prefix, newset, rec_new, slot=0):
-        """Against maxset | prefix; maxset gains the new signal, and the words
-        that gain bits also gain their prefix bits (include/syzsig.h)."""
-        vals, off, nvals, nrec = self.kept.pop(slot)
-        start = maxset.w | (prefix.numpy().view(np.uint32)[:WORDS] if prefix is not None else 0)
-        work = BitSet(start.copy())
-        self.triage(work, newset, vals, off, nvals, nrec, rec_new)
-        gained = work.w != start
-        maxset.w[gained] = work.w[gained]
+        """The flags; newset gains marks minus maxset | prefix, maxset |= marks."""
+        marks = self.kept[slot][4]
+        pre = prefix.numpy().view(np.uint32)[:WORDS] if prefix is not None else 0
+        if newset is not None:
+            newset.w |= marks.w & ~(maxset.w | pre)
+        self.prefix_flags(maxset, prefix, rec_new, slot)
+        maxset.w |= marks.w
 
     def triage(self, maxset, newset, vals, off, nvals, nrec, rec_new):
         """The sequential loop (fuzzer.go:665-690) restated over bitmaps."""
