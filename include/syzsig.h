@@ -199,10 +199,11 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
 int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
 			    uint32_t* d_total);
 /* The two halves of sg_triage_batch_dev (flags and set updates, no diff) for
- * the prefix protocol.  Begin: marks |= every signal of the batch not in base
- * (the local new signal, fuzzer.go:666; base != marks), and each such signal's
- * first record in the batch is kept in the context's slot (0 or 1: two batches
- * can be kept, so one batch's exchange runs while the next is begun).  End: the
+ * the prefix protocol.  Begin: marks (empty at begin; base != marks) gets every
+ * signal of the batch not in base (the local new signal, fuzzer.go:666), and
+ * each such signal's first record in the batch is kept in the context's slot
+ * (0 or 1: two batches can be kept, so one batch's exchange runs while the
+ * next is begun).  End: the
  * sequential loop's flags (fuzzer.go:645-693) of the batch's nrec records
  * against maxsig | d_prefix (d_prefix: nullable, 2^27 words in the set layout,
  * e.g. another set's or an exchanged bitmap), written to d_rec_new; maxsig must

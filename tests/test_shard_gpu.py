@@ -153,6 +153,7 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, keep):
         ms2 = C.SignalSet(ctx2)
         C.SignalAdd(ms2, m0 if as_prefix else np.union1d(m0, extra))
         rec2 = torch.full((nrec,), 7, dtype=torch.uint8, device="cuda")
+        st.clear(marks)  # (begin's marks start empty: include/syzsig.h)
         st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=0)
         st.prefix_flags(ms2, _Words(pre) if as_prefix else None, rec2, slot=0)
         torch.cuda.synchronize()
