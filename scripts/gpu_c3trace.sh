@@ -1,0 +1,10 @@
+#!/bin/bash
+# C3 two-phase step at one rank under a kernel trace (both prefix forms).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=${TAG:-c3t}
+for K in 0 1; do
+SG_PREFIX_KEEP=$K timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c3trace_${T}_$K -o run -- python3 -u bench.py --mode c3 --c3-two-phase --steps 2 --warmup 1 > gpurun_out/c3trace_${T}_$K.log 2>&1
+rc=$?; echo "keep=$K rc=$rc"; tail -1 gpurun_out/c3trace_${T}_$K.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+done
