@@ -2236,20 +2236,38 @@ static int slot_reserve(sg_ctx* ctx, PrefixSlot& s, size_t bytes) {
   return SG_OK;
 }
 
-// flags of the kept pairs {s, record}: one pair per thread and step, coalesced;
-// a bucket's pairs are adjacent, so their bitmap words share cache lines
-constexpr int kFixT = 256;
+// flags of the kept pairs {s, record}: kFixU pairs per thread in flight (the
+// pair read, the bitmap read it selects and the flag store are a dependent
+// chain; one pair per thread and step measured 7.2 ms per C3 slice); a
+// bucket's pairs are adjacent, so their bitmap words share cache lines
+constexpr int kFixT = 256, kFixU = 8;
 __global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict__ pairs,
                                                         const unsigned long long* __restrict__ npairs,
                                                         const uint32_t* __restrict__ mwords,
                                                         const uint32_t* __restrict__ owords, uint8_t* __restrict__ rec_new) {
-  const uint64_t n = *npairs, stride = (uint64_t)gridDim.x * kFixT;
-  for (uint64_t i = (uint64_t)blockIdx.x * kFixT + threadIdx.x; i < n; i += stride) {
-    const uint2 p = pairs[i];
-    const uint32_t t = sgd::set_pos(p.x);
-    uint32_t w = mwords[t >> 5];
-    if (owords) w |= owords[t >> 5];
-    if (!((w >> (t & 31)) & 1u)) rec_new[p.y] = 1;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;  // (records < 2^32 - 1)
+  const uint64_t n = *npairs, stride = (uint64_t)gridDim.x * kFixT * kFixU;
+  for (uint64_t base = (uint64_t)blockIdx.x * kFixT * kFixU + threadIdx.x; base < n; base += stride) {
+    uint2 p[kFixU];
+#pragma unroll
+    for (int u = 0; u < kFixU; u++) {
+      const uint64_t i = base + (uint64_t)u * kFixT;
+      p[u] = i < n ? __builtin_nontemporal_load(&pairs[i]) : make_uint2(0u, kNone);
+    }
+    uint32_t t[kFixU], w[kFixU];
+#pragma unroll
+    for (int u = 0; u < kFixU; u++) {
+      t[u] = sgd::set_pos(p[u].x);
+      w[u] = p[u].y != kNone ? mwords[t[u] >> 5] : ~0u;
+    }
+    if (owords) {
+#pragma unroll
+      for (int u = 0; u < kFixU; u++)
+        if (p[u].y != kNone) w[u] |= owords[t[u] >> 5];
+    }
+#pragma unroll
+    for (int u = 0; u < kFixU; u++)
+      if (!((w[u] >> (t[u] & 31)) & 1u)) rec_new[p[u].y] = 1;
   }
 }
 
@@ -2380,7 +2398,8 @@ int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owo
   if (!S.keep) {
     if (S.n) {
       ScopedTimer tm(ctx, "prefix_flags");
-      hipLaunchKernelGGL(k_prefix_flags, dim3((uint32_t)std::min<uint64_t>(div_up(S.n, kFixT), 8192)), dim3(kFixT), 0,
+      hipLaunchKernelGGL(k_prefix_flags, dim3((uint32_t)std::min<uint64_t>(div_up(S.n, kFixT * kFixU), 2048)),
+                         dim3(kFixT), 0,
                          ctx->stream, (const uint2*)((char*)S.ws + 256), (const unsigned long long*)S.ws, mwords,
                          owords, d_rec_new);
     }
