@@ -2252,7 +2252,12 @@ __global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict_
 #pragma unroll
     for (int u = 0; u < kFixU; u++) {
       const uint64_t i = base + (uint64_t)u * kFixT;
-      p[u] = i < n ? __builtin_nontemporal_load(&pairs[i]) : make_uint2(0u, kNone);
+      if (i < n) {
+        const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(pairs) + i);
+        p[u] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+      } else {
+        p[u] = make_uint2(0u, kNone);
+      }
     }
     uint32_t t[kFixU], w[kFixU];
 #pragma unroll
