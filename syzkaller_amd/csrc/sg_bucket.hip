@@ -2270,9 +2270,19 @@ __global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict_
       for (int u = 0; u < kFixU; u++)
         if (p[u].y != kNone) w[u] |= owords[t[u] >> 5];
     }
+    // a record owns ~100s of pairs: read its flag first (the 1-B flags of a
+    // batch stay in L2) and store only while it reads 0 -- a flag another
+    // XCD's L2 holds may still read 0 here, which costs a redundant store
+    uint8_t f[kFixU];
+#pragma unroll
+    for (int u = 0; u < kFixU; u++) {
+      const bool miss = !((w[u] >> (t[u] & 31)) & 1u);
+      f[u] = miss ? rec_new[p[u].y] : 1;
+      t[u] = miss ? 1u : 0u;
+    }
 #pragma unroll
     for (int u = 0; u < kFixU; u++)
-      if (!((w[u] >> (t[u] & 31)) & 1u)) rec_new[p[u].y] = 1;
+      if (t[u] && !f[u]) rec_new[p[u].y] = 1;
   }
 }
 
@@ -2407,6 +2417,12 @@ int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owo
                          dim3(kFixT), 0,
                          ctx->stream, (const uint2*)((char*)S.ws + 256), (const unsigned long long*)S.ws, mwords,
                          owords, d_rec_new);
+    }
+    if (ctx->debug_part && S.n) {  // diagnostics (syncs): the kept pairs
+      unsigned long long np = 0;
+      SG_HIP(hipMemcpyAsync(&np, S.ws, 8, hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      fprintf(stderr, "sg prefix: %llu entries, %llu pairs\n", (unsigned long long)S.n, np);
     }
     if (update && S.n) {
       ScopedTimer tm(ctx, "prefix_merge");
