@@ -210,8 +210,9 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
  * contain begin's base.  End's set updates: newsig (nullable) gains the new
  * signal (marks minus maxsig | d_prefix), and maxsig |= marks -- its new signal
  * and bits of d_prefix (the prefix protocol ORs a superset of d_prefix into
- * maxsig afterwards).  Flags: end without the set updates (maxsig is only
- * read).  Marks must stay unchanged until end; only begin's launches read the
+ * maxsig afterwards).  Flags: the flags without newsig; maxsig ends between
+ * its value and maxsig | marks | d_prefix (the protocol ORs a superset of
+ * marks | d_prefix into it next).  Marks must stay unchanged until end; only begin's launches read the
  * batch's buffers, and other calls may run on the context between begin and
  * end/flags (the slots have workspaces of their own).  End and flags close
  * the slot. */

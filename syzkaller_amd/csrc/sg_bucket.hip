@@ -2197,9 +2197,12 @@ static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std:
 // against M = maxsig | prefix for any M containing base: every s of the batch
 // outside M is outside base, so its pair is kept, and its first owner is the
 // loop's (a record is queued iff it is the first to hold some s outside M).
-// SG_PREFIX_KEEP=1 selects the earlier form, kept for measurement: begin
-// keeps the partitions and marks the buckets (k_bucket_mark), end runs the
-// bucket stage against maxsig | prefix.
+// That is the form SG_PREFIX_PAIRS=1 selects.  The default keeps the
+// partitions instead: begin marks the buckets (k_bucket_mark, the base slice
+// in LDS), end runs the bucket stage against maxsig | prefix.  On a fresh C3
+// slice (1.76G entries, 361M pairs) the pairs' flag pass (3.9 ms: two random
+// cache lines per pair) costs more than the mark pass (2 x 1.0 ms); the pair
+// form's end shrinks with the batch's novelty, the kept partitions' does not.
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // The slot's workspace stands in for the context's during one call (the
@@ -2236,10 +2239,10 @@ static int slot_reserve(sg_ctx* ctx, PrefixSlot& s, size_t bytes) {
   return SG_OK;
 }
 
-// flags of the kept pairs {s, record}: kFixU pairs per thread in flight (the
-// pair read, the bitmap read it selects and the flag store are a dependent
-// chain; one pair per thread and step measured 7.2 ms per C3 slice); a
-// bucket's pairs are adjacent, so their bitmap words share cache lines
+// flags of the kept pairs {s, record}: kFixU pairs per thread in flight (one
+// pair per thread and step: 7.2 ms per C3 slice, eight: 3.9 ms).  Bound by
+// the random cache-line accesses, two per pair (the bitmap word, the flag
+// byte): 361M pairs of a fresh C3 slice at ~0.2 G lines/s/CU
 constexpr int kFixT = 256, kFixU = 8;
 __global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict__ pairs,
                                                         const unsigned long long* __restrict__ npairs,
@@ -2270,19 +2273,9 @@ __global__ __launch_bounds__(kFixT) void k_prefix_flags(const uint2* __restrict_
       for (int u = 0; u < kFixU; u++)
         if (p[u].y != kNone) w[u] |= owords[t[u] >> 5];
     }
-    // a record owns ~100s of pairs: read its flag first (the 1-B flags of a
-    // batch stay in L2) and store only while it reads 0 -- a flag another
-    // XCD's L2 holds may still read 0 here, which costs a redundant store
-    uint8_t f[kFixU];
-#pragma unroll
-    for (int u = 0; u < kFixU; u++) {
-      const bool miss = !((w[u] >> (t[u] & 31)) & 1u);
-      f[u] = miss ? rec_new[p[u].y] : 1;
-      t[u] = miss ? 1u : 0u;
-    }
 #pragma unroll
     for (int u = 0; u < kFixU; u++)
-      if (t[u] && !f[u]) rec_new[p[u].y] = 1;
+      if (!((w[u] >> (t[u] & 31)) & 1u)) rec_new[p[u].y] = 1;
   }
 }
 
@@ -2312,8 +2305,8 @@ __global__ void k_prefix_merge(const uint32_t* __restrict__ marks, uint32_t* __r
 }
 
 static bool prefix_keep_mode() {  // read at each begin (tests switch it)
-  const char* e = getenv("SG_PREFIX_KEEP");
-  return e && atoi(e) != 0;
+  const char* e = getenv("SG_PREFIX_PAIRS");
+  return !(e && atoi(e) != 0);
 }
 
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,

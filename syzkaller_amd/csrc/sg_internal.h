@@ -60,8 +60,8 @@ struct PrefixSlice {
   size_t ws_base;
 };
 
-// One kept batch of the two-phase triage: its first-owner pairs (or, with
-// SG_PREFIX_KEEP, its record slices and their partitions), in a workspace of
+// One kept batch of the two-phase triage: its record slices and their
+// partitions (or, with SG_PREFIX_PAIRS, its first-owner pairs), in a workspace of
 // its own (two slots, so one batch's exchange can run while the next one is
 // partitioned)
 struct PrefixSlot {
@@ -205,9 +205,9 @@ struct EmitArgs {
 // Workspace bytes of one partitioned launch over n entries / nrec records.
 size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
 // Two-phase triage (sg_bucket.hip): begin ORs into marks_words the batch's
-// signal not in base_words and keeps each such signal's first record in the
-// slot; end flags the records against mwords | owords and, with `update`,
-// ORs the marks into mwords (nwords gaining what mwords | owords lacked).
+// signal not in base_words and keeps the batch's partitions (or each such
+// signal's first record) in the slot; end flags the records against
+// mwords | owords and, with `update`, updates mwords / nwords.
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec);
 int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new,

@@ -218,7 +218,7 @@ class HipStages:
              else None, newset.h if newset is not None else None, rec_new.data_ptr())
 
     def prefix_flags(self, maxset, prefix, rec_new, slot=0):
-        """prefix_end's flags only (maxset is only read)."""
+        """prefix_end's flags; maxset gains at most the batch's marks | prefix."""
         call("sg_prefix_flags_dev", self.ctx.h, slot, maxset.h, ctypes.c_void_p(prefix.data_ptr()) if prefix is not None
              else None, rec_new.data_ptr())
 
@@ -319,20 +319,23 @@ class PrefixTriage:
     bitmap prefixes instead of candidate pairs:
 
       1. C_k = the signal of rank k's records not in M0 (the replicated
-         maxSignal): sg_prefix_begin_dev runs the local triage's bucket stage
-         against M0 in emitting form -- C_k's bits, and each s of C_k with its
-         first record in rank k's slice, kept for step 3.
+         maxSignal): sg_prefix_begin_dev partitions rank k's records once
+         (kept for step 3) and marks that signal bucket by bucket.  (Only
+         M0 | P_k matters below, so marking every signal would do too; the
+         test against M0 keeps the LDS atomics to the candidates: marking
+         every signal measured 1.26 vs 1.0 ms per C2-sized slice.)
       2. P_k = OR of C_j over ranks j < k, T = OR of every C_j: all-to-all of
          bitmap slices, an exclusive prefix-OR per slice on the owning rank
          (sg_bitmap_prefix_or_dev; RCCL has no bitwise OR), all-to-all of the
          prefixes back, all-gather of the totals.
-      3. The flags against M0 | P_k (sg_prefix_flags_dev: record r is
-         queued iff it is the first owner of some s of C_k outside M0 | P_k;
-         rank 0 reads no P, P_0 being empty).  M0 | P_k is the sequential
-         loop's maxSignal before rank k's first record (P_k is the new signal
-         of every earlier record), and within the rank the first owners are
-         the loop's, so the flags are the loop's.
-      4. maxSignal = M0 | T and newSignal |= T on every rank.
+      3. The local triage of rank k's records against M0 | P_k
+         (sg_prefix_flags_dev, on the partitions of step 1, reading P_k beside
+         maxSignal; rank 0 reads none, P_0 being empty).  M0 | P_k is the
+         sequential loop's maxSignal before rank k's first record (P_k is the
+         new signal of every earlier record), and within the rank the local
+         triage is the loop itself, so the flags are the loop's.
+      4. maxSignal = M0 | T and newSignal |= T on every rank (step 3 left
+         maxSignal between M0 and M0 | T).
     Per rank and step the exchange moves about 2.5 bitmaps (512 MiB each)
     whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
     rank it is the plain local triage.
@@ -342,10 +345,12 @@ class PrefixTriage:
     steps 3-4.  Batches alternate between two slots, so the next batch can be
     started -- partitioned and marked while this one's bitmaps travel -- before
     this one is finished:  start(b0), start(b1), finish(b0), start(b2),
-    finish(b1), ...  Beginning batch i+1 against a maxSignal that still lacks
-    batch i's total T_i only adds signal of M0' = M0 | T_i to C (and to the
-    kept first owners), M0' | P' = M0' | P, and step 3 tests against the
-    current maxSignal, M0', so the flags are unchanged.  Stage contracts:
+    finish(b1), ...  Marking batch i+1 against a maxSignal that still lacks
+    batch i's total T_i only adds signal of M0' = M0 | T_i to C, and
+    M0' | P' = M0' | P, so the flags are unchanged.  (SG_PREFIX_PAIRS=1: begin
+    keeps each s of C_k with its first record instead of the partitions, and
+    step 3 tests those pairs against the current maxSignal | P_k; measured
+    slower on fresh batches, include/syzsig.h and sg_bucket.hip.)  Stage contracts:
     HipStages."""
 
     def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None,

@@ -102,12 +102,12 @@ class _Words:
         return self.s.device_words()
 
 
-@pytest.mark.parametrize("keep", [False, True])
+@pytest.mark.parametrize("pairs", [False, True])
 @pytest.mark.parametrize("as_prefix", [False, True])
-def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, keep):
-    """sg_prefix_begin_dev / sg_prefix_end_dev (first-owner pairs kept between
-    the two calls, or with SG_PREFIX_KEEP the partitions; several record
-    slices via a lowered per-launch record limit) against the oracle: the
+def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, pairs):
+    """sg_prefix_begin_dev / sg_prefix_end_dev (the partitions kept between
+    the two calls, or with SG_PREFIX_PAIRS the first-owner pairs; several
+    record slices via a lowered per-launch record limit) against the oracle: the
     marks are the batch's signal not in the base set, and the flags after end
     are the sequential loop's against maxsig | prefix.  Without a prefix
     maxsig / newsig end as the loop's; with one, maxsig ends between M0 ∪ new
@@ -115,8 +115,8 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, keep):
     from syzkaller_amd.shard import HipStages
 
     monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
-    if keep:
-        monkeypatch.setenv("SG_PREFIX_KEEP", "1")
+    if pairs:
+        monkeypatch.setenv("SG_PREFIX_PAIRS", "1")
     ctx2 = C.Context(0)
     st = HipStages(ctx2)
     vals, off = _batch(305, 5000, hi=1 << 18)
@@ -149,17 +149,20 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, keep):
         ms.or_device(pre.device_words())
         got = ms.export()
     assert np.array_equal(got, om.export())
-    if not keep:  # flags only: the same flags, maxsig only read
-        ms2 = C.SignalSet(ctx2)
-        C.SignalAdd(ms2, m0 if as_prefix else np.union1d(m0, extra))
-        rec2 = torch.full((nrec,), 7, dtype=torch.uint8, device="cuda")
-        st.clear(marks)  # (begin's marks start empty: include/syzsig.h)
-        st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=0)
-        st.prefix_flags(ms2, _Words(pre) if as_prefix else None, rec2, slot=0)
-        torch.cuda.synchronize()
-        assert np.array_equal(rec2.cpu().numpy(), ef)
-        assert np.array_equal(ms2.export(), m0 if as_prefix else np.union1d(m0, extra))
-        del ms2
+    # sg_prefix_flags_dev: the same flags; maxsig gains at most marks | prefix
+    ms0 = m0 if as_prefix else np.union1d(m0, extra)
+    ms2 = C.SignalSet(ctx2)
+    C.SignalAdd(ms2, ms0)
+    rec2 = torch.full((nrec,), 7, dtype=torch.uint8, device="cuda")
+    st.clear(marks)  # (begin's marks start empty: include/syzsig.h)
+    st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=0)
+    st.prefix_flags(ms2, _Words(pre) if as_prefix else None, rec2, slot=0)
+    torch.cuda.synchronize()
+    assert np.array_equal(rec2.cpu().numpy(), ef)
+    got2 = ms2.export()
+    assert np.isin(ms0, got2).all()
+    assert np.isin(got2, np.union1d(np.union1d(ms0, marks.export()), extra if as_prefix else ms0)).all()
+    del ms2
     del base, marks, ms, ns, pre
     ctx2.close()
 
