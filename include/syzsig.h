@@ -199,8 +199,8 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
 int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
 			    uint32_t* d_total);
 /* The two halves of sg_triage_batch_dev (flags and set updates, no diff) for
- * the prefix protocol.  Begin: marks (empty at begin; base != marks) gets every
- * signal of the batch not in base (the local new signal, fuzzer.go:666), and
+ * the prefix protocol.  Begin: marks (base != marks) = every signal of the
+ * batch not in base (the local new signal, fuzzer.go:666), and
  * each such signal's first record in the batch is kept in the context's slot
  * (0 or 1: two batches can be kept, so one batch's exchange runs while the
  * next is begun).  End: the

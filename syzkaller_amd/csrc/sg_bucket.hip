@@ -2017,16 +2017,24 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
 // (a workgroup per bucket: its maxSignal slice in LDS, its newSignal words
 // written by it alone).  Entries are read as 16-B quads from the bucket start
 // rounded down (the pass-2 buffer is padded), kMarkU quads per thread in
-// flight; the first ones are issued before the slice is installed.
+// flight; the first ones are issued before the slice is installed.  kFirst:
+// nwords = those signals (every word written, empty buckets' too: no clear
+// beforehand and no read of the old words).
 constexpr int kMarkT = 256, kMarkU = 2;
+template <bool kFirst>
 __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
                                                         const uint32_t* __restrict__ mwords,
                                                         uint32_t* __restrict__ nwords) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
+  constexpr int kW = kBucketWords / kMarkT;  // slice words per thread
+  typedef uint32_t mvec __attribute__((ext_vector_type(kW)));
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint4 q = bdesc[b];
-  if (q.x >= q.y) return;
+  if (q.x >= q.y) {
+    if (kFirst) *reinterpret_cast<mvec*>(nwords + bucket_word(b, kW * tid)) = mvec{};
+    return;
+  }
   constexpr uint32_t kStep = kMarkT * 4 * kMarkU;
   auto load = [&](uint32_t base, v4u32 (&v)[kMarkU]) {
 #pragma unroll
@@ -2039,9 +2047,7 @@ __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restri
   uint32_t base = q.x & ~3u;
   v4u32 v[kMarkU];
   load(base, v);
-  constexpr int kW = kBucketWords / kMarkT;  // slice words per thread
   {
-    typedef uint32_t mvec __attribute__((ext_vector_type(kW)));
     const uint64_t w0 = bucket_word(b, kW * tid);
     reinterpret_cast<mvec*>(mslice)[tid] = *reinterpret_cast<const mvec*>(mwords + w0);
     reinterpret_cast<mvec*>(nbits)[tid] = mvec{};
@@ -2066,6 +2072,10 @@ __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restri
     for (int u = 0; u < kMarkU; u++) v[u] = y[u];
   }
   __syncthreads();
+  if (kFirst) {
+    *reinterpret_cast<mvec*>(nwords + bucket_word(b, kW * tid)) = reinterpret_cast<const mvec*>(nbits)[tid];
+    return;
+  }
   for (uint32_t i = tid; i < kBucketWords; i += kMarkT)
     if (nbits[i]) nwords[bucket_word(b, i)] |= nbits[i];
 }
@@ -2335,6 +2345,7 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
     unsigned long long* np = (unsigned long long*)S.ws;
     uint2* pairs = (uint2*)((char*)S.ws + 256);
     SG_HIP(hipMemsetAsync(np, 0, 8, ctx->stream));
+    SG_HIP(hipMemsetAsync(marks_words, 0, kSetBytes, ctx->stream));  // (the later slices' filter)
     size_t need = 0;
     for (const RecSlice& x : sl)
       if (x.e1 > x.e0)
@@ -2367,6 +2378,7 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
   if (rc) return rc;
   SlotWs guard(ctx, S);
   size_t base = 0;
+  bool first = true;
   for (const RecSlice& x : sl) {
     PrefixSlice ps{x.r0, x.r1, x.e0, x.e1, base};
     if (x.e1 > x.e0) {
@@ -2380,15 +2392,22 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
       if (rc) return rc;
       {
         ScopedTimer tm(ctx, "bucket_mark");
-        hipLaunchKernelGGL(k_bucket_mark, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream,
-                           (const uint32_t*)ws_at(ctx, bp.oV2), (const uint4*)ws_at(ctx, bp.oBD), base_words,
-                           marks_words);
+        const uint32_t* v2 = (const uint32_t*)ws_at(ctx, bp.oV2);
+        const uint4* bd = (const uint4*)ws_at(ctx, bp.oBD);
+        if (first)  // the batch's first slice writes every marks word
+          hipLaunchKernelGGL(k_bucket_mark<true>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd, base_words,
+                             marks_words);
+        else
+          hipLaunchKernelGGL(k_bucket_mark<false>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd,
+                             base_words, marks_words);
+        first = false;
       }
       SG_HIP(hipGetLastError());
       base = roff_at + align256((nr + 1) * 8);
     }
     S.slices.push_back(ps);
   }
+  if (first) SG_HIP(hipMemsetAsync(marks_words, 0, kSetBytes, ctx->stream));  // no entries
   S.nrec = nrec;
   S.open = true;
   return SG_OK;

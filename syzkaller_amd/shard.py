@@ -412,7 +412,6 @@ class PrefixTriage:
         self.next_slot ^= 1
         b = self.slots[slot]
         # 1. this rank's new signal against M0 (its partitions kept for 3.)
-        st.clear(b["cset"])
         st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
         # 2. exclusive prefix and total over the ranks (slice by slice, or
         # whole bitmaps in gather mode)

@@ -75,6 +75,7 @@ class NumpyPrefixStages:
 
     def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0):
         v = vals[:nvals].numpy().view(np.uint32)
+        marks.w[:] = 0  # (marks = the batch's signal not in base)
         if v.size:
             marks.add(v[~base.has(v)])
         self.kept[slot] = (vals, off, nvals, nrec, marks)

@@ -133,6 +133,7 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, pairs):
     v, o = _dev(vals, np.int32), _dev(off, np.int64)
     nrec = off.size - 1
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    C.SignalAdd(marks, extra[::3])  # begin overwrites the marks
     st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=1)
     st.prefix_end(ms, _Words(pre) if as_prefix else None, ns, rec_new, slot=1)
     torch.cuda.synchronize()
@@ -154,7 +155,7 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, pairs):
     ms2 = C.SignalSet(ctx2)
     C.SignalAdd(ms2, ms0)
     rec2 = torch.full((nrec,), 7, dtype=torch.uint8, device="cuda")
-    st.clear(marks)  # (begin's marks start empty: include/syzsig.h)
+    C.SignalAdd(marks, extra)  # (begin overwrites marks: include/syzsig.h)
     st.prefix_begin(base, marks, v, o, vals.size, nrec, slot=0)
     st.prefix_flags(ms2, _Words(pre) if as_prefix else None, rec2, slot=0)
     torch.cuda.synchronize()
