@@ -302,8 +302,9 @@ __global__ void k_set_add(uint32_t* __restrict__ words, const uint32_t* __restri
 __global__ void k_set_or(uint32_t* __restrict__ words, const uint32_t* __restrict__ other) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kSetWords / 4; i += stride) {
+    const uint4 b = reinterpret_cast<const uint4*>(other)[i];
+    if (!(b.x | b.y | b.z | b.w)) continue;  // (a sparse `other` reads little else)
     uint4 a = reinterpret_cast<uint4*>(words)[i];
-    uint4 b = reinterpret_cast<const uint4*>(other)[i];
     a.x |= b.x;
     a.y |= b.y;
     a.z |= b.z;
@@ -317,8 +318,10 @@ __global__ void k_set_or_new(uint32_t* __restrict__ words, const uint32_t* __res
                              const uint32_t* __restrict__ exclude) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kSetWords / 4; i += stride) {
+    const uint4 b = reinterpret_cast<const uint4*>(other)[i];
+    if (!(b.x | b.y | b.z | b.w)) continue;
     uint4 a = reinterpret_cast<uint4*>(words)[i];
-    const uint4 b = reinterpret_cast<const uint4*>(other)[i], x = reinterpret_cast<const uint4*>(exclude)[i];
+    const uint4 x = reinterpret_cast<const uint4*>(exclude)[i];
     a.x |= b.x & ~x.x;
     a.y |= b.y & ~x.y;
     a.z |= b.z & ~x.z;
