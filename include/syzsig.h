@@ -335,6 +335,13 @@ int sg_union_fold(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t
 /* HasDifference (cover.go:106-117): *out = 1 iff a has an element (multiset,
  * no sentinel special case) not matched in b. */
 int sg_has_difference(sg_ctx* ctx, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, int* out);
+/* Batched HasDifference over npair pairs laid out as in sg_merge_batch (pair
+ * k: a[a_beg[k] .. +a_len[k]) against b[b_beg[k] .. +b_len[k]); pairs may
+ * share b): out[k] = 1 iff that a has an element not matched in that b, else
+ * 0.  Host pointers. */
+int sg_has_difference_batch(sg_ctx* ctx, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+			    const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+			    const uint64_t* b_len, size_t npair, uint8_t* out);
 
 /* ---- executor edge signal (executor/executor.h:389-401, :497-526) --------- */
 /* Raw per-call u32 PC traces -> per-call signal, executor-exact: edge

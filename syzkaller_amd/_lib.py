@@ -91,6 +91,8 @@ SIGNATURES = {
                                c_size_t, P64, P64]),
     "sg_union_fold": (c_int, [c_void_p, P32, P64, c_size_t, P32, c_size_t, P32, c_size_t, P64]),
     "sg_has_difference": (c_int, [c_void_p, P32, c_size_t, P32, c_size_t, PINT]),
+    "sg_has_difference_batch": (c_int, [c_void_p, P32, c_size_t, P64, P64, P32, c_size_t, P64, P64, c_size_t,
+                                        c_void_p]),
     "sg_exec_signal": (c_int, [c_void_p, P32, P64, P64, c_size_t, P32, P64]),
     "sg_exec_signal_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
                                    c_void_p]),

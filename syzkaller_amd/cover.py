@@ -221,6 +221,17 @@ def HasDifference(cov0, cov1, ctx=None):
     return bool(out.value)
 
 
+def has_difference_batch(a, a_beg, a_len, b, b_beg, b_len, ctx=None):
+    """HasDifference (cover.go:106-117) of every pair, laid out as merge_batch's:
+    a bool array."""
+    a, b = _u32(a), _u32(b)
+    ab, al, bb, bl = _u64(a_beg), _u64(a_len), _u64(b_beg), _u64(b_len)
+    out = np.zeros(max(ab.size, 1), dtype=np.uint8)
+    call("sg_has_difference_batch", _ctx(ctx).h, _p32(a), a.size, _p64(ab), _p64(al), _p32(b), b.size, _p64(bb),
+         _p64(bl), ab.size, out.ctypes.data)
+    return out[: ab.size].astype(bool)
+
+
 def to_csr(lists):
     lens = np.array([len(x) for x in lists], dtype=U64)
     off = np.zeros(len(lists) + 1, dtype=U64)

@@ -599,6 +599,29 @@ __global__ void k_has_difference(const uint32_t* __restrict__ a, uint64_t na, co
   if (__any(hit) && (threadIdx.x & 63) == 0) *flag = 1;
 }
 
+// Batched HasDifference: a workgroup per pair, its a-range strided over the
+// threads (element t-th copy of x vs x's count in b, both by binary search in
+// the pair's own ranges); one flag byte per pair.
+constexpr int kHdT = 256;
+__global__ __launch_bounds__(kHdT) void k_has_difference_batch(const uint32_t* __restrict__ a,
+                                                               const uint64_t* __restrict__ a_beg,
+                                                               const uint64_t* __restrict__ a_len,
+                                                               const uint32_t* __restrict__ b,
+                                                               const uint64_t* __restrict__ b_beg,
+                                                               const uint64_t* __restrict__ b_len, uint8_t* out) {
+  const uint64_t k = blockIdx.x;
+  const uint32_t* pa = a + a_beg[k];
+  const uint32_t* pb = b + b_beg[k];
+  const uint64_t na = a_len[k], nb = b_len[k];
+  bool hit = false;
+  for (uint64_t i = threadIdx.x; i < na && !hit; i += kHdT) {
+    const uint32_t x = pa[i];
+    const uint64_t t = i - lower_bound(pa, i, x);
+    hit = t >= upper_bound(pb, nb, x) - lower_bound(pb, nb, x);
+  }
+  if (__syncthreads_or(hit) && threadIdx.x == 0) out[k] = 1;
+}
+
 // ---- segmented sort ----------------------------------------------------------
 struct SortChunk {
   uint64_t start;  // global element index
@@ -1047,6 +1070,47 @@ int sg_has_difference(sg_ctx* ctx, const uint32_t* a, size_t na, const uint32_t*
   SG_HIP(hipMemcpyAsync(&f, ctx->dscal, 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   *out = f ? 1 : 0;
+  return SG_OK;
+}
+
+int sg_has_difference_batch(sg_ctx* ctx, const uint32_t* a, size_t a_total, const uint64_t* a_beg,
+                            const uint64_t* a_len, const uint32_t* b, size_t b_total, const uint64_t* b_beg,
+                            const uint64_t* b_len, size_t npair, uint8_t* out) {
+  if (!ctx || (npair && (!a_beg || !a_len || !b_beg || !b_len || !out)) || (a_total && !a) || (b_total && !b) ||
+      npair > 0x7FFFFFFFu)
+    return SG_EINVAL;
+  for (size_t k = 0; k < npair; k++)
+    if (a_beg[k] + a_len[k] > a_total || b_beg[k] + b_len[k] > b_total) {
+      set_error("sg_has_difference_batch: pair %zu out of range", k);
+      return SG_EINVAL;
+    }
+  if (npair == 0) return SG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  WsPlan p;
+  const size_t o_a = p.add(a_total * 4), o_b = p.add(b_total * 4), o_m = p.add(npair * 32), o_o = p.add(npair);
+  rc = ws_reserve(ctx, p.total);
+  if (rc) return rc;
+  uint32_t* da = (uint32_t*)ws_at(ctx, o_a);
+  uint32_t* db = (uint32_t*)ws_at(ctx, o_b);
+  uint64_t* dm = (uint64_t*)ws_at(ctx, o_m);
+  uint8_t* dout = (uint8_t*)ws_at(ctx, o_o);
+  if (a_total) SG_HIP(hipMemcpyAsync(da, a, a_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (b_total) SG_HIP(hipMemcpyAsync(db, b, b_total * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dm, a_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dm + npair, a_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dm + 2 * npair, b_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dm + 3 * npair, b_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemsetAsync(dout, 0, npair, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "has_difference");
+    hipLaunchKernelGGL(k_has_difference_batch, dim3((uint32_t)npair), dim3(kHdT), 0, ctx->stream, da, dm, dm + npair,
+                       db, dm + 2 * npair, dm + 3 * npair, dout);
+  }
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out, dout, npair, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
   return SG_OK;
 }
 

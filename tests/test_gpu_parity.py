@@ -89,6 +89,41 @@ def test_ops_large_multiset(C):
         assert C.HasDifference(b, a) == O.has_difference(b, a)
 
 
+def test_has_difference_batch_vs_oracle(C):
+    """sg_has_difference_batch against the oracle's HasDifference per pair:
+    empty sides, duplicates (the t-th copy against b's count), sentinels, equal
+    lists, a shared b, and pairs longer than a workgroup's stride."""
+    from syzkaller_amd import cover as cv
+
+    rng = np.random.default_rng(131)
+    pairs = [(np.zeros(0, np.uint32), np.zeros(0, np.uint32)), (np.array([5], np.uint32), np.zeros(0, np.uint32)),
+             (np.zeros(0, np.uint32), np.array([5], np.uint32)), (np.array([3, 3], np.uint32), np.array([3], np.uint32)),
+             (np.array([3], np.uint32), np.array([3, 3], np.uint32)),
+             (np.array([SENT], np.uint32), np.array([SENT], np.uint32)), (np.array([1, SENT], np.uint32), np.array([1], np.uint32))]
+    shared = np.sort(rng.integers(0, 3000, size=20000)).astype(np.uint32)
+    for it in range(200):
+        n0 = int(rng.integers(0, 3000 if it % 10 == 0 else 40))
+        hi = [4, 64, 3000, 1 << 32][it % 4]
+        a = np.sort(rng.integers(0, hi, size=n0, dtype=np.uint64)).astype(np.uint32)
+        if it % 3 == 0:
+            b = shared
+        elif it % 3 == 1:
+            b = a.copy() if it % 2 else np.sort(rng.integers(0, hi, size=int(rng.integers(0, 40)), dtype=np.uint64)).astype(np.uint32)
+        else:
+            b = np.sort(np.concatenate([a, rng.integers(0, hi, size=5, dtype=np.uint64).astype(np.uint32)]))
+        pairs.append((a, b))
+    av = np.concatenate([p[0] for p in pairs])
+    al = np.array([p[0].size for p in pairs], np.uint64)
+    ab = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.uint64)
+    bl = np.array([p[1].size for p in pairs], np.uint64)
+    bv = np.concatenate([p[1] for p in pairs])
+    bb = np.concatenate([[0], np.cumsum(bl)[:-1]]).astype(np.uint64)
+    got = cv.has_difference_batch(av, ab, al, bv, bb, bl)
+    want = np.array([O.has_difference(a, b) for a, b in pairs])
+    assert np.array_equal(got, want)
+    assert 0 < want.sum() < len(pairs)
+
+
 def test_merge_batch_small_side_multisets(C):
     """The one-small-side merge (sg_merge.hip k_merge_small): pairs whose
     small list fits in LDS against large lists with long runs of one value
