@@ -192,9 +192,10 @@ int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint6
 // d_vals are raw per-call PC traces, triaged by their edge signal.
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
                   uint64_t n, uint64_t nrec, uint8_t* d_rec_new, bool trace = false);
-// Candidate emission of the partitioned path (sharded triage, sg_shard.hip):
-// each distinct s not in the snapshot, once per launch, as {s, rec_base +
-// first record}, counted per owning shard.
+// Candidate emission of the partitioned path (sharded triage, sg_shard.hip;
+// the prefix protocol's pair form): each distinct s not in the snapshot, once
+// per launch, as {s, rec_base + first record}, counted per owning shard when
+// shard_cnt is given.
 struct EmitArgs {
   uint2* pairs;
   unsigned long long* npairs;
