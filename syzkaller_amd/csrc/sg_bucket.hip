@@ -942,12 +942,6 @@ __device__ __forceinline__ void flush_shard_counts(const BucketArgs& a, const ui
       if (shcnt[i]) atomicAdd(&a.shard_cnt[i], (unsigned long long)shcnt[i]);
 }
 
-// non-empty flag per bucket (scanned into list positions)
-__global__ void k_bucket_nz(const uint4* __restrict__ bdesc, uint32_t* __restrict__ nz) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < kNumBuckets) nz[b] = bdesc[b].x < bdesc[b].y ? 1u : 0u;
-}
-
 __global__ void k_bucket_compact(const uint4* __restrict__ bdesc, const uint32_t* __restrict__ lpos,
                                  uint32_t* __restrict__ blist_b, uint4* __restrict__ blist_q) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -959,14 +953,17 @@ __global__ void k_bucket_compact(const uint4* __restrict__ bdesc, const uint32_t
   }
 }
 
-// {lo, hi, c0, nch} of every bucket, from the pass-2 scan
+// {lo, hi, c0, nch} of every bucket, from the pass-2 scan, and its
+// non-empty flag (scanned into list positions)
 __global__ void k_bucket_desc(const uint32_t* __restrict__ goff2, const uint32_t* __restrict__ gcount,
-                              const uint32_t* __restrict__ cfirst, uint4* __restrict__ bdesc) {
+                              const uint32_t* __restrict__ cfirst, uint4* __restrict__ bdesc, uint32_t* __restrict__ nz) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= kNumBuckets) return;
   const uint32_t d = b >> 8, f = b & 255, c0 = cfirst[d], nch = cfirst[d + 1] - c0;
   const uint32_t* row = goff2 + (uint64_t)f * *gcount + c0;
-  bdesc[b] = make_uint4(row[0], row[nch], c0, nch);
+  const uint32_t lo = row[0], hi = row[nch];
+  bdesc[b] = make_uint4(lo, hi, c0, nch);
+  nz[b] = lo < hi ? 1u : 0u;
 }
 
 // gbnd[b * NG + g]: bucket b = (d, f) holds the runs of slice d's chunks in
@@ -1634,7 +1631,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan32_apply(const uint32_t* _
   }
 #pragma unroll
   for (int k = 0; k < kScanPer; k++) s += v[k];
-  uint32_t run = sums[blockIdx.x] + block_excl_scan(s, wsum, &tot);
+  uint32_t run = (sums ? sums[blockIdx.x] : 0u) + block_excl_scan(s, wsum, &tot);
   uint32_t o[kScanPer];
 #pragma unroll
   for (int k = 0; k < kScanPer; k++) {
@@ -1662,6 +1659,12 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
   const uint64_t nb = (n + kScanTile - 1) / kScanTile;
   if (nb == 0) {
     SG_HIP(hipMemsetAsync(out, 0, 4, ctx->stream));
+    return SG_OK;
+  }
+  if (nb == 1) {  // one tile: the apply pass alone
+    hipLaunchKernelGGL(k_scan32_apply, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n, n_dev, mul,
+                       (const uint32_t*)nullptr, out);
+    SG_HIP(hipGetLastError());
     return SG_OK;
   }
   hipLaunchKernelGGL(k_scan32_reduce, dim3((uint32_t)nb), dim3(kScanThreads), 0, ctx->stream, in, n, n_dev, mul,
@@ -1860,13 +1863,12 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
     ScopedTimer tm(ctx, "p2_scatter");
     hipLaunchKernelGGL(k_p2_scatter, dim3(G), dim3(kPThreads), 0, ctx->stream, a2);
   }
-  hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
-                     gcount, (const uint32_t*)cfirst, bdesc);
-  hipLaunchKernelGGL(k_bucket_groups, dim3(div_up((uint64_t)kNumBuckets * NG, 256)), dim3(256), 0, ctx->stream,
-                     (const uint32_t*)goff2, gcount, (const uint32_t*)cbase, NG, gbnd);
   uint32_t* bnz = (uint32_t*)ws_at(ctx, bp.oBN);
   uint32_t* blpos = (uint32_t*)ws_at(ctx, bp.oBP);
-  hipLaunchKernelGGL(k_bucket_nz, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc, bnz);
+  hipLaunchKernelGGL(k_bucket_desc, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint32_t*)goff2,
+                     gcount, (const uint32_t*)cfirst, bdesc, bnz);
+  hipLaunchKernelGGL(k_bucket_groups, dim3(div_up((uint64_t)kNumBuckets * NG, 256)), dim3(256), 0, ctx->stream,
+                     (const uint32_t*)goff2, gcount, (const uint32_t*)cbase, NG, gbnd);
   rc = scan32(ctx, bnz, blpos, kNumBuckets, scr);
   if (rc) return rc;
   hipLaunchKernelGGL(k_bucket_compact, dim3(kNumBuckets / 256), dim3(256), 0, ctx->stream, (const uint4*)bdesc,
