@@ -657,6 +657,67 @@ __global__ __launch_bounds__(kBlock) void k_sort_chunks(const uint32_t* __restri
   for (uint32_t i = threadIdx.x; i < ch.len; i += kBlock) out[ch.start + i] = s[i];
 }
 
+// Canonicalize of a batch whose segments all fit one tile (<= kTile): each
+// chunk is one whole segment, so the unique pass runs in LDS right after the
+// chunk's sort (no mask, scan or search passes): the kept values (cover.go:31-37:
+// x != the previous sorted value, the first against kSent) go to the
+// segment's start in order, the positions past them keep the sorted values,
+// out_len[seg] = their number.  In place (the chunk is read whole first).
+__global__ __launch_bounds__(kBlock) void k_sort_unique_chunks(uint32_t* vals, const SortChunk* __restrict__ chunks,
+                                                               const uint32_t* __restrict__ seg,
+                                                               uint64_t* __restrict__ out_len) {
+  __shared__ uint32_t s[kTile];
+  __shared__ uint32_t wsum[kBlock / 64];
+  const SortChunk ch = chunks[blockIdx.x];
+  uint32_t P = 2;
+  while (P < ch.len) P <<= 1;
+  for (uint32_t i = threadIdx.x; i < P; i += kBlock) s[i] = i < ch.len ? vals[ch.start + i] : kSent;
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = threadIdx.x; t < P / 2; t += kBlock) {
+        uint32_t i = 2 * t - (t & (j - 1));
+        uint32_t l = i + j;
+        bool up = (i & k) == 0;
+        uint32_t x = s[i], y = s[l];
+        if ((x > y) == up) {
+          s[i] = y;
+          s[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // each thread: kTile / kBlock consecutive positions
+  constexpr int kPer = kTile / kBlock;
+  const uint32_t i0 = threadIdx.x * kPer;
+  uint32_t keep = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; q++) {
+    const uint32_t i = i0 + q;
+    if (i < ch.len && s[i] != (i ? s[i - 1] : kSent)) keep |= 1u << q;
+  }
+  const uint32_t c = __popc(keep), lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t pos = incl - c, total = 0;
+#pragma unroll
+  for (int v = 0; v < kBlock / 64; v++) {
+    pos += v < (int)w ? wsum[v] : 0u;
+    total += wsum[v];
+  }
+  uint32_t* out = vals + ch.start;
+  for (uint32_t m = keep; m; m &= m - 1) out[pos++] = s[i0 + __builtin_ctz(m)];
+  for (uint32_t i = total + threadIdx.x; i < ch.len; i += kBlock) out[i] = s[i];  // the stale tail
+  if (threadIdx.x == 0) out_len[seg[blockIdx.x]] = total;
+}
+
 struct BigSeg {
   uint64_t start;  // global element index of the segment
   uint64_t len;
@@ -764,6 +825,34 @@ __global__ void k_unique_write(CanonArgs a) {
 }
 
 // ---- host orchestration ----------------------------------------------------------
+// chunks: one per non-empty segment, in segment order
+static int canonicalize_small(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg,
+                              const std::vector<SortChunk>& chunks, uint64_t* out_len) {
+  std::vector<uint32_t> seg;
+  seg.reserve(chunks.size());
+  for (uint64_t k = 0; k < nseg; k++)
+    if (off[k + 1] > off[k]) seg.push_back((uint32_t)k);
+  WsPlan p;
+  const size_t o_ch = p.add(chunks.size() * sizeof(SortChunk)), o_seg = p.add(seg.size() * 4), o_len = p.add(nseg * 8);
+  int rc = ws_reserve(ctx, p.total);
+  if (rc) return rc;
+  SortChunk* dch = (SortChunk*)ws_at(ctx, o_ch);
+  uint32_t* dseg = (uint32_t*)ws_at(ctx, o_seg);
+  uint64_t* dlen = (uint64_t*)ws_at(ctx, o_len);
+  SG_HIP(hipMemsetAsync(dlen, 0, nseg * 8, ctx->stream));  // (empty segments)
+  if (!chunks.empty()) {
+    SG_HIP(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(SortChunk), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipMemcpyAsync(dseg, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    ScopedTimer tm(ctx, "canon_sort");
+    hipLaunchKernelGGL(k_sort_unique_chunks, dim3((uint32_t)chunks.size()), dim3(kBlock), 0, ctx->stream, d_vals, dch,
+                       dseg, dlen);
+  }
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(out_len, dlen, nseg * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));  // (the host vectors above are read by the queued copies)
+  return SG_OK;
+}
+
 int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg, uint64_t* out_len) {
   // off: host offsets (nseg+1); d_vals: device values (sorted+uniqued in place)
   uint64_t n = off[nseg];
@@ -780,6 +869,8 @@ int canonicalize_dev(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_
       parity[k] = passes & 1;
     }
   }
+  if (big.empty() && nseg <= 0xFFFFFFFFull)  // every segment fits one tile: sort and unique in one pass
+    return canonicalize_small(ctx, d_vals, off, nseg, chunks, out_len);
   std::sort(big.begin(), big.end(), [](const BigSeg& x, const BigSeg& y) { return x.len > y.len; });
   std::vector<uint64_t> vs(big.size() + 1, 0);
   for (size_t i = 0; i < big.size(); i++) vs[i + 1] = vs[i] + big[i].len;

@@ -211,6 +211,32 @@ def test_canonicalize_batch_ragged(C):
         assert np.array_equal(got[off[k]:off[k + 1]], exp)
 
 
+def test_canonicalize_batch_tile_segments(C):
+    """Every segment <= 4096 (the one-pass sort + unique in LDS): empty
+    segments, sentinel-only and sentinel-tailed ones, all-equal values, full
+    4096-element segments, and many short lists."""
+    rng = np.random.default_rng(132)
+    lens = [0, 1, 4096, 0, 3, 4095, 64, 65, 2] + [int(x) for x in rng.integers(0, 300, size=400)] + [0]
+    segs = []
+    for k, L in enumerate(lens):
+        v = rng.integers(0, [4, 1000, 1 << 32][k % 3], size=L, dtype=np.uint64).astype(np.uint32)
+        if k % 7 == 1 and L:
+            v[:] = SENT
+        elif k % 7 == 2 and L:
+            v[rng.integers(0, L)] = SENT
+        elif k % 7 == 3:
+            v[:] = 9
+        segs.append(v)
+    vals = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    got = vals.copy()
+    out_len = C.canonicalize_batch(got, off)
+    for k in range(len(lens)):
+        exp, m = O.canonicalize(segs[k])
+        assert out_len[k] == m, k
+        assert np.array_equal(got[off[k]:off[k + 1]], exp), k
+
+
 def test_minimize_vs_oracle(C):
     rng = np.random.default_rng(106)
     for n, hi in [(1, 5), (7, 20), (50, 100), (2000, 5000), (20000, 1 << 16)]:
