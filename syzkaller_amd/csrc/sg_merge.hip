@@ -657,6 +657,70 @@ __global__ __launch_bounds__(kBlock) void k_sort_chunks(const uint32_t* __restri
   for (uint32_t i = threadIdx.x; i < ch.len; i += kBlock) out[ch.start + i] = s[i];
 }
 
+// Bitonic sort of P (a power of two, <= kBlock * E) values held E per thread
+// (element i = thread * E + r) in registers: partners within a thread swap in
+// registers, partners within a wave (distance < 64 E) come by __shfl_xor, and
+// only the longer distances go through LDS (s, >= kBlock * E slots) with
+// barriers -- 3 of the 55 stages for P = 1024.  Threads past P / E hold
+// padding and only ever meet each other.
+template <int E>
+__device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], uint32_t P, uint32_t* s) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j < (uint32_t)E) {
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          if ((r & j) == 0) {
+            const uint32_t i = t * E + r;
+            const bool up = (i & k) == 0;
+            const uint32_t x = v[r], y = v[r | j];
+            if ((x > y) == up) {
+              v[r] = y;
+              v[r | j] = x;
+            }
+          }
+        }
+      } else if (j / E < 64) {
+        const int m = (int)(j / E);
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const uint32_t i = t * E + r, y = __shfl_xor(v[r], m);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[r] = keep_min ? min(v[r], y) : max(v[r], y);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < E; r++) s[t * E + r] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const uint32_t i = t * E + r, y = s[i ^ j];
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[r] = keep_min ? min(v[r], y) : max(v[r], y);
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// chunk [start, start + len) sorted into s[0 .. P) (padding kSent)
+template <int E>
+__device__ __forceinline__ void sort_chunk_regs(const uint32_t* vals, const SortChunk& ch, uint32_t P, uint32_t* s) {
+  uint32_t v[E];
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const uint32_t i = threadIdx.x * E + r;
+    v[r] = i < ch.len ? vals[ch.start + i] : kSent;
+  }
+  bitonic_regs<E>(v, P, s);
+  __syncthreads();  // (the last LDS stage's reads are done)
+#pragma unroll
+  for (int r = 0; r < E; r++) s[threadIdx.x * E + r] = v[r];
+  __syncthreads();
+}
+
 // Canonicalize of a batch whose segments all fit one tile (<= kTile): each
 // chunk is one whole segment, so the unique pass runs in LDS right after the
 // chunk's sort (no mask, scan or search passes): the kept values (cover.go:31-37:
@@ -671,23 +735,17 @@ __global__ __launch_bounds__(kBlock) void k_sort_unique_chunks(uint32_t* vals, c
   const SortChunk ch = chunks[blockIdx.x];
   uint32_t P = 2;
   while (P < ch.len) P <<= 1;
-  for (uint32_t i = threadIdx.x; i < P; i += kBlock) s[i] = i < ch.len ? vals[ch.start + i] : kSent;
-  __syncthreads();
-  for (uint32_t k = 2; k <= P; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t t = threadIdx.x; t < P / 2; t += kBlock) {
-        uint32_t i = 2 * t - (t & (j - 1));
-        uint32_t l = i + j;
-        bool up = (i & k) == 0;
-        uint32_t x = s[i], y = s[l];
-        if ((x > y) == up) {
-          s[i] = y;
-          s[l] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  // values per thread: the fewest that hold P (register bitonic stages)
+  if (P <= kBlock)
+    sort_chunk_regs<1>(vals, ch, P, s);
+  else if (P <= 2 * kBlock)
+    sort_chunk_regs<2>(vals, ch, P, s);
+  else if (P <= 4 * kBlock)
+    sort_chunk_regs<4>(vals, ch, P, s);
+  else if (P <= 8 * kBlock)
+    sort_chunk_regs<8>(vals, ch, P, s);
+  else
+    sort_chunk_regs<16>(vals, ch, P, s);
   // each thread: kTile / kBlock consecutive positions
   constexpr int kPer = kTile / kBlock;
   const uint32_t i0 = threadIdx.x * kPer;
