@@ -1676,12 +1676,6 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
   return SG_OK;
 }
 
-// exported (sg_internal.h): a u32 exclusive scan for other files
-size_t scan_u32_ws(uint64_t n) { return scan32_ws(n); }
-int scan_u32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* scratch) {
-  return scan32(ctx, in, out, n, scratch);
-}
-
 // ------------------------------------------------------------------ host ---
 struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, NG, ng, gmax;

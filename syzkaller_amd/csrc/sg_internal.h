@@ -169,10 +169,6 @@ inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) /
 // Device exclusive scan of u32 counts into u64 offsets, out[n] = total
 // (sg_scan.hip).  Uses the workspace tail beyond `ws_used`.
 int scan_counts(sg_ctx* ctx, const uint32_t* d_in, uint64_t* d_out, uint64_t n, size_t ws_used);
-// u32 exclusive scan (sg_bucket.hip): out[0 .. n] (out[n] = total, mod 2^32);
-// scratch: scan_u32_ws(n) bytes of device memory
-int scan_u32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* scratch);
-size_t scan_u32_ws(uint64_t n);
 size_t scan_ws_bytes(uint64_t n);
 
 // Members of a set, ascending, into device memory (sg_ctx.hip; ctx lock held).

@@ -239,19 +239,16 @@ __global__ void k_dec_runs(const uint8_t* __restrict__ in, const uint32_t* __res
   }
 }
 
-// values of each list: running sums of its deltas.  excl is a u32 scan
-// (mod 2^32) of all deltas: value i = excl[i] + delta[i] - excl[list start],
-// and the list's sum passes 32 bits exactly where an addition wraps -- the
-// value comes out below its predecessor excl[i] - excl[list start].
-__global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint32_t* __restrict__ excl,
+// values of each list: running sums of its deltas (u64 scan), range-checked
+__global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t* __restrict__ excl,
                              const uint64_t* __restrict__ voff, const uint64_t* __restrict__ kw, uint64_t N,
                              uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
     const uint64_t k = list_of_w(voff, kw, i);
-    const uint32_t prev = excl[i] - excl[voff[k]], v = prev + delta[i];
-    if (v < prev) *err = 1;
-    out[i] = v;
+    const uint64_t v = excl[i] + delta[i] - excl[voff[k]];
+    if (v > 0xFFFFFFFFull) *err = 1;
+    out[i] = (uint32_t)v;
   }
 }
 
@@ -329,16 +326,16 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   const uint64_t nblk = (nb + 31) / 32;
   WsPlan p;
   const size_t o_tm = p.add(nblk * 4 + 4), o_tc = p.add(nblk * 4 + 4), o_vb = p.add((nblk + 1) * 8),
-               o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 4), o_err = p.add(8), o_hd = p.add(nblk * 4 + 4),
-               o_kwv = p.add(nblk * 8), o_xs = p.add(scan_u32_ws(nb));
+               o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8), o_err = p.add(8), o_hd = p.add(nblk * 4 + 4),
+               o_kwv = p.add(nblk * 8);
   const size_t scan_off = p.total;
-  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nblk));
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nb));
   if (rc) return rc;
   uint32_t* tmask = (uint32_t*)ws_at(ctx, o_tm);
   uint32_t* tcnt = (uint32_t*)ws_at(ctx, o_tc);
   uint64_t* vbase = (uint64_t*)ws_at(ctx, o_vb);
   uint32_t* delta = (uint32_t*)ws_at(ctx, o_d);
-  uint32_t* excl = (uint32_t*)ws_at(ctx, o_x);
+  uint64_t* excl = (uint64_t*)ws_at(ctx, o_x);
   uint32_t* err = (uint32_t*)ws_at(ctx, o_err);
   uint32_t* heads = (uint32_t*)ws_at(ctx, o_hd);
   uint64_t* kwv = (uint64_t*)ws_at(ctx, o_kwv);  // N <= nb
@@ -361,7 +358,7 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
     hipLaunchKernelGGL(k_byte_heads, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_in_off, n, heads);
     hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, heads, nb, vbase, delta, err);
   }
-  rc = scan_u32(ctx, delta, excl, N, (uint32_t*)ws_at(ctx, o_xs));
+  rc = scan_counts(ctx, delta, excl, N, scan_off);
   if (rc) return rc;
   if (N) {
     hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_voff, n, N, kwv);
