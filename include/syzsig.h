@@ -212,7 +212,7 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
  * and bits of d_prefix (the prefix protocol ORs a superset of d_prefix into
  * maxsig afterwards).  Flags: the flags without newsig; maxsig ends between
  * its value and maxsig | marks | d_prefix (the protocol ORs a superset of
- * marks | d_prefix into it next).  Marks must stay unchanged until end; only begin's launches read the
+ * marks | d_prefix into it next), so maxsig is written by flags too.  Marks must stay unchanged until end; only begin's launches read the
  * batch's buffers, and other calls may run on the context between begin and
  * end/flags (the slots have workspaces of their own).  End and flags close
  * the slot. */
@@ -220,7 +220,7 @@ int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks,
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec);
 int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
 		      uint8_t* d_rec_new);
-int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, const sg_set* maxsig, const uint32_t* d_prefix,
+int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix,
 			uint8_t* d_rec_new);
 
 /* syz-fuzzer/fuzzer.go:467-489 addInput(), over n inputs in order:

@@ -682,7 +682,12 @@ int sg_set_or_dev(sg_set* set, const uint32_t* d_words) {
 }
 
 int sg_set_or_new_dev(sg_set* set, const uint32_t* d_words, sg_set* exclude) {
-  if (!set || !d_words || !exclude || exclude->ctx != set->ctx) return SG_EINVAL;
+  if (!set || !d_words || !exclude || exclude->ctx != set->ctx || exclude == set ||
+      d_words == (const uint32_t*)set->words) {
+    // k_set_or_new takes words and exclude __restrict__: no aliasing
+    set_error("sg_set_or_new_dev: invalid argument (null, another context's set, or exclude/words aliasing set)");
+    return SG_EINVAL;
+  }
   sg_ctx* ctx = set->ctx;
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);

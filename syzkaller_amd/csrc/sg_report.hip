@@ -236,7 +236,9 @@ __global__ void k_chunk_prep(ChunkArgs a) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c > a.nch) return;
   uint64_t lo = 0, hi = a.nsym;
-  if (c > 0) lo = ub64(a.send, a.nsym, a.pcs[c * kSites - 1]);
+  // the previous chunk's last site (chunk nch, above every site, follows a
+  // possibly partial last chunk: its bound is the last site, not pcs[nch kSites - 1])
+  if (c > 0) lo = ub64(a.send, a.nsym, a.pcs[min<uint64_t>(c * kSites, a.npcs) - 1]);
   if (c < a.nch) {
     const uint64_t last = a.pcs[min<uint64_t>((c + 1) * kSites, a.npcs) - 1];
     a.bnd[c] = last;
@@ -263,7 +265,9 @@ __global__ void k_site_index(ChunkArgs a) {
   if (c >= a.nch) return;
   const uint64_t* ps = a.pcs + (uint64_t)c * kSites;
   const uint32_t m = (uint32_t)min<uint64_t>(kSites, a.npcs - (uint64_t)c * kSites);
-  const uint64_t s0 = ps[0], x0 = s0 + ((uint64_t)k << a.ssh[c]), x = x0 < s0 ? ~0ull : x0;
+  const uint32_t sh = a.ssh[c];
+  const uint64_t s0 = ps[0], d = (uint64_t)k << sh, x0 = s0 + d;
+  const uint64_t x = (sh < 64 && (d >> sh) == k && x0 >= s0) ? x0 : ~0ull;  // saturate a wrapped bound
   uint32_t lo = 0, hi = m;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;

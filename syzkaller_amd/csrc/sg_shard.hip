@@ -423,7 +423,7 @@ int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t
   return prefix_end(ctx, slot, maxsig->words, d_prefix, newsig ? newsig->words : nullptr, d_rec_new, true);
 }
 
-int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, const sg_set* maxsig, const uint32_t* d_prefix,
+int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix,
                         uint8_t* d_rec_new) {
   if (!ctx || !maxsig || maxsig->ctx != ctx) {
     set_error("sg_prefix_flags_dev: invalid argument");

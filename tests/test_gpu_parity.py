@@ -794,6 +794,39 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
         assert np.array_equal(got, exp), sites.size
 
 
+def test_cover_uncovered_symbol_past_last_site(C):
+    """Queries above the last call site but inside a symbol (the symbol holding
+    the last site reaches past it, and later symbols hold no site), with a site
+    count that is not a multiple of the 4096-site chunk: such a query lands in
+    the past-the-end chunk, whose symbol range starts at the last site's symbol
+    (syz-manager/cover.go:278-299 marks that symbol's sites and later ones find
+    none)."""
+    rng = np.random.default_rng(797)
+    hi32 = np.uint64(0xffffffff) << np.uint64(32)
+    for nsites in (1, 4095, 4097, 4100, 8195):
+        starts, ends, allsites = _symtab(rng, nsites + 64)
+        # keep the sites of the leading symbols only, cut inside a symbol (the
+        # first cut at or below nsites that is not a multiple of 4096), so that
+        # symbol reaches past the last kept site
+        while True:
+            sites = allsites[:nsites]
+            last = sites[-1]
+            k = int(np.searchsorted(ends, last, side="right"))
+            if starts[k] <= last < ends[k] - np.uint64(1) and nsites % 4096:
+                break
+            nsites -= 1
+        gap = np.arange(int(last) + 1, int(ends[k]), dtype=np.uint64)
+        later = np.concatenate([starts[k + 1:], ends[k + 1:] - np.uint64(1)])
+        pcs = np.concatenate([gap, later, rng.choice(sites, size=3000)])
+        q = (pcs + np.uint64(5) - hi32).astype(np.uint32)
+        exp = O.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        assert np.array_equal(got, exp), nsites
+        qs = np.sort(q)
+        assert np.array_equal(C.cover_uncovered(qs, 0xffffffff, starts, ends, sites),
+                              O.cover_uncovered(qs, 0xffffffff, starts, ends, sites)), nsites
+
+
 def test_cover_uncovered_partial_functions(C):
     """A non-degenerate report (C5's shape, scaled down): 10% of the functions
     are touched, each on about half of its call sites, so the result holds
