@@ -34,22 +34,85 @@ All inputs are generated on the GPU and resident in HBM before the timed
 region.  value = all signal entries triaged by all ranks / max-over-ranks time.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+      N>1 either under a launcher that sets RANK / LOCAL_RANK / WORLD_SIZE /
+      MASTER_* (python -m torch.distributed.run --nproc-per-node N ... bench.py
+      --gpus N), or plain: without WORLD_SIZE, `--gpus N` starts the N rank
+      processes itself (spawn_ranks: the parent makes no GPU call, prints rank
+      0's line and exits non-zero when any rank fails).
 """
 import argparse
 import ctypes
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _gpus_arg(argv):
+    """--gpus N / --gpus=N from argv (1 when absent)."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def spawn_ranks(n, argv, poll_s=0.2, script=None):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes of
+    this script (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1,
+    a free MASTER_PORT), as children, never by exec.  This process touches no
+    GPU (it has imported neither torch nor the library).  Rank 0's stdout is
+    this process's stdout: it prints the one JSON line.  When a rank fails the
+    others are stopped (they would wait in a collective) and its exit status is
+    returned; 0 when all succeed."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        while any([p.poll() is None for p in procs]):  # (a list: poll every rank)
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(poll_s)
+        else:
+            bad = [p.returncode for p in procs if p.returncode != 0]
+            rc = bad[0] if bad else 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        print(f"bench.py: a rank failed (exit status {rc})", file=sys.stderr)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _gpus_arg(sys.argv[1:]) > 1:
+    sys.exit(spawn_ranks(_gpus_arg(sys.argv[1:]), sys.argv[1:]))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 from syzkaller_amd import _lib  # noqa: E402,F401  (fails loudly without libsyzsig.so)
 from syzkaller_amd._lib import call, lib  # noqa: E402
@@ -526,6 +589,30 @@ def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
     wall_x = time.perf_counter() - t1
     ex = [ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 3)]
     tx = [ev[i + 1].elapsed_time(ev[i + 2]) for i in range(0, len(ev), 3)]
+    roof, acct = None, None
+    if not args.no_account:
+        # the §8(d) bytes of the timed steps, with N_in = the raw PCs read: the
+        # set-exact step's flags and set updates are the executor-exact
+        # signal's, so N_uniq / N_cand / N_out are counted on that signal
+        # (outside the timed region, each trace against the starting state)
+        diff_vals = torch.empty(g.npcs, dtype=torch.int32, device="cuda")
+        diff_off = torch.empty(g.ncalls + 1, dtype=torch.int64, device="cuda")
+        per = []
+        for tr, so in zip(traces, offs):
+            call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
+                 cfg["programs"], g.ncalls, g.npcs, g.sig.data_ptr(), so.data_ptr())
+            torch.cuda.synchronize()
+            n = int(so[-1].item())
+            b = Batch(g.sig[:n], so, n, g.ncalls, None)
+            per.append(account(ctx, maxsig, m0set, newsig, [b], cfg["calls"], rec_new, diff_vals, diff_off))
+        del diff_vals, diff_off
+        acct = {k: float(np.mean([a[k] for a in per])) for k in per[0] if isinstance(per[0][k], (int, float))}
+        acct["paths_agree"] = all(a["paths_agree"] for a in per)
+        acct["n_signal"] = acct["n_in"]
+        acct["n_in"] = float(g.npcs)  # the trace read: 4 bytes per raw PC
+        roof = roofline(acct, float(np.mean(tri)), kernels, "from_traces")
+        roof["formula"] = ("4N_in (raw PCs) + 4N_uniq + 8N_cand + 4N_cand + 4N_out + N_rec/8 (SURVEY.md §8(d); "
+                           "N_uniq, N_cand, N_out counted on the executor-exact signal of the same traces)")
     del traces, offs
     torch.cuda.empty_cache()
     return {"workload": "C2 from traces: the timed step triages the batch's "
@@ -533,7 +620,7 @@ def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
                         "loads), each step against its own copy of the starting maxSignal made before the timed "
                         "region",
             "value": g.npcs * steps / wall, "unit": "raw PCs/s", "ms_per_step": wall * 1e3 / steps, "steps": steps,
-            "triage_ms_events": float(np.mean(tri)), "kernels": kernels,
+            "triage_ms_events": float(np.mean(tri)), "kernels": kernels, "roofline": roof, "accounting": acct,
             "executor_exact": {"value": g.npcs * steps / wall_x, "unit": "raw PCs/s",
                                "ms_per_step": wall_x * 1e3 / steps, "signal_per_step": units / steps,
                                "exec_ms_events": float(np.mean(ex)), "triage_ms_events": float(np.mean(tx)),

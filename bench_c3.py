@@ -17,12 +17,13 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, kernel_table, n_uniq, pmc_bytes_per_step, step_bytes,
-                   triage, HBM_PEAK_GBS, Context, SignalSet, U32_WORDS, StepTimer)
+from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, cpu_baseline, kernel_table, n_uniq, pmc_bytes_per_step,
+                   step_bytes, triage, HBM_PEAK_GBS, Context, SignalSet, U32_WORDS, StepTimer)
 from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
-                                "set_add", "prefix_or", "bucket_mark", "prefix_flags", "prefix_merge"]
+                                "set_add", "prefix_or", "bucket_mark", "prefix_flags", "prefix_merge", "set_or",
+                                "set_or_new"]
 
 
 def _cdev():
@@ -119,8 +120,10 @@ def run_c3(ctx, args, cfg, rank, world):
     ctx.timing(True)
     if side_ctx is not None:
         side_ctx.timing(True)
+    call("sg_ctx_marker", ctx.h, 0, 4)  # the timed region, for kernel traces / PMC passes (workload "c3")
     t0 = time.perf_counter()
     run(timed, states)
+    call("sg_ctx_marker", ctx.h, 1, 4)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -160,11 +163,30 @@ def run_c3(ctx, args, cfg, rank, world):
     ms_step = wall * 1e3 / args.steps
     # roofline: whole-job step bytes over all ranks / step time / aggregate peak
     bpr = step_bytes(acct) / world
+    # HBM bytes of one rank's step: the PMC section of the per-rank work (the
+    # two-phase prefix step measured at one rank, profiles/pmc_traffic.json "c3")
+    pmc_names = [k for k in kernels if k not in ("scan", "bucket_spill", "set_add")]
+    traffic, ttag = pmc_bytes_per_step(pmc_names, "c3") if prefix else (None, None)
     roof = {"bound": "hbm", "achieved": round(bpr / (ms_step / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(bpr / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(bpr / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
             "scope": "whole sharded step per GPU (wall clock, max over ranks; exchanges included)",
             "algo_bytes_per_step_per_gpu": bpr,
-            "formula": "SURVEY.md §8(d) C2/C3 bytes over all ranks / N (N_out taken as the new-signal count)"}
+            "formula": "SURVEY.md §8(d) C2/C3 bytes over all ranks / N (N_out taken as the new-signal count)",
+            "traffic_source": (f"profiles/pmc_traffic.json ({ttag}): FETCH_SIZE/WRITE_SIZE of one rank's two-phase "
+                               f"prefix step (bench.py --mode c3 --c3-two-phase at one rank, 128Ki programs), summed "
+                               f"over its kernels; RCCL traffic not included" if traffic is not None else None),
+            "traffic_over_algo": round(traffic / bpr, 3) if traffic else None}
+    cpu = None
+    if not getattr(args, "no_cpu", False):
+        # rank 0's records come first in the batch's record order: its flags
+        # are the sequential loop's over its own slice against the snapshot,
+        # which the oracle reproduces on a bounded prefix of that slice
+        if rank == 0:
+            gpu_flags = rec_new[: b.nrec].cpu().numpy()
+            cpu = cpu_baseline(m0set.export(), b, calls, gpu_flags, args.cpu_budget / 2, args.cpu_threads)
+            cpu["sample"] = "rank 0's slice: " + cpu["sample"]
+        if world > 1:
+            dist.barrier()
     if prefix:
         xgmi = last.get("exchange_bytes", 0)
     else:
@@ -201,7 +223,7 @@ def run_c3(ctx, args, cfg, rank, world):
                             f"signal-sharded x{world}") + " (one rank per GPU, RCCL)",
         },
         "roofline": roof,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "kernels": kernels,
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,

@@ -1126,6 +1126,17 @@ __device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t sl, uint32_t r
   return false;  // map (nearly) full: the bucket spills
 }
 
+// A ticket: atomicAdd(p, 1) whose result is waited for later, by take_wait.
+// (The compiler's atomic optimizer scans a plain atomicAdd's result across the
+// wave at once, so thread 0's wave waited a global round trip at every bucket
+// install while the other waves waited for it at the next barrier.)
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* p) {
+  uint32_t r;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(1u) : "memory");
+  return r;
+}
+__device__ __forceinline__ void take_wait(uint32_t& r) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r)::"memory"); }
+
 template <bool kDbg, bool kEmit>
 __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWaves))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
@@ -1153,19 +1164,22 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
   // 2 x gridDim.  Thread 0 takes each ticket a bucket before it resolves it and
   // resolves it a bucket before it is needed, so neither wait is exposed.
   const uint32_t nl = *a.nlist;
-  uint32_t pend_t = kEmpty;  // thread 0: ticket taken, not yet resolved
+  // (tickets are taken at every install, also past the list's end: waiting
+  // for the list entry before taking the next would be another round trip)
+  uint32_t pend_t = 0;  // thread 0: ticket taken, not yet resolved
   if (tid == 0) {
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
     sh_b[0] = list_bucket(a, blockIdx.x, nl, &q0);
     sh_q[0] = q0;
     sh_b[1] = list_bucket(a, gridDim.x + blockIdx.x, nl, &q1);
     sh_q[1] = q1;
-    pend_t = 2 * gridDim.x + atomicAdd(a.ticket, 1u);
+    pend_t = take_ticket(a.ticket);
   }
   __syncthreads();
   uint32_t b = uni(sh_b[0]), b1 = uni(sh_b[1]);
   uint4 q = uni(sh_q[0]), q1 = uni(sh_q[1]);
   if (b >= kNumBuckets) {
+    if (tid == 0) take_wait(pend_t);
     if (kDbg && tid == 0) {
       for (int j = 0; j < 8; j++) a.dbg[8 * blockIdx.x + j] = 0;
       a.dbg[8 * blockIdx.x] = t_start;
@@ -1198,8 +1212,9 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
     uint32_t pend_b = kNumBuckets;
     uint4 pend_q = make_uint4(0, 0, 0, 0);
     if (tid == 0) {
-      pend_b = list_bucket(a, pend_t, nl, &pend_q);
-      pend_t = pend_b < kNumBuckets ? 2 * gridDim.x + atomicAdd(a.ticket, 1u) : kEmpty;
+      take_wait(pend_t);  // (taken a bucket ago; the install waited for older loads already)
+      pend_b = list_bucket(a, 2 * gridDim.x + pend_t, nl, &pend_q);
+      pend_t = take_ticket(a.ticket);
       sh_fail = 0;  // (every wave read the previous bucket's before the barrier above)
     }
     lds_barrier();
@@ -1224,6 +1239,8 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       // this thread's kBU consecutive entries: the new-signal test (fuzzer.go:666),
       // all LDS reads issued before the first use
       const uint32_t p0 = round_pos(base, 0);
+      // (the spill flag read with the slice words: one LDS wait for both)
+      const uint32_t failed = __hip_atomic_load(&sh_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       uint32_t mw[kBU];
 #pragma unroll
       for (int u = 0; u < kBU; u++) mw[u] = mslice[x[u] >> 21];
@@ -1262,7 +1279,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
 #pragma unroll
         for (int u = 0; u < kBU; u++) gu[u] = gu[u] ? gu[u] - 1 : 0u;
       }
-      if (cm && __hip_atomic_load(&sh_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+      if (cm && failed == 0) {
         if (NG > 64) {  // the groups by search, stepped forward
           uint32_t g = group_of(gb, NG, p0 + __builtin_ctz(cm));
           uint32_t nb = g + 1 < NG ? gb[g + 1] : kEmpty;  // next boundary

@@ -676,6 +676,7 @@ int sg_set_or_dev(sg_set* set, const uint32_t* d_words) {
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
+  ScopedTimer tm(ctx, "set_or");
   hipLaunchKernelGGL(k_set_or, dim3(4096), dim3(256), 0, ctx->stream, set->words, d_words);
   SG_HIP(hipGetLastError());
   return SG_OK;
@@ -692,6 +693,7 @@ int sg_set_or_new_dev(sg_set* set, const uint32_t* d_words, sg_set* exclude) {
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
+  ScopedTimer tm(ctx, "set_or_new");
   hipLaunchKernelGGL(k_set_or_new, dim3(4096), dim3(256), 0, ctx->stream, set->words, d_words, exclude->words);
   SG_HIP(hipGetLastError());
   return SG_OK;
