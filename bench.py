@@ -258,7 +258,7 @@ def pmc_bytes_per_step(kernels, workload):
             seen.append(k)
         elif k not in ("scan", "bucket_spill"):  # a summary of another kernel set: stale
             return None, None
-    return (tot if seen else None), f"{d.get('tag')}/{workload}"
+    return (tot if seen else None), f"{w.get('tag', d.get('tag'))}/{workload}"
 
 
 class StepTimer:

@@ -166,7 +166,8 @@ def run_c3(ctx, args, cfg, rank, world):
     # HBM bytes of one rank's step: the PMC section of the per-rank work (the
     # two-phase prefix step measured at one rank, profiles/pmc_traffic.json "c3")
     pmc_names = [k for k in kernels if k not in ("scan", "bucket_spill", "set_add")]
-    traffic, ttag = pmc_bytes_per_step(pmc_names, "c3") if prefix else (None, None)
+    # (measured at the default 128Ki programs per rank: another size has no section)
+    traffic, ttag = pmc_bytes_per_step(pmc_names, "c3") if prefix and nprog == 131072 else (None, None)
     roof = {"bound": "hbm", "achieved": round(bpr / (ms_step / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(bpr / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
             "scope": "whole sharded step per GPU (wall clock, max over ranks; exchanges included)",

@@ -1174,6 +1174,11 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
     sh_b[1] = list_bucket(a, gridDim.x + blockIdx.x, nl, &q1);
     sh_q[1] = q1;
     pend_t = take_ticket(a.ticket);
+    // (waited for here, once: a ticket register flowing into the loop may be
+    // copied by the compiler before the atomic returns; inside the loop it is
+    // written by the atomic and read at the next install only -- check the ISA
+    // for a v_mov of it after any change here)
+    take_wait(pend_t);
   }
   __syncthreads();
   uint32_t b = uni(sh_b[0]), b1 = uni(sh_b[1]);
@@ -1215,6 +1220,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       take_wait(pend_t);  // (taken a bucket ago; the install waited for older loads already)
       pend_b = list_bucket(a, 2 * gridDim.x + pend_t, nl, &pend_q);
       pend_t = take_ticket(a.ticket);
+      if (kEmit) take_wait(pend_t);  // (this form spills; a spilled ticket must have landed)
       sh_fail = 0;  // (every wave read the previous bucket's before the barrier above)
     }
     lds_barrier();
