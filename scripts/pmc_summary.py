@@ -9,7 +9,7 @@ Per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half of the bytes of a wide coalesced streaming read, so the
 read side is doubled ("fetch_bytes_x2"); the raw value is kept too.
 
-usage: pmc_summary.py FETCH.csv WRITE.csv OUT.json TAG [workloads=c2,from_traces,steady] [merge]
+usage: pmc_summary.py FETCH.csv WRITE.csv OUT.json TAG [workloads=c2,from_traces,steady] [merge] [steps=2]
 ("merge": keep OUT.json's other workload sections; each section records its
 own tag and sources)"""
 import csv
@@ -43,8 +43,9 @@ def load(path, counter, nregions):
     return out
 
 
-def main(fetch_csv, write_csv, out_json, tag, workloads="c2,from_traces,steady", merge=""):
+def main(fetch_csv, write_csv, out_json, tag, workloads="c2,from_traces,steady", merge="", steps="2"):
     names = workloads.split(",")
+    steps = int(steps)  # timed steps per region (the PMC passes run bench.py --steps 2)
     old = {}
     if merge == "merge":
         try:
@@ -66,9 +67,9 @@ def main(fetch_csv, write_csv, out_json, tag, workloads="c2,from_traces,steady",
             if not fb or not wb:
                 continue
             fetch, write = sum(fb) / len(fb), sum(wb) / len(wb)
-            sec[k] = {"launches": len(fb), "fetch_bytes_raw": fetch, "fetch_bytes_x2": 2 * fetch,
-                      "write_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write}
-        res["workloads"][name] = {"kernels": sec, "tag": tag, "source": [fetch_csv, write_csv]}
+            sec[k] = {"launches": len(fb), "launches_per_step": len(fb) / steps, "fetch_bytes_raw": fetch,
+                      "fetch_bytes_x2": 2 * fetch, "write_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write}
+        res["workloads"][name] = {"kernels": sec, "tag": tag, "source": [fetch_csv, write_csv], "steps": steps}
     if old:
         for name, sec in old.get("workloads", {}).items():
             if name not in res["workloads"]:
@@ -79,4 +80,4 @@ def main(fetch_csv, write_csv, out_json, tag, workloads="c2,from_traces,steady",
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:7])
+    main(*sys.argv[1:8])
