@@ -497,6 +497,12 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->gen_prob) hipFree(ctx->gen_prob);
   if (ctx->gen_alias) hipFree(ctx->gen_alias);
   if (ctx->gen_perm) hipFree(ctx->gen_perm);
+  if (ctx->copy_stream) {
+    hipStreamSynchronize(ctx->copy_stream);
+    for (auto e : ctx->pipe_ev)
+      if (e) hipEventDestroy(e);
+    hipStreamDestroy(ctx->copy_stream);
+  }
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

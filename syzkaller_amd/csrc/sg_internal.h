@@ -88,6 +88,10 @@ struct sg_ctx {
   // grow-only device staging for the host entry points' inputs / outputs
   void* dstage = nullptr;
   size_t dstage_cap = 0;
+  // the host ingest pipeline (sg_host.hip): its copy stream and the events
+  // between the two staging slots' DMA and triage
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t pipe_ev[4] = {};
   // first-owner table and its decreasing key floor; the key space is 2^32 - 1
   // (SG_OWNER_KEY_SPACE lowers it, so tests reach the generation reset)
   uint32_t* owner = nullptr;
@@ -188,6 +192,11 @@ struct OwnerJob {
 int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint64_t* d_cmask, uint64_t* d_dmask,
                         uint32_t* d_tile_rec, uint8_t* d_seg_flag, uint32_t* set_a, uint32_t* set_b);
 
+// A batch in host memory through pinned double-buffered staging, record
+// slice by record slice, each slice's copies overlapping the previous one's
+// partitioned triage (sg_host.hip); takes the ctx lock.
+int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* vals, const uint64_t* rec_off,
+                  uint64_t nrec, uint8_t* rec_new, bool trace);
 // Partitioned flags-only triage (sg_bucket.hip); ctx lock held.  trace:
 // d_vals are raw per-call PC traces, triaged by their edge signal.
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,

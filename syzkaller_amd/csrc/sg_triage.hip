@@ -694,6 +694,13 @@ int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t*
     }
   if (nvals && !vals) return SG_EINVAL;
   bool want_diff = diff_vals || diff_off || n_diff;
+  if (!want_diff) {  // flags and set updates: the pipelined ingest (sg_host.hip)
+    if (maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {
+      set_error("sg_triage_batch: set belongs to another context");
+      return SG_EINVAL;
+    }
+    return host_pipeline(ctx, maxsig->words, newsig ? newsig->words : nullptr, vals, rec_off, nrec, rec_new, false);
+  }
   // device staging: vals, off, rec_new, diff_vals, diff_off  (pipeline scratch
   // is carved behind these by the _dev entry point, which reserves again).
   uint32_t* dv;
@@ -769,27 +776,13 @@ int sg_triage_traces(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t
     }
   const uint64_t npcs = call_off[ncalls];
   if (npcs && !pcs) return SG_EINVAL;
-  const size_t b_pcs = (npcs * 4 + 255) & ~size_t(255), b_off = ((ncalls + 1) * 8 + 255) & ~size_t(255),
-               b_flag = (ncalls + 256) & ~size_t(255);
-  char* stage = nullptr;
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    int rc = check_alloc(ctx);
-    if (rc) return rc;
-    rc = dstage_reserve(ctx, b_pcs + b_off + b_flag + 256);
-    if (rc) return rc;
-    stage = (char*)ctx->dstage;
+  if (maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {
+    set_error("sg_triage_traces: set belongs to another context");
+    return SG_EINVAL;
   }
-  uint32_t* dp = (uint32_t*)stage;
-  uint64_t* doff = (uint64_t*)(stage + b_pcs);
-  uint8_t* dflag = (uint8_t*)(stage + b_pcs + b_off);
-  if (npcs) SG_HIP(hipMemcpyAsync(dp, pcs, npcs * 4, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemcpyAsync(doff, call_off, (ncalls + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-  int rc = sg_triage_traces_dev(ctx, maxsig, newsig, dp, doff, npcs, ncalls, dflag);
-  if (rc) return rc;
-  if (ncalls) SG_HIP(hipMemcpyAsync(rec_new, dflag, ncalls, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  return SG_OK;
+  // the pipelined ingest (sg_host.hip): record (call) slices, each a trace slice
+  // starting at a call start
+  return host_pipeline(ctx, maxsig->words, newsig ? newsig->words : nullptr, pcs, call_off, ncalls, rec_new, true);
 }
 
 int sg_set_diff(sg_set* set, const uint32_t* sig, size_t n, uint32_t* out, size_t* nout) {
