@@ -721,7 +721,65 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
         torch.cuda.synchronize()
         out["cpu_baseline"] = cpu_baseline(m0set.export(), timed[0], calls, rec_new[: timed[0].nrec].cpu().numpy(),
                                            args.cpu_budget / 2, args.cpu_threads)
+    del batches, timed
+    torch.cuda.empty_cache()
+    if args.from_traces:
+        out["from_traces"] = run_steady_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, min(args.steps, 4))
     return out
+
+
+def run_steady_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
+    """The steady state end to end from raw traces, the way the fuzzer
+    consumes them: the set-exact triage's flags and set updates, then the
+    executor-exact per-call lists of the queued records only (fuzzer.go:678-683
+    copies inf.Signal only for them), by sg_exec_signal_queued_dev; against the
+    triage alone and against executor-exact lists of every call."""
+    traces = []
+    for k in range(steps):
+        call("sg_gen_population_traces_dev", ctx.h, UNIVERSE_SEED, POP_SEED, args.npop, 5_000 + args.warmup + k,
+             args.noise, cfg["zipf_s"], cfg["ranks"], 0, cfg["programs"], cfg["calls"], cfg["pcs_per_call"],
+             g.trace.data_ptr())
+        traces.append(g.trace.clone())
+    so = torch.empty(g.ncalls + 1, dtype=torch.int64, device="cuda")
+    states = [SignalSet(ctx) for _ in traces]
+    res = {}
+    queued = []
+    for mode in ("flags", "flags+queued", "flags+all"):
+        for st in states:
+            call("sg_set_copy", st.h, m0set.h)
+        torch.cuda.synchronize()
+        ev = []
+        for tr, st in zip(traces, states):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append(e)
+            call("sg_triage_traces_dev", ctx.h, st.h, newsig.h, tr.data_ptr(), g.call_off.data_ptr(), g.npcs,
+                 g.ncalls, rec_new.data_ptr())
+            if mode == "flags+queued":
+                call("sg_exec_signal_queued_dev", ctx.h, tr.data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
+                     cfg["programs"], g.ncalls, g.npcs, rec_new.data_ptr(), g.sig.data_ptr(), so.data_ptr())
+            elif mode == "flags+all":
+                call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
+                     cfg["programs"], g.ncalls, g.npcs, g.sig.data_ptr(), so.data_ptr())
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append(e)
+            if mode == "flags":
+                queued.append(rec_new[: g.ncalls].view(cfg["programs"], cfg["calls"]).clone())
+        torch.cuda.synchronize()
+        res[mode] = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 2)]))
+    for st in states:
+        st.close()
+    q = torch.stack(queued).to(torch.float32)
+    del traces
+    torch.cuda.empty_cache()
+    return {"workload": f"steady state from {g.npcs} resident raw PCs per step: sg_triage_traces_dev (flags, set "
+                        "updates), then sg_exec_signal_queued_dev (executor-exact lists of the queued records)",
+            "steps": steps, "ms_flags": res["flags"], "ms_flags_queued_lists": res["flags+queued"],
+            "ms_flags_all_lists": res["flags+all"], "queued_lists_over_flags": res["flags+queued"] / res["flags"],
+            "queued_record_frac": float(q.mean().item()),
+            "programs_with_queued_frac": float((q.amax(2) > 0).float().mean().item()),
+            "value": g.npcs / (res["flags+queued"] / 1e3), "unit": "raw PCs/s"}
 
 
 def main():

@@ -354,6 +354,16 @@ int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, c
 		   size_t nprog, uint32_t* sig_vals, uint64_t* sig_off);
 int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
 		       uint64_t nprog, uint64_t ncalls, uint64_t npcs, uint32_t* d_sig_vals, uint64_t* d_sig_off);
+/* The executor-exact lists of the queued calls only (syz-fuzzer/fuzzer.go:678-683
+ * copies inf.Signal of a record only when it is queued for triage): after a
+ * set-exact triage of the same traces (sg_triage_traces_dev, flags d_rec_new),
+ * call c's list is exactly sg_exec_signal_dev's when d_rec_new[c] != 0 and
+ * empty otherwise.  Each program runs its calls up to its last queued one (the
+ * executor's table state at a call depends only on the calls before it);
+ * programs without a queued call do not run.  Layout as sg_exec_signal_dev. */
+int sg_exec_signal_queued_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off,
+			      const uint64_t* d_prog_off, uint64_t nprog, uint64_t ncalls, uint64_t npcs,
+			      const uint8_t* d_rec_new, uint32_t* d_sig_vals, uint64_t* d_sig_off);
 
 /* ---- synthetic Zipf traces (bench / test input generator) ----------------- */
 /* Zipf(s) over `nranks` PC ranks mapped through a permutation seeded by

@@ -96,6 +96,8 @@ SIGNATURES = {
     "sg_exec_signal": (c_int, [c_void_p, P32, P64, P64, c_size_t, P32, P64]),
     "sg_exec_signal_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
                                    c_void_p]),
+    "sg_exec_signal_queued_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
+                                          c_void_p, c_void_p]),
     "sg_gen_zipf_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_double, c_uint32, c_uint64, c_uint64, c_uint32,
                                        c_uint32, c_void_p]),
     "sg_gen_population_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_double, c_double,

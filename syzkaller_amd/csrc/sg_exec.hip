@@ -102,22 +102,29 @@ __device__ __forceinline__ unsigned long long mark_val(uint32_t pos, uint32_t d,
 
 // kCount (diagnostics, SG_DEBUG_PART): stats[0..2] += windows, speculative
 // passes, edges of the wave's program.
+// pstop (nullable): the wave runs its program's calls [prog_off[p], pstop[p])
+// only -- the executor's table state at a call depends on the calls before it,
+// never on later ones; emit (nullable): only calls with emit[c] != 0 write
+// their signal (the others still update the table; cnt[c] stays 0).
 template <bool kCount>
 __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__ pcs,
                                                     const uint64_t* __restrict__ call_off,
                                                     const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
-                                                    uint32_t* __restrict__ cnt, unsigned long long* stats) {
+                                                    uint32_t* __restrict__ cnt, unsigned long long* stats,
+                                                    const uint64_t* __restrict__ pstop = nullptr,
+                                                    const uint8_t* __restrict__ emit = nullptr) {
   uint64_t n_win = 0, n_pass = 0, n_edge = 0;
   __shared__ uint32_t table[kDedupSize];
   __shared__ unsigned long long markA[kMarkN], markB[kMarkN];
   const int lane = threadIdx.x;
   const uint32_t pos0 = (uint32_t)lane, pos1 = 64u + (uint32_t)lane;
   const uint64_t p = blockIdx.x;
+  const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
+  if (c1 <= c0) return;  // (one wave: the whole workgroup leaves)
   for (uint32_t i = lane; i < kDedupSize; i += 64) table[i] = 0;
   for (uint32_t i = lane; i < kMarkN; i += 64) markA[i] = markB[i] = kNoMark;
   __syncthreads();
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint64_t c0 = prog_off[p], c1 = prog_off[p + 1];
   // the program's calls are contiguous in the trace: the next 128 PCs are
   // always in flight (the next window of this call, or the next call's first)
   const uint64_t pend = call_off[c1];
@@ -125,6 +132,7 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
   uint32_t npc0 = w0 + pos0 < pend ? pcs[w0 + pos0] : 0u, npc1 = w0 + pos1 < pend ? pcs[w0 + pos1] : 0u;
   for (uint64_t c = c0; c < c1; c++) {
     const uint64_t b = call_off[c], e = call_off[c + 1];
+    const bool em = !emit || emit[c] != 0;
     uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
     uint64_t outpos = b;
     for (uint64_t j = b; j < e; j += 128) {
@@ -218,10 +226,12 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
       // the (exec-masked, so branched-around) stores keeps the wait off the
       // next window's critical path
       asm volatile("" ::"v"(npc0), "v"(npc1));
-      if ((keep0 >> lane) & 1ull) tmp[outpos + __popcll(keep0 & lt)] = sig0;
-      outpos += __popcll(keep0);
-      if ((keep1 >> lane) & 1ull) tmp[outpos + __popcll(keep1 & lt)] = sig1;
-      outpos += __popcll(keep1);
+      if (em) {
+        if ((keep0 >> lane) & 1ull) tmp[outpos + __popcll(keep0 & lt)] = sig0;
+        outpos += __popcll(keep0);
+        if ((keep1 >> lane) & 1ull) tmp[outpos + __popcll(keep1 & lt)] = sig1;
+        outpos += __popcll(keep1);
+      }
     }
     if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
   }
@@ -230,6 +240,23 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
     atomicAdd(&stats[1], (unsigned long long)n_pass);
     atomicAdd(&stats[2], (unsigned long long)n_edge);
   }
+}
+
+// the calls each program has to run for its queued calls' lists: up to and
+// including its last queued call (fuzzer.go:678-683 copies the signal of
+// queued records only); pstop[p] = prog_off[p] when it has none
+__global__ void k_prog_stop(const uint64_t* __restrict__ prog_off, const uint8_t* __restrict__ rec_new, uint64_t nprog,
+                            uint64_t* __restrict__ pstop) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nprog) return;
+  const uint64_t c0 = prog_off[p];
+  uint64_t stop = c0;
+  for (uint64_t c = prog_off[p + 1]; c > c0; c--)
+    if (rec_new[c - 1]) {
+      stop = c;
+      break;
+    }
+  pstop[p] = stop;
 }
 
 // dense CSR from the per-call capacity layout: one wave per call
@@ -359,9 +386,9 @@ using namespace sg;
 
 extern "C" {
 
-int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
-                       uint64_t nprog, uint64_t ncalls, uint64_t npcs, uint32_t* d_sig_vals, uint64_t* d_sig_off) {
-  if (!ctx || !d_call_off || !d_prog_off || !d_sig_off || (npcs && (!d_pcs || !d_sig_vals))) return SG_EINVAL;
+static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
+                       uint64_t nprog, uint64_t ncalls, uint64_t npcs, const uint8_t* d_rec_new, uint32_t* d_sig_vals,
+                       uint64_t* d_sig_off) {
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
@@ -370,19 +397,23 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
     return SG_OK;
   }
   WsPlan p;
-  size_t o_tmp = p.add(npcs * 4), o_cnt = p.add(ncalls * 4);
+  size_t o_tmp = p.add(npcs * 4), o_cnt = p.add(ncalls * 4), o_stop = p.add(d_rec_new ? nprog * 8 : 0);
   size_t scan_off = p.total;
   rc = ws_reserve(ctx, p.total + scan_ws_bytes(ncalls));
   if (rc) return rc;
   uint32_t* tmp = (uint32_t*)ws_at(ctx, o_tmp);
   uint32_t* cnt = (uint32_t*)ws_at(ctx, o_cnt);
+  uint64_t* pstop = d_rec_new ? (uint64_t*)ws_at(ctx, o_stop) : nullptr;
   SG_HIP(hipMemsetAsync(cnt, 0, ncalls * 4, ctx->stream));
+  if (pstop && nprog)
+    hipLaunchKernelGGL(k_prog_stop, dim3(div_up(nprog, 256)), dim3(256), 0, ctx->stream, d_prog_off, d_rec_new, nprog,
+                       pstop);
   if (nprog && ctx->debug_part) {  // diagnostics: speculative passes per 128-edge window (syncs)
     unsigned long long* st = nullptr;
     SG_HIP(hipMalloc(&st, 32));
     SG_HIP(hipMemsetAsync(st, 0, 32, ctx->stream));
     hipLaunchKernelGGL(k_exec_signal<true>, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off,
-                       d_prog_off, tmp, cnt, st);
+                       d_prog_off, tmp, cnt, st, (const uint64_t*)pstop, d_rec_new);
     unsigned long long h[3] = {0, 0, 0};
     SG_HIP(hipMemcpy(h, st, 24, hipMemcpyDeviceToHost));
     SG_HIP(hipFree(st));
@@ -391,7 +422,7 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   } else if (nprog) {
     ScopedTimer tm(ctx, "exec_signal");
     hipLaunchKernelGGL(k_exec_signal<false>, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off,
-                       d_prog_off, tmp, cnt, (unsigned long long*)nullptr);
+                       d_prog_off, tmp, cnt, (unsigned long long*)nullptr, (const uint64_t*)pstop, d_rec_new);
   }
   SG_HIP(hipGetLastError());
   rc = scan_counts(ctx, cnt, d_sig_off, ncalls, scan_off);
@@ -403,6 +434,23 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   }
   SG_HIP(hipGetLastError());
   return SG_OK;
+}
+
+int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off, const uint64_t* d_prog_off,
+                       uint64_t nprog, uint64_t ncalls, uint64_t npcs, uint32_t* d_sig_vals, uint64_t* d_sig_off) {
+  if (!ctx || !d_call_off || !d_prog_off || !d_sig_off || (npcs && (!d_pcs || !d_sig_vals))) return SG_EINVAL;
+  return exec_signal(ctx, d_pcs, d_call_off, d_prog_off, nprog, ncalls, npcs, nullptr, d_sig_vals, d_sig_off);
+}
+
+int sg_exec_signal_queued_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off,
+                              const uint64_t* d_prog_off, uint64_t nprog, uint64_t ncalls, uint64_t npcs,
+                              const uint8_t* d_rec_new, uint32_t* d_sig_vals, uint64_t* d_sig_off) {
+  if (!ctx || !d_call_off || !d_prog_off || !d_sig_off || (npcs && (!d_pcs || !d_sig_vals)) ||
+      (ncalls && !d_rec_new)) {
+    set_error("sg_exec_signal_queued_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  return exec_signal(ctx, d_pcs, d_call_off, d_prog_off, nprog, ncalls, npcs, d_rec_new, d_sig_vals, d_sig_off);
 }
 
 int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, const uint64_t* prog_off,

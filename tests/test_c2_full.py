@@ -56,7 +56,8 @@ def test_c2_full_batch_steady_state_vs_oracle(ctx):
     nvals, nrec = sig.numel(), off.numel() - 1
     assert nrec == nprog * calls and nvals > 800_000_000  # the C2 shape
     ms, ns = SignalSet(ctx), SignalSet(ctx)
-    call("sg_set_add_dev", ms.h, torch.from_numpy(m0.view(np.int32)).cuda().data_ptr(), m0.size)
+    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernel has read it)
+    call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
     call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
          None, None)
@@ -102,7 +103,8 @@ def test_c2_full_fresh_batch_sets_vs_oracle(ctx):
     del trace
     nvals, nrec = sig.numel(), off.numel() - 1
     ms, ns = SignalSet(ctx), SignalSet(ctx)
-    call("sg_set_add_dev", ms.h, torch.from_numpy(m0.view(np.int32)).cuda().data_ptr(), m0.size)
+    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernel has read it)
+    call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
     call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
          None, None)

@@ -47,7 +47,8 @@ def _dev_reference(ctx, m0, d_vals, d_off, trace):
     from syzkaller_amd.cover import SignalSet
 
     ms, ns = SignalSet(ctx), SignalSet(ctx)
-    call("sg_set_add_dev", ms.h, torch.from_numpy(m0.view(np.int32)).cuda().data_ptr(), m0.size)
+    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernel has read it)
+    call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
     nrec = d_off.numel() - 1
     flags = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
     if trace:

@@ -178,3 +178,77 @@ def test_traces_record_slices(C, monkeypatch):
     finally:
         ctx.close()
         monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
+
+
+def test_exec_signal_queued_lists(C, ctx):
+    """sg_exec_signal_queued_dev after a set-exact trace triage: each queued
+    call's list equals the executor-exact list (sg_exec_signal_dev, pinned to
+    the compiled reference executor), every other call's list is empty
+    (fuzzer.go:678-683 copies the signal of queued records only).  A steady
+    population batch, so programs hold queued calls at any position, none,
+    or several; then the oracle on a small ragged batch."""
+    import torch
+
+    from syzkaller_amd._lib import call
+
+    nprog, calls, pcs, npop = 4096, 16, 1024, 512
+    n, ncalls = nprog * calls * pcs, nprog * calls
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    tr = torch.empty(n, dtype=torch.int32, device="cuda")
+    call("sg_gen_zipf_traces_dev", ctx.h, 0x5A17C0DE, 0x9091A7E5, 1.1, 1 << 20, 0, npop, calls, pcs, tr.data_ptr())
+    co = torch.arange(0, n + 1, pcs, dtype=torch.int64, device="cuda")
+    po = torch.arange(0, ncalls + 1, calls, dtype=torch.int64, device="cuda")
+    sig = torch.empty(n, dtype=torch.int32, device="cuda")
+    so = torch.empty(ncalls + 1, dtype=torch.int64, device="cuda")
+    call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), co.data_ptr(), po.data_ptr(), npop, npop * calls, npop * calls * pcs,
+         sig.data_ptr(), so.data_ptr())
+    torch.cuda.synchronize()
+    m0 = np.unique(sig[: int(so[npop * calls].item())].cpu().numpy().view(np.uint32))
+    call("sg_gen_population_traces_dev", ctx.h, 0x5A17C0DE, 0x9091A7E5, npop, 6_001, 2e-4, 1.1, 1 << 20, 0, nprog,
+         calls, pcs, tr.data_ptr())
+    ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
+    C.SignalAdd(ms, m0)
+    flags = torch.zeros(ncalls, dtype=torch.uint8, device="cuda")
+    call("sg_triage_traces_dev", ctx.h, ms.h, ns.h, tr.data_ptr(), co.data_ptr(), n, ncalls, flags.data_ptr())
+    call("sg_exec_signal_dev", ctx.h, tr.data_ptr(), co.data_ptr(), po.data_ptr(), nprog, ncalls, n, sig.data_ptr(),
+         so.data_ptr())
+    qsig = torch.empty(n, dtype=torch.int32, device="cuda")
+    qso = torch.empty(ncalls + 1, dtype=torch.int64, device="cuda")
+    call("sg_exec_signal_queued_dev", ctx.h, tr.data_ptr(), co.data_ptr(), po.data_ptr(), nprog, ncalls, n,
+         flags.data_ptr(), qsig.data_ptr(), qso.data_ptr())
+    torch.cuda.synchronize()
+    f = flags.cpu().numpy().astype(bool)
+    assert 0.01 < f.mean() < 0.9
+    fp = f.reshape(nprog, calls)
+    assert fp.any(1).mean() < 1.0 and (fp.sum(1) > 1).any()  # programs with none / several queued calls
+    full_off, q_off = so.cpu().numpy(), qso.cpu().numpy()
+    full_len, q_len = np.diff(full_off), np.diff(q_off)
+    assert np.array_equal(q_len, np.where(f, full_len, 0))
+    fv, qv = sig.cpu().numpy(), qsig.cpu().numpy()
+    idx = np.flatnonzero(f)
+    src = np.concatenate([np.arange(full_off[c], full_off[c + 1]) for c in idx])
+    assert np.array_equal(qv[: q_off[-1]], fv[src])
+    ms.close()
+    ns.close()
+    # the oracle, a small ragged batch with arbitrary flags
+    rng = np.random.default_rng(707)
+    lens = rng.integers(0, 300, size=48)
+    call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    prog_off = np.array([0, 5, 5, 17, 30, 48], np.uint64)
+    p = _zipf_pcs(rng, int(call_off[-1]), nranks=1 << 10)
+    es, eo = O.exec_signal(p, call_off, prog_off)
+    fl = (rng.random(48) < 0.3).astype(np.uint8)
+    # (device copies held in names: a temporary's memory could be reused
+    # before the kernel reads it)
+    dp, dco, dpo = (torch.from_numpy(a.view(t)).cuda() for a, t in ((p, np.int32), (call_off, np.int64),
+                                                                     (prog_off, np.int64)))
+    dfl = torch.from_numpy(fl).cuda()
+    dq = torch.empty(max(int(call_off[-1]), 1), dtype=torch.int32, device="cuda")
+    dqo = torch.empty(49, dtype=torch.int64, device="cuda")
+    call("sg_exec_signal_queued_dev", ctx.h, dp.data_ptr(), dco.data_ptr(), dpo.data_ptr(), 5, 48, int(call_off[-1]),
+         dfl.data_ptr(), dq.data_ptr(), dqo.data_ptr())
+    torch.cuda.synchronize()
+    got_off, got = dqo.cpu().numpy().view(np.uint64), dq.cpu().numpy().view(np.uint32)
+    for c in range(48):
+        want = es[eo[c]:eo[c + 1]] if fl[c] else np.zeros(0, np.uint32)
+        assert np.array_equal(got[got_off[c]:got_off[c + 1]], want), c
