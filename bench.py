@@ -799,6 +799,10 @@ def main():
     ap.add_argument("--no-from-traces", dest="from_traces", action="store_false")
     ap.add_argument("--c3-proto", choices=["prefix", "pairs"], default="prefix",
                     help="C3 protocol: bitmap prefixes (default) or candidate pairs hash-sharded by signal")
+    ap.add_argument("--c3-form", choices=["auto", "kept", "pairs"], default="auto",
+                    help="the prefix protocol's per-batch step-1 form (auto: by the last batch's novelty)")
+    ap.add_argument("--c3-steady", action="store_true",
+                    help="measurement: C3 over steady-state batches (a fixed population with flaky coverage)")
     ap.add_argument("--c3-two-phase", action="store_true",
                     help="measurement: the prefix protocol's two-phase path at one rank too")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of single-thread CPU baseline work")

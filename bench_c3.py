@@ -51,14 +51,29 @@ def run_c3(ctx, args, cfg, rank, world):
     t_gen = time.perf_counter()
     # the replicated snapshot: every rank builds the same 16M-entry maxSignal
     # from the same warm batch (deterministic, so no broadcast is needed)
-    warm = g.zipf(ctx, dict(cfg, programs=nprog), 2_000_000, prog_base=0)
-    batches = [g.zipf(ctx, cfg, 3_000 + k, prog_base=rank * nprog) for k in range(args.warmup + args.steps)]
+    steady = getattr(args, "c3_steady", False)
+    maxsig, newsig, m0set = SignalSet(ctx), SignalSet(ctx), SignalSet(ctx)
+    if steady:
+        # the low-novelty steady state (bench.py run_steady's recipe): maxSignal
+        # = the population's signal, batches of population programs re-executed
+        # with flaky coverage
+        rec_new = torch.empty(nprog * calls, dtype=torch.uint8, device="cuda")
+        step = max(1, min(nprog, args.npop))
+        for m in range(0, args.npop, step):
+            mb = g.members(ctx, cfg, m, min(args.npop, m + step))
+            triage(ctx, m0set, None, mb, rec_new)
+            torch.cuda.synchronize()
+            del mb
+        batches = [g.population(ctx, cfg, 5_000 + k, args.npop, args.noise, prog_base=rank * nprog)
+                   for k in range(args.warmup + args.steps)]
+    else:
+        warm = g.zipf(ctx, dict(cfg, programs=nprog), 2_000_000, prog_base=0)
+        batches = [g.zipf(ctx, cfg, 3_000 + k, prog_base=rank * nprog) for k in range(args.warmup + args.steps)]
+        rec_new = torch.empty(max(b.nrec for b in batches), dtype=torch.uint8, device="cuda")
+        build_m0(ctx, m0set, warm, calls, args.m0, rec_new)
+        del warm
     del g
     t_gen = time.perf_counter() - t_gen
-    rec_new = torch.empty(max(b.nrec for b in batches), dtype=torch.uint8, device="cuda")
-    maxsig, newsig, m0set = SignalSet(ctx), SignalSet(ctx), SignalSet(ctx)
-    build_m0(ctx, m0set, warm, calls, args.m0, rec_new)
-    del warm
     m0_count = len(m0set)
     if world > 1:
         counts = [torch.zeros(1, dtype=torch.int64, device=_cdev()) for _ in range(world)]
@@ -78,9 +93,11 @@ def run_c3(ctx, args, cfg, rank, world):
             side_ctx = Context(ctx.device)
             with torch.cuda.stream(side):
                 side_st = HipStages(side_ctx)
-        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=two_phase, side_stages=side_st, side_stream=side)
+        tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=two_phase, side_stages=side_st, side_stream=side,
+                           form=getattr(args, "c3_form", "auto"))
     else:
         tri = ShardedTriage(HipStages(ctx), Comm())
+    forms = []  # the prefix protocol's step-1 form per batch
     rec_base = rank * nprog * calls
     nrec_total = world * nprog * calls
     # every step runs against the restored snapshot: overlapped steps use a
@@ -100,6 +117,8 @@ def run_c3(ctx, args, cfg, rank, world):
                 tri.step(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
                 continue
             p = tri.start(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_news[i % 2], nrec_total)
+            if prefix:
+                forms.append(p["last"].get("form"))
             if pend is not None:
                 tri.finish(pend)
             pend = p
@@ -228,6 +247,7 @@ def run_c3(ctx, args, cfg, rank, world):
         "kernels": kernels,
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,
+        "prefix_forms": forms[-args.steps:] if prefix and forms else None,
         "path": ("prefix (syzkaller_amd/shard.py PrefixTriage)" if prefix else
                  "sharded (syzkaller_amd/shard.py ShardedTriage + sg_shard.hip)"),
         "gen_s": round(t_gen, 2),

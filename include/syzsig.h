@@ -218,6 +218,16 @@ int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t npart
  * the slot. */
 int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks, const uint32_t* d_vals,
 			const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec);
+/* sg_prefix_begin_dev with the batch's form chosen by the caller (there:
+ * SG_PREFIX_PAIRS): form 0 keeps the batch's partitions (end re-runs the bucket
+ * stage against maxsig | d_prefix), form 1 its distinct signals not in base
+ * with their first records (end tests those pairs; cheaper when few).  The
+ * results are the same.  d_ncand (nullable, device u64) receives the number of
+ * distinct signals of the batch not in base -- the novelty a caller picks the
+ * next batch's form from (syzkaller_amd/shard.py PrefixTriage). */
+int sg_prefix_begin_form_dev(sg_ctx* ctx, uint32_t slot, uint32_t form, sg_set* base, sg_set* marks,
+			     const uint32_t* d_vals, const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec,
+			     uint64_t* d_ncand);
 int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
 		      uint8_t* d_rec_new);
 int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix,

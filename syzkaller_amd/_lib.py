@@ -71,6 +71,8 @@ SIGNATURES = {
     "sg_prefix_begin_dev": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64]),
     "sg_prefix_end_dev": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sg_prefix_flags_dev": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
+    "sg_prefix_begin_form_dev": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64,
+                                         c_uint64, c_void_p]),
     "sg_add_inputs": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, c_size_t]),
     "sg_triage_newsig": (c_int, [c_void_p, c_void_p, P32, P64, c_size_t, P32, P64]),
     "sg_triage_intersect": (c_int, [c_void_p, P32, P64, P32, P64, c_size_t, P64]),

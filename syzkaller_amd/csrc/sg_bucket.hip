@@ -2046,10 +2046,13 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
 // nwords = those signals (every word written, empty buckets' too: no clear
 // beforehand and no read of the old words).
 constexpr int kMarkT = 256, kMarkU = 2;
+// ncand (nullable): += the signals this launch newly marks (the batch's
+// distinct signals not in mwords, summed over its record slices)
 template <bool kFirst>
 __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
                                                         const uint32_t* __restrict__ mwords,
-                                                        uint32_t* __restrict__ nwords) {
+                                                        uint32_t* __restrict__ nwords,
+                                                        unsigned long long* __restrict__ ncand) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
   constexpr int kW = kBucketWords / kMarkT;  // slice words per thread
@@ -2097,12 +2100,25 @@ __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restri
     for (int u = 0; u < kMarkU; u++) v[u] = y[u];
   }
   __syncthreads();
+  uint32_t fresh = 0;  // this thread's newly marked signals
   if (kFirst) {
-    *reinterpret_cast<mvec*>(nwords + bucket_word(b, kW * tid)) = reinterpret_cast<const mvec*>(nbits)[tid];
-    return;
+    const mvec nb = reinterpret_cast<const mvec*>(nbits)[tid];
+    *reinterpret_cast<mvec*>(nwords + bucket_word(b, kW * tid)) = nb;
+#pragma unroll
+    for (int j = 0; j < kW; j++) fresh += __popc(nb[j]);
+  } else {
+    for (uint32_t i = tid; i < kBucketWords; i += kMarkT)
+      if (nbits[i]) {
+        uint32_t* w = nwords + bucket_word(b, i);
+        const uint32_t old = *w;
+        fresh += __popc(nbits[i] & ~old);
+        *w = old | nbits[i];
+      }
   }
-  for (uint32_t i = tid; i < kBucketWords; i += kMarkT)
-    if (nbits[i]) nwords[bucket_word(b, i)] |= nbits[i];
+  if (ncand) {
+    const uint32_t wsum = __builtin_amdgcn_readlane(sgd::wave_incl_add(fresh), 63);  // (one atomic per wave)
+    if ((tid & 63) == 0 && wsum) atomicAdd(ncand, (unsigned long long)wsum);
+  }
 }
 
 __global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
@@ -2345,7 +2361,7 @@ static bool prefix_keep_mode() {  // read at each begin (tests switch it)
 }
 
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
-                 const uint64_t* d_off, uint64_t n, uint64_t nrec) {
+                 const uint64_t* d_off, uint64_t n, uint64_t nrec, int form, uint64_t* d_ncand) {
   if (slot >= kPrefixSlots) {
     set_error("prefix triage: slot %u out of range", slot);
     return SG_EINVAL;
@@ -2357,7 +2373,8 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
   PrefixSlot& S = ctx->prefix[slot];
   S.slices.clear();
   S.open = false;
-  S.keep = prefix_keep_mode();
+  S.keep = form < 0 ? prefix_keep_mode() : form == 0;
+  if (d_ncand) SG_HIP(hipMemsetAsync(d_ncand, 0, 8, ctx->stream));
   S.marks = marks_words;
   S.n = n;
   std::vector<RecSlice> sl;
@@ -2392,6 +2409,8 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
       rc = buckets_one(ctx, bp, const_cast<uint32_t*>(base_words), marks_words, nullptr, &e, ns, nr, marks_words);
       if (rc) return rc;
     }
+    // (each distinct signal not in base is one pair)
+    if (d_ncand) SG_HIP(hipMemcpyAsync(d_ncand, np, 8, hipMemcpyDeviceToDevice, ctx->stream));
     S.nrec = nrec;
     S.open = true;
     return SG_OK;
@@ -2419,12 +2438,13 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
         ScopedTimer tm(ctx, "bucket_mark");
         const uint32_t* v2 = (const uint32_t*)ws_at(ctx, bp.oV2);
         const uint4* bd = (const uint4*)ws_at(ctx, bp.oBD);
+        unsigned long long* nc = (unsigned long long*)d_ncand;
         if (first)  // the batch's first slice writes every marks word
           hipLaunchKernelGGL(k_bucket_mark<true>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd, base_words,
-                             marks_words);
+                             marks_words, nc);
         else
           hipLaunchKernelGGL(k_bucket_mark<false>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd,
-                             base_words, marks_words);
+                             base_words, marks_words, nc);
         first = false;
       }
       SG_HIP(hipGetLastError());

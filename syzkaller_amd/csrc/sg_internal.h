@@ -218,8 +218,10 @@ size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
 // signal not in base_words and keeps the batch's partitions (or each such
 // signal's first record) in the slot; end flags the records against
 // mwords | owords and, with `update`, updates mwords / nwords.
+// form: 0 kept partitions, 1 first-owner pairs, -1 from SG_PREFIX_PAIRS; d_ncand
+// (nullable, device): the batch's distinct signals not in base_words.
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
-                 const uint64_t* d_off, uint64_t n, uint64_t nrec);
+                 const uint64_t* d_off, uint64_t n, uint64_t nrec, int form = -1, uint64_t* d_ncand = nullptr);
 int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owords, uint32_t* nwords, uint8_t* d_rec_new,
                bool update);
 // One emitting launch (nrec <= kMaxLaunchRecords, n < 2^32 - 2^15), scratch

@@ -407,6 +407,20 @@ int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks,
   return prefix_begin(ctx, slot, base->words, marks->words, d_vals, d_rec_off, nvals, nrec);
 }
 
+int sg_prefix_begin_form_dev(sg_ctx* ctx, uint32_t slot, uint32_t form, sg_set* base, sg_set* marks,
+                             const uint32_t* d_vals, const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec,
+                             uint64_t* d_ncand) {
+  if (!ctx || !base || !marks || base == marks || base->ctx != ctx || marks->ctx != ctx || !d_rec_off ||
+      (nvals && !d_vals) || form > 1) {
+    set_error("sg_prefix_begin_form_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  return prefix_begin(ctx, slot, base->words, marks->words, d_vals, d_rec_off, nvals, nrec, (int)form, d_ncand);
+}
+
 int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
                       uint8_t* d_rec_new) {
   if (!ctx || !maxsig || maxsig->ctx != ctx || (newsig && newsig->ctx != ctx)) {

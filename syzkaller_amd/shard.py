@@ -208,9 +208,16 @@ class HipStages:
         call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
              total.data_ptr())
 
-    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0):
-        call("sg_prefix_begin_dev", self.ctx.h, slot, base.h, marks.h, vals.data_ptr() if nvals else None,
-             off.data_ptr(), nvals, nrec)
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0, form=None, ncand=None):
+        """form: None (the library's default), 0 kept partitions, 1 pairs;
+        ncand (nullable int64 device tensor): the batch's novelty count."""
+        if form is None and ncand is None:
+            call("sg_prefix_begin_dev", self.ctx.h, slot, base.h, marks.h, vals.data_ptr() if nvals else None,
+                 off.data_ptr(), nvals, nrec)
+            return
+        call("sg_prefix_begin_form_dev", self.ctx.h, slot, 0 if form is None else form, base.h, marks.h,
+             vals.data_ptr() if nvals else None, off.data_ptr(), nvals, nrec,
+             ctypes.c_void_p(ncand.data_ptr()) if ncand is not None else None)
 
     def prefix_end(self, maxset, prefix, newset, rec_new, slot=0):
         """prefix: None or an int32 device tensor of >= 2^27 words (bitmap layout)."""
@@ -347,14 +354,22 @@ class PrefixTriage:
     this one is finished:  start(b0), start(b1), finish(b0), start(b2),
     finish(b1), ...  Marking batch i+1 against a maxSignal that still lacks
     batch i's total T_i only adds signal of M0' = M0 | T_i to C, and
-    M0' | P' = M0' | P, so the flags are unchanged.  (SG_PREFIX_PAIRS=1: begin
-    keeps each s of C_k with its first record instead of the partitions, and
-    step 3 tests those pairs against the current maxSignal | P_k; measured
-    slower on fresh batches, include/syzsig.h and sg_bucket.hip.)  Stage contracts:
-    HipStages."""
+    M0' | P' = M0' | P, so the flags are unchanged.
+
+    Step 1's form is chosen per batch (form="auto"): "kept" keeps the rank's
+    partitions and step 3 re-runs the bucket stage against M0 | P_k (a mark
+    pass more than a plain triage, whatever the novelty); "pairs" keeps each s
+    of C_k with its first record and step 3 tests those pairs against the
+    current maxSignal | P_k (its cost grows with |C_k|: slower on fresh
+    batches, cheaper in the fuzzer's low-novelty steady state; include/syzsig.h,
+    sg_bucket.hip).  The rank takes "pairs" while the last batch it has a count
+    for had |C_k| below pairs_below of its signal entries; the counts come back
+    without a host wait (a pinned copy, read once its event has passed).  The
+    forms are interchangeable stage by stage, so ranks may differ.  Stage
+    contracts: HipStages."""
 
     def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None,
-                 gather=None):
+                 gather=None, form="auto", pairs_below=0.05):
         self.st = stages
         self.comm = comm if comm is not None else Comm()
         self.device = device
@@ -386,9 +401,29 @@ class PrefixTriage:
                              pref=torch.empty(n, dtype=torch.int32, device=device),
                              tot=torch.empty(self.S, dtype=torch.int32, device=device))
                 b["cset"] = stages.wrap(b["C"])
+                b["ncand"] = torch.zeros(1, dtype=torch.int64, device=device)
+                b["ncand_h"] = torch.zeros(1, dtype=torch.int64, pin_memory=(device != "cpu"))
                 self.slots.append(b)
         self.next_slot = 0
         self.last = {}
+        self.form, self.pairs_below = form, pairs_below
+        self.novelty = None  # |C_k| / entries of the last batch whose count has come back
+        self._nov = None     # (slot, entries, event) of the count in flight
+
+    def _form(self):
+        """This batch's step-1 form (0 kept, 1 pairs; None: the library's default)."""
+        if self.form == "kept":
+            return 0
+        if self.form == "pairs":
+            return 1
+        if self.form != "auto":
+            return None
+        if self._nov is not None:
+            slot, n, ev = self._nov
+            if ev is None or ev.query():
+                self.novelty = float(self.slots[slot]["ncand_h"].item()) / max(n, 1)
+                self._nov = None
+        return 1 if self.novelty is not None and self.novelty < self.pairs_below else 0
 
     def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new, nrec_total=None):
         """Same contract as ShardedTriage.step."""
@@ -411,8 +446,21 @@ class PrefixTriage:
         slot = self.next_slot
         self.next_slot ^= 1
         b = self.slots[slot]
-        # 1. this rank's new signal against M0 (its partitions kept for 3.)
-        st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
+        # 1. this rank's new signal against M0 (its partitions, or its pairs, kept for 3.)
+        form = self._form()
+        if form is None:
+            st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
+        else:
+            st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot, form=form, ncand=b["ncand"])
+            if self._nov is None and nvals:  # (one count in flight at a time; an empty batch tells nothing)
+                ev = None
+                if b["ncand"].is_cuda:
+                    b["ncand_h"].copy_(b["ncand"], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                else:
+                    b["ncand_h"].copy_(b["ncand"])
+                self._nov = (slot, nvals, ev)
         # 2. exclusive prefix and total over the ranks (slice by slice, or
         # whole bitmaps in gather mode)
         if self.gather:
@@ -441,7 +489,8 @@ class PrefixTriage:
             exchange(st)
         pend["slot"] = slot
         xb = 4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))
-        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": xb}
+        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": xb,
+                        "form": {0: "kept", 1: "pairs", None: "default"}[form]}
         return pend
 
     def finish(self, pend):

@@ -45,6 +45,7 @@ class NumpyPrefixStages:
 
     def __init__(self):
         self.kept = {}
+        self.forms = []  # the forms begin was asked for (both restate the same contract)
 
     def new_set(self):
         return BitSet()
@@ -73,12 +74,15 @@ class NumpyPrefixStages:
             acc = acc | p[k]
         total.numpy().view(np.uint32)[:words] = acc
 
-    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0):
+    def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0, form=None, ncand=None):
         v = vals[:nvals].numpy().view(np.uint32)
         marks.w[:] = 0  # (marks = the batch's signal not in base)
         if v.size:
             marks.add(v[~base.has(v)])
         self.kept[slot] = (vals, off, nvals, nrec, marks)
+        self.forms.append(form)
+        if ncand is not None:  # the batch's distinct signals not in base
+            ncand[0] = int(np.unpackbits(marks.w.view(np.uint8)).sum())
 
     def prefix_flags(self, maxset, prefix, rec_new, slot=0):
         """The loop's flags against maxset | prefix (include/syzsig.h)."""
@@ -126,13 +130,14 @@ M0 = np.arange(0, 3000, 5, dtype=np.uint32)
 BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
 
 
-def _worker(rank, world, port, q, pipelined, gather, drain=False):
+def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.05):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from syzkaller_amd.shard import Comm, PrefixTriage
 
-        tri = PrefixTriage(NumpyPrefixStages(), Comm(), device="cpu", gather=gather)
+        stages = NumpyPrefixStages()
+        tri = PrefixTriage(stages, Comm(), device="cpu", gather=gather, pairs_below=pairs_below)
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
@@ -165,17 +170,20 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False):
         if pend is not None:
             finish(pend)
         q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(),
-               drained if drain else ns.export()))
+               drained if drain else ns.export(), stages.forms))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,pipelined,gather,drain", [(2, False, False, False), (4, False, False, False),
-                                                          (2, True, False, False), (4, True, False, False),
-                                                          (2, True, True, False), (4, False, True, False),
-                                                          (2, True, False, True), (4, True, True, True)])
-def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain):
+@pytest.mark.parametrize("world,pipelined,gather,drain,pairs_below",
+                         [(2, False, False, False, 0.05), (4, False, False, False, 0.05),
+                          (2, True, False, False, 0.05), (4, True, False, False, 0.05),
+                          (2, True, True, False, 0.05), (4, False, True, False, 0.05),
+                          (2, True, False, True, 0.05), (4, True, True, True, 0.05),
+                          (2, False, False, False, 2.0), (4, True, False, True, 2.0),
+                          (2, True, True, False, -1.0)])
+def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain, pairs_below):
     """drain: newSignal is read and cleared after every finish() while the next
     batch is already started -- each drained set must be exactly that batch's
     new signal (fuzzer.go:674: only what maxSignal lacked), not a re-report of
@@ -185,13 +193,23 @@ def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather, drain)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather, drain, pairs_below))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, out, m, n = q.get(timeout=240)
+        r, out, m, n, forms = q.get(timeout=240)
         res[r] = (out, m, n)
+        # the form of each batch from the novelty of the last counted one: kept
+        # first (no count yet); pairs_below 2.0 (above any novelty): pairs after
+        assert forms[0] == 0, forms
+        if pairs_below > 1.0:  # kept until a non-empty batch has been counted, pairs after
+            assert forms[-1] == 1 and forms == sorted(forms), forms
+        elif pairs_below < 0:
+            assert set(forms) == {0}, forms
+        else:  # by each rank's novelty (later batches overlap the earlier ones' signal)
+            assert set(forms) <= {0, 1}, forms
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

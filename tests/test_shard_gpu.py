@@ -208,7 +208,7 @@ def test_shard_owners_and_flags_vs_numpy(ctx):
         assert np.array_equal(got.cpu().numpy(), exp.numpy()), (rec_lo, nrec)
 
 
-def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=False):
+def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=False, form="auto"):
     from syzkaller_amd import cover as C
     from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
     from tests.test_shard import split
@@ -224,9 +224,9 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=
         with torch.cuda.stream(side):
             side_st = HipStages(side_ctx)
         tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=True, side_stages=side_st,
-                           side_stream=side, gather=False)
+                           side_stream=side, gather=False, form=form)
     elif proto == "prefix":
-        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=collectives)
+        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=collectives, form=form)
     else:
         tri = ShardedTriage(HipStages(ctx), Comm(collectives=collectives))
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
@@ -272,9 +272,12 @@ def _expected():
     return flags, om.export().tolist(), on.export().tolist()
 
 
-@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
-def test_sharded_protocol_one_rank_vs_oracle(ctx, proto):
-    out, m, n = _run_protocol(0, 1, 0, BATCHES, M0, proto)
+@pytest.mark.parametrize("proto,form", [("pairs", "auto"), ("prefix", "auto"), ("prefix_pipelined", "auto"),
+                                        ("prefix_pipelined", "pairs"), ("prefix_pipelined", "kept")])
+def test_sharded_protocol_one_rank_vs_oracle(ctx, proto, form):
+    """form: PrefixTriage's per-batch step-1 form (auto by the last counted
+    batch's novelty, or forced) -- the same flags and sets whichever runs."""
+    out, m, n = _run_protocol(0, 1, 0, BATCHES, M0, proto, form=form)
     ef, em, en = _expected()
     for b, (r0, fl) in enumerate(out):
         assert np.array_equal(np.array(fl, np.uint8), ef[b]), b
