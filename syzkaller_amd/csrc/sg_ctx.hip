@@ -456,6 +456,7 @@ int sg_ctx_create(int device, sg_ctx** out) {
     if (v > 0 && v < c->owner_key_space) c->owner_key_space = v;
   }
   c->debug_part = getenv("SG_DEBUG_PART") != nullptr;
+  c->hist_lean = getenv("SG_HIST_LEAN") != nullptr && getenv("SG_HIST_LEAN")[0] != '0';
   int rc = ensure_device(c);
   if (rc) {
     delete c;
