@@ -442,6 +442,53 @@ def timed_steps(ctx, maxsig, m0set, newsig, batches, rec_new, world, tag=1):
     return wall, tri
 
 
+def timed_steps_pipelined(ctx, m0set, newsig, batches, flags0):
+    """The timed steps through syzkaller_amd/pipeline.py: step i+1's partition
+    on a second stream beside step i's bucket stage (bucket stages in step
+    order, each step against its own copy of the starting maxSignal, as in
+    timed_steps).  Every step's flags are checked against the sequential path
+    outside the timed region; flags0 = step 0's from timed_steps."""
+    from syzkaller_amd.pipeline import PipelinedTriage
+
+    states = [SignalSet(ctx) for _ in batches]
+    for st in states:
+        call("sg_set_copy", st.h, m0set.h)
+    flags = [torch.empty(b.nrec, dtype=torch.uint8, device="cuda") for b in batches]
+    pt = PipelinedTriage(ctx)
+    for st, b, f in zip(states[:2], batches[:2], flags[:2]):  # warm: both slots' workspaces
+        pt.submit(st, newsig, b.vals, b.off, b.nvals, b.nrec, f)
+    for st in states[:2]:
+        call("sg_set_copy", st.h, m0set.h)
+    torch.cuda.synchronize()
+    call("sg_ctx_marker", ctx.h, 0, 5)
+    t0 = time.perf_counter()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for st, b, f in zip(states, batches, flags):
+        pt.submit(st, newsig, b.vals, b.off, b.nvals, b.nrec, f)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record()
+    call("sg_ctx_marker", ctx.h, 1, 5)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    pt.close()
+    ok = bool(np.array_equal(flags[0].cpu().numpy(), flags0))
+    rec_new = torch.empty(max(b.nrec for b in batches), dtype=torch.uint8, device="cuda")
+    for b, f in zip(batches[1:], flags[1:]):  # the sequential path, outside the timed region
+        call("sg_set_copy", states[0].h, m0set.h)
+        triage(ctx, states[0], None, b, rec_new)
+        ok = ok and bool(torch.equal(rec_new[: b.nrec], f))
+    counts = {len(st) for st in states[1:]}
+    for st in states:
+        st.close()
+    ms = e0.elapsed_time(e1) / len(batches)
+    return {"ms_per_step": round(ms, 4), "wall_ms_per_step": round(wall * 1e3 / len(batches), 4),
+            "flags_equal_sequential": ok, "steps": len(batches),
+            "how": "syzkaller_amd/pipeline.py: step i+1's partition (sg_prefix_begin_form_dev form 2) on a second "
+                   "stream beside step i's bucket stage (sg_prefix_end_dev), the bucket stages in step order",
+            "state_sizes_after": sorted(counts)}
+
+
 def kernel_table(ctx, names, steps):
     out = {}
     for name in names:
@@ -504,6 +551,8 @@ def run_c2(ctx, args, cfg, rank):
         m0_values = m0set.export()
         res["cpu"] = cpu_baseline(m0_values, timed[0], calls, gpu_flags0, args.cpu_budget, args.cpu_threads,
                                   os.cpu_count())
+    if args.pipeline:
+        res["pipelined"] = timed_steps_pipelined(ctx, m0set, newsig, timed, gpu_flags0)
     if args.host_api:
         res["host_api"] = run_host_api(ctx, timed[0], maxsig, newsig, m0set, gpu_flags0)
     del batches, timed
@@ -812,6 +861,8 @@ def main():
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host entry point leg (C2 batch from pageable host memory)")
     ap.add_argument("--no-account", action="store_true", help="skip the byte-accounting replay")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="C2: also time the two-stage pipelined loop (syzkaller_amd/pipeline.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -886,6 +937,7 @@ def main():
             "steady_state": r.get("steady"),
             "from_traces": r.get("from_traces"),
             "host_api": r.get("host_api"),
+            "pipelined": r.get("pipelined"),
             "path": "partitioned (flags + set updates)",
             "gen_s": r["gen_s"],
         }

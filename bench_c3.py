@@ -22,7 +22,7 @@ from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, cpu_baseline, kern
 from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
-                                "set_add", "prefix_or", "bucket_mark", "prefix_flags", "prefix_merge", "set_or",
+                                "set_add", "prefix_or", "bucket_mark", "prefix_flags", "prefix_merge", "set_or", "set_or_new_or",
                                 "set_or_new"]
 
 

@@ -114,6 +114,10 @@ int sg_set_or_dev(sg_set* set, const uint32_t* d_words);
  * against an older maxSignal (fuzzer.go:674 adds to newSignal only what
  * maxSignal lacks). */
 int sg_set_or_new_dev(sg_set* set, const uint32_t* d_words, sg_set* exclude);
+/* Both in one pass over words: newsig |= words & ~maxsig, then maxsig |= words
+ * (newsig nullable; the two sets distinct, of one context, neither aliasing
+ * words).  Words that are zero are read once and nothing else is touched. */
+int sg_set_or_new_or_dev(sg_set* newsig, sg_set* maxsig, const uint32_t* d_words);
 /* dst = src (both sets of the same context). */
 int sg_set_copy(sg_set* dst, sg_set* src);
 /* *out = number of the n device-resident values not in set (duplicates
@@ -198,6 +202,11 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
  * d_total = OR of all parts.  RCCL has no bitwise-OR reduction. */
 int sg_bitmap_prefix_or_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t* d_prefix,
 			    uint32_t* d_total);
+/* One rank's share of it (the gather form, where every rank holds all parts):
+ * d_prefix (nullable: rank 0's is zero) = OR of parts 0..rank-1, d_total = OR
+ * of all parts; rank < nparts. */
+int sg_bitmap_prefix_or_rank_dev(sg_ctx* ctx, const uint32_t* d_parts, uint32_t nparts, uint64_t words, uint32_t rank,
+				 uint32_t* d_prefix, uint32_t* d_total);
 /* The two halves of sg_triage_batch_dev (flags and set updates, no diff) for
  * the prefix protocol.  Begin: marks (base != marks) = every signal of the
  * batch not in base (the local new signal, fuzzer.go:666), and
@@ -224,7 +233,12 @@ int sg_prefix_begin_dev(sg_ctx* ctx, uint32_t slot, sg_set* base, sg_set* marks,
  * with their first records (end tests those pairs; cheaper when few).  The
  * results are the same.  d_ncand (nullable, device u64) receives the number of
  * distinct signals of the batch not in base -- the novelty a caller picks the
- * next batch's form from (syzkaller_amd/shard.py PrefixTriage). */
+ * next batch's form from (syzkaller_amd/shard.py PrefixTriage).  Form 2 (base,
+ * marks and d_ncand NULL) keeps the partitions and marks nothing: begin + end
+ * with d_prefix NULL is sg_triage_batch_dev (flags and set updates) cut in
+ * two, so a caller can partition batch i+1 (begin, on one stream) while batch
+ * i's bucket stage runs (end, on another; the fuzzer loop's order is kept by
+ * running the ends in batch order). */
 int sg_prefix_begin_form_dev(sg_ctx* ctx, uint32_t slot, uint32_t form, sg_set* base, sg_set* marks,
 			     const uint32_t* d_vals, const uint64_t* d_rec_off, uint64_t nvals, uint64_t nrec,
 			     uint64_t* d_ncand);

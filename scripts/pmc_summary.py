@@ -23,7 +23,7 @@ KERNELS = {"p1_hist": ("k_hist_rep<false>", "k_hist_trace", "k_p1_hist"), "p1_sc
            "triage_claim": ("k_claim<true>",), "triage_resolve": ("k_resolve<true>",),
            "count_missing": ("k_count_missing",), "emit_scatter": ("k_scatter(",),
            "bucket_mark": ("k_bucket_mark",), "prefix_or": ("k_prefix_or",), "prefix_flags": ("k_prefix_flags",),
-           "prefix_merge": ("k_prefix_merge",), "set_or": ("k_set_or(",), "set_or_new": ("k_set_or_new",)}
+           "prefix_merge": ("k_prefix_merge",), "set_or": ("k_set_or(",), "set_or_new": ("k_set_or_new(",), "set_or_new_or": ("k_set_or_new_or",)}
 
 
 def load(path, counter, nregions):

@@ -1410,23 +1410,49 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
     } else if (kEmit) {
-      // every distinct candidate of the bucket with its first record
-      constexpr int kPer = kHash / kBThreads / 2;
+      // every distinct candidate of the bucket with its first record: the
+      // thread's occupied slots counted, one block scan and one global
+      // atomic for the bucket's run of pairs, then the slots re-read and
+      // written (two barriers per bucket; with the pairs held in registers
+      // between two scans, six)
+      constexpr int kOwn = kHash / kBThreads;  // slots per thread
+      __shared__ uint32_t ewc[kBThreads / 64];
+      __shared__ unsigned long long ebase;
+      const int lane = tid & 63, w = tid >> 6;
+      uint32_t c = 0;
 #pragma unroll
-      for (int half = 0; half < 2; half++) {
-        uint32_t sig[kPer], rec[kPer];
+      for (int k = 0; k < kOwn; k++) c += ht[k * kBThreads + tid] != kEmpty ? 1u : 0u;
+      const uint32_t incl = sgd::wave_incl_add(c);
+      if (lane == 63) ewc[w] = incl;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-          const uint32_t i = (half * kPer + k) * kBThreads + tid;
-          const uint32_t v = ht[i];
-          const uint32_t sl = map_signal(i, v);
-          sig[k] = part_sig((b << 16) | sl);
-          rec[k] = v != kEmpty ? (v & kRecMask) : kEmpty;
-          ht[i] = kEmpty;
-          if (a.nwords && v != kEmpty) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+        for (int i = 0; i < kBThreads / 64; i++) {
+          const uint32_t v = ewc[i];
+          ewc[i] = acc;
+          acc += v;
         }
-        emit_pairs(a, sig, rec, shcnt);  // (ends with a barrier)
+        ebase = acc ? atomicAdd(a.npairs, (unsigned long long)acc) : 0ull;
       }
+      __syncthreads();
+      uint64_t pos = ebase + ewc[w] + incl - c;
+      if (c) {
+#pragma unroll
+        for (int k = 0; k < kOwn; k++) {
+          const uint32_t i = k * kBThreads + tid;
+          const uint32_t v = ht[i];
+          if (v != kEmpty) {
+            const uint32_t sl = map_signal(i, v);
+            const uint32_t sg = part_sig((b << 16) | sl);
+            a.pairs[pos++] = make_uint2(sg, a.rec_base + (v & kRecMask));
+            if (a.shard_cnt) atomicAdd(&shcnt[shard_of(sg, a.nshards)], 1u);
+            if (a.nwords) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+            ht[i] = kEmpty;
+          }
+        }
+      }
+      __syncthreads();  // nbits complete; ewc / ebase free for the next bucket
       if (a.nwords) {  // the candidates' bits: words kWPT tid .., written by this block alone
         const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
         uint32_t* ng = a.nwords + bucket_word(b, kWPT * tid);
@@ -2077,21 +2103,24 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
 // nwords = those signals (every word written, empty buckets' too: no clear
 // beforehand and no read of the old words).
 constexpr int kMarkT = 256, kMarkU = 2;
-// ncand (nullable): += the signals this launch newly marks (the batch's
-// distinct signals not in mwords, summed over its record slices)
+// bcnt (nullable): per bucket, the signals this launch newly marks (summed by
+// k_sum_counts into the batch's count of distinct signals not in mwords; one
+// atomic per wave on a single counter serialised: 2 x 3.3 ms per C3 slice)
 template <bool kFirst>
 __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restrict__ in, const uint4* __restrict__ bdesc,
                                                         const uint32_t* __restrict__ mwords,
                                                         uint32_t* __restrict__ nwords,
-                                                        unsigned long long* __restrict__ ncand) {
+                                                        uint32_t* __restrict__ bcnt) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
+  __shared__ uint32_t wcnt[kMarkT / 64];
   constexpr int kW = kBucketWords / kMarkT;  // slice words per thread
   typedef uint32_t mvec __attribute__((ext_vector_type(kW)));
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint4 q = bdesc[b];
   if (q.x >= q.y) {
     if (kFirst) *reinterpret_cast<mvec*>(nwords + bucket_word(b, kW * tid)) = mvec{};
+    if (bcnt && tid == 0) bcnt[b] = 0;
     return;
   }
   constexpr uint32_t kStep = kMarkT * 4 * kMarkU;
@@ -2146,9 +2175,33 @@ __global__ __launch_bounds__(kMarkT) void k_bucket_mark(const uint32_t* __restri
         *w = old | nbits[i];
       }
   }
-  if (ncand) {
-    const uint32_t wsum = __builtin_amdgcn_readlane(sgd::wave_incl_add(fresh), 63);  // (one atomic per wave)
-    if ((tid & 63) == 0 && wsum) atomicAdd(ncand, (unsigned long long)wsum);
+  if (bcnt) {
+    const uint32_t wsum = __builtin_amdgcn_readlane(sgd::wave_incl_add(fresh), 63);
+    if ((tid & 63) == 0) wcnt[tid >> 6] = wsum;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int i = 0; i < kMarkT / 64; i++) t += wcnt[i];
+      bcnt[b] = t;
+    }
+  }
+}
+
+// *acc += the n counts (one workgroup)
+__global__ __launch_bounds__(1024) void k_sum_counts(const uint32_t* __restrict__ c, uint32_t n,
+                                                     unsigned long long* __restrict__ acc) {
+  __shared__ unsigned long long ws[16];
+  unsigned long long t = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) t += c[i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (int i = 0; i < 16; i++) s += ws[i];
+    *acc += s;
   }
 }
 
@@ -2404,7 +2457,8 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
   PrefixSlot& S = ctx->prefix[slot];
   S.slices.clear();
   S.open = false;
-  S.keep = form < 0 ? prefix_keep_mode() : form == 0;
+  S.keep = form < 0 ? prefix_keep_mode() : form != 1;
+  const bool mark = form != 2;  // form 2: the partitions alone (a plain triage split in two)
   if (d_ncand) SG_HIP(hipMemsetAsync(d_ncand, 0, 8, ctx->stream));
   S.marks = marks_words;
   S.n = n;
@@ -2465,17 +2519,22 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
                          roff);
       rc = partition_one(ctx, d_vals + x.e0, roff, ns, nr, base, true, bp);
       if (rc) return rc;
-      {
+      if (mark) {
         ScopedTimer tm(ctx, "bucket_mark");
         const uint32_t* v2 = (const uint32_t*)ws_at(ctx, bp.oV2);
         const uint4* bd = (const uint4*)ws_at(ctx, bp.oBD);
-        unsigned long long* nc = (unsigned long long*)d_ncand;
+        // (per-bucket counts in the partition's non-empty flags, which the
+        // bucket stage does not read)
+        uint32_t* bc = d_ncand ? (uint32_t*)ws_at(ctx, bp.oBN) : nullptr;
         if (first)  // the batch's first slice writes every marks word
           hipLaunchKernelGGL(k_bucket_mark<true>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd, base_words,
-                             marks_words, nc);
+                             marks_words, bc);
         else
           hipLaunchKernelGGL(k_bucket_mark<false>, dim3(kNumBuckets), dim3(kMarkT), 0, ctx->stream, v2, bd,
-                             base_words, marks_words, nc);
+                             base_words, marks_words, bc);
+        if (bc)
+          hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(1024), 0, ctx->stream, (const uint32_t*)bc, kNumBuckets,
+                             (unsigned long long*)d_ncand);
         first = false;
       }
       SG_HIP(hipGetLastError());
@@ -2483,7 +2542,7 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
     }
     S.slices.push_back(ps);
   }
-  if (first) SG_HIP(hipMemsetAsync(marks_words, 0, kSetBytes, ctx->stream));  // no entries
+  if (first && mark) SG_HIP(hipMemsetAsync(marks_words, 0, kSetBytes, ctx->stream));  // no entries
   S.nrec = nrec;
   S.open = true;
   return SG_OK;

@@ -208,14 +208,25 @@ class HipStages:
         call("sg_bitmap_prefix_or_dev", self.ctx.h, parts.data_ptr(), nparts, words, prefix.data_ptr(),
              total.data_ptr())
 
+    def prefix_or_rank(self, parts, nparts, words, rank, prefix, total):
+        """prefix (None for rank 0) = OR of parts < rank, total = OR of all."""
+        call("sg_bitmap_prefix_or_rank_dev", self.ctx.h, parts.data_ptr(), nparts, words, rank,
+             ctypes.c_void_p(prefix.data_ptr()) if prefix is not None else None, total.data_ptr())
+
+    def or_new_or(self, newset, sset, t):
+        """newset (nullable) |= t & ~sset, then sset |= t, in one pass."""
+        call("sg_set_or_new_or_dev", newset.h if newset is not None else None, sset.h, ctypes.c_void_p(t.data_ptr()))
+
     def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0, form=None, ncand=None):
-        """form: None (the library's default), 0 kept partitions, 1 pairs;
+        """form: None (the library's default), 0 kept partitions, 1 pairs,
+        2 partitions only (base, marks None: a plain triage's first half);
         ncand (nullable int64 device tensor): the batch's novelty count."""
         if form is None and ncand is None:
             call("sg_prefix_begin_dev", self.ctx.h, slot, base.h, marks.h, vals.data_ptr() if nvals else None,
                  off.data_ptr(), nvals, nrec)
             return
-        call("sg_prefix_begin_form_dev", self.ctx.h, slot, 0 if form is None else form, base.h, marks.h,
+        call("sg_prefix_begin_form_dev", self.ctx.h, slot, 0 if form is None else form,
+             base.h if base is not None else None, marks.h if marks is not None else None,
              vals.data_ptr() if nvals else None, off.data_ptr(), nvals, nrec,
              ctypes.c_void_p(ncand.data_ptr()) if ncand is not None else None)
 
@@ -382,19 +393,20 @@ class PrefixTriage:
         self.S = -(-W // G)  # words per slice (the last slice padded)
         # gather mode: one all-gather of the whole C_k, every rank computes its
         # own prefix: (G-1) bitmaps per rank against the all-to-all form's
-        # 3 (G-1) / G, so fewer bytes for G = 2
-        self.gather = (G == 2) if gather is None else gather
+        # 3 (G-1) / G, so fewer bytes for G = 2 (and at one rank no exchange:
+        # T = C)
+        self.gather = (G <= 2) if gather is None else gather
         self.W = W
         self.slots = []
         if G > 1 or two_phase_at_one:
             n = self.S * G
             for _ in range(2):
                 if self.gather:
-                    b = {"C": torch.zeros(W, dtype=torch.int32, device=device),
-                         "allc": torch.empty(G * W, dtype=torch.int32, device=device),
-                         "pref": torch.empty(G * W, dtype=torch.int32, device=device),
-                         "T": torch.empty(W, dtype=torch.int32, device=device)}
-                    b["P"] = b["pref"][self.comm.rank * W:(self.comm.rank + 1) * W]
+                    # (this rank's P_k and T only; at one rank T is C itself)
+                    C = torch.zeros(W, dtype=torch.int32, device=device)
+                    b = {"C": C, "allc": torch.empty(G * W, dtype=torch.int32, device=device) if G > 1 else C,
+                         "P": torch.empty(W, dtype=torch.int32, device=device) if self.comm.rank > 0 else None,
+                         "T": torch.empty(W, dtype=torch.int32, device=device) if G > 1 else C}
                 else:
                     b = {k: torch.zeros(n, dtype=torch.int32, device=device) for k in ("C", "P", "T")}
                     b.update(recv=torch.empty(n, dtype=torch.int32, device=device),
@@ -464,14 +476,15 @@ class PrefixTriage:
         # 2. exclusive prefix and total over the ranks (slice by slice, or
         # whole bitmaps in gather mode)
         if self.gather:
-            got_c = c.start_all_gather_equal(b["allc"], b["C"])
+            got_c = c.start_all_gather_equal(b["allc"], b["C"]) if G > 1 else _Done()
         else:
             got_c = c.start_all_to_all_equal(b["recv"], b["C"])
 
         def exchange(stages):
             got_c.wait()
-            if self.gather:  # pref part k = P_k; this rank's is b["P"]
-                stages.prefix_or(b["allc"], G, self.W, b["pref"], b["T"])
+            if self.gather:  # this rank's P_k and T (one part: T = C)
+                if G > 1:
+                    stages.prefix_or_rank(b["allc"], G, self.W, c.rank, b["P"], b["T"])
                 pend["got_p"] = pend["got_t"] = _Done()
             else:
                 stages.prefix_or(b["recv"], G, self.S, b["pref"], b["tot"])
@@ -509,10 +522,17 @@ class PrefixTriage:
             # which an overlapped batch finished since may have grown, and
             # newSignal may have been drained (the Poll, fuzzer.go:358-364) in
             # between -- so T & ~maxSignal, before step 3 changes maxSignal
-            if newsig is not None:
-                st.or_new_words(newsig, b["T"], maxsig)
-            st.prefix_flags(maxsig, b["P"] if self.comm.rank > 0 else None, pend["rec_new"], slot)
-            # 4. the replicated state after the whole batch
-            st.or_words(maxsig, b["T"])
+            P = b["P"] if self.comm.rank > 0 else None
+            if pend["last"].get("form") == "pairs":
+                # the pairs' flags leave maxSignal as it is: 3., then both set
+                # updates (4.) in one pass over T
+                st.prefix_flags(maxsig, P, pend["rec_new"], slot)
+                st.or_new_or(newsig, maxsig, b["T"])
+            else:
+                if newsig is not None:
+                    st.or_new_words(newsig, b["T"], maxsig)
+                st.prefix_flags(maxsig, P, pend["rec_new"], slot)
+                # 4. the replicated state after the whole batch
+                st.or_words(maxsig, b["T"])
         self.last = pend["last"]
         return pend["nrec_total"]

@@ -74,6 +74,21 @@ class NumpyPrefixStages:
             acc = acc | p[k]
         total.numpy().view(np.uint32)[:words] = acc
 
+    def prefix_or_rank(self, parts, nparts, words, rank, prefix, total):
+        p = parts.numpy().view(np.uint32)[: nparts * words].reshape(nparts, words)
+        if prefix is not None:
+            acc = np.zeros(words, np.uint32)
+            for k in range(rank):
+                acc |= p[k]
+            prefix.numpy().view(np.uint32)[:words] = acc
+        total.numpy().view(np.uint32)[:words] = np.bitwise_or.reduce(p, axis=0)
+
+    def or_new_or(self, newset, s, t):
+        w = t.numpy().view(np.uint32)[:WORDS]
+        if newset is not None:
+            newset.w |= w & ~s.w
+        s.w |= w
+
     def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0, form=None, ncand=None):
         v = vals[:nvals].numpy().view(np.uint32)
         marks.w[:] = 0  # (marks = the batch's signal not in base)
