@@ -2226,69 +2226,51 @@ static int read_off(sg_ctx* ctx, const uint64_t* d_off, uint64_t r, uint64_t* v)
 // tenth of them overflow the LDS candidate map into the slow spill kernel.
 constexpr uint64_t kSliceEntries = 1ull << 30;
 
-int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
-                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new, bool trace) {
-  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
-    set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
-    return SG_EINVAL;
-  }
-  if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
-  const uint64_t m = ctx->max_launch_recs;
-  if (nrec <= m && n <= kSliceEntries)
-    return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new, nullptr, 0, trace);
-  if (ctx->slice_off_cap < m + 1) {
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
-    ctx->slice_off = nullptr;
-    ctx->slice_off_cap = 0;
-    SG_HIP(hipMalloc(&ctx->slice_off, (m + 1) * 8));
-    ctx->slice_off_cap = m + 1;
-  }
-  uint64_t* roff = ctx->slice_off;
-  uint64_t e0 = 0;
-  int rc = read_off(ctx, d_off, 0, &e0);
-  if (rc) return rc;
-  for (uint64_t r0 = 0; r0 < nrec;) {
-    // record slices: <= m records, and <= kSliceEntries entries unless one
-    // record alone holds more.  The sequential loop (fuzzer.go:665) cut
-    // between two records sees the same maxSignal at every record.
-    uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
-    rc = read_off(ctx, d_off, r1, &e1);
-    if (rc) return rc;
-    if (e1 - e0 > kSliceEntries) {  // largest r1 > r0 with e1 - e0 <= kSliceEntries (at least one record)
-      uint64_t lo = r0 + 1, hi = r1;
-      while (lo < hi) {
-        const uint64_t mid = (lo + hi + 1) / 2;
-        uint64_t em = 0;
-        rc = read_off(ctx, d_off, mid, &em);
-        if (rc) return rc;
-        if (em - e0 <= kSliceEntries)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      r1 = lo;
-      rc = read_off(ctx, d_off, r1, &e1);
-      if (rc) return rc;
-    }
-    hipLaunchKernelGGL(k_rebase, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_off + r0, r1 - r0 + 1, e0,
-                       roff);
-    // (a slice starts at a record boundary: a trace slice's first entry is a call start)
-    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + e0, roff, e1 - e0, r1 - r0, d_rec_new + r0, nullptr, 0, trace);
-    if (rc) return rc;
-    SG_HIP(hipStreamSynchronize(ctx->stream));  // the next slice's offsets overwrite roff
-    r0 = r1;
-    e0 = e1;
-  }
-  return SG_OK;
-}
-
 // The record slices of a batch: <= max_launch_recs records and <=
 // kSliceEntries entries each (unless one record alone holds more).
 struct RecSlice {
   uint64_t r0, r1, e0, e1;
 };
-static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
+
+// The cuts by one device thread (a binary search per entry-limited slice):
+// out[0] = the number of slices, then {r0, r1, e0, e1} per slice, at most
+// kCutCap of them (a count past kCutCap: the host walks them itself).  One
+// launch, one small read and one wait per batch, where the host's own search
+// waited on the stream ~20 times (each wait an idle GPU between two batches).
+constexpr uint32_t kCutCap = 4096;
+constexpr uint32_t kCutHead = 64;  // slices read back with the count
+__global__ void k_slice_cuts(const uint64_t* __restrict__ off, uint64_t nrec, uint64_t m, uint64_t lim,
+                             uint64_t* __restrict__ out) {
+  if (threadIdx.x || blockIdx.x) return;
+  uint64_t r0 = 0, e0 = off[0], k = 0;
+  while (r0 < nrec && k <= kCutCap) {
+    uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = off[r1];
+    if (e1 - e0 > lim) {  // largest r1 > r0 with off[r1] - e0 <= lim (at least one record)
+      uint64_t lo = r0 + 1, hi = r1;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) / 2;
+        if (off[mid] - e0 <= lim)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      r1 = lo;
+      e1 = off[r1];
+    }
+    if (k < kCutCap) {
+      out[1 + 4 * k] = r0;
+      out[2 + 4 * k] = r1;
+      out[3 + 4 * k] = e0;
+      out[4 + 4 * k] = e1;
+    }
+    k++;
+    r0 = r1;
+    e0 = e1;
+  }
+  out[0] = k;
+}
+
+static int record_slices_host(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
   out.clear();
   const uint64_t m = ctx->max_launch_recs;
   uint64_t e0 = 0;
@@ -2317,6 +2299,66 @@ static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std:
     out.push_back({r0, r1, e0, e1});
     r0 = r1;
     e0 = e1;
+  }
+  return SG_OK;
+}
+
+static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
+  out.clear();
+  if (nrec == 0) return SG_OK;
+  if (!ctx->slice_cuts) SG_HIP(hipMalloc(&ctx->slice_cuts, (1 + 4 * (size_t)kCutCap) * 8));
+  hipLaunchKernelGGL(k_slice_cuts, dim3(1), dim3(64), 0, ctx->stream, d_off, nrec, (uint64_t)ctx->max_launch_recs,
+                     kSliceEntries, ctx->slice_cuts);
+  SG_HIP(hipGetLastError());
+  std::vector<uint64_t> h(1 + 4 * (size_t)kCutHead);
+  SG_HIP(hipMemcpyAsync(h.data(), ctx->slice_cuts, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  const uint64_t k = h[0];
+  if (k > kCutCap) return record_slices_host(ctx, d_off, nrec, out);
+  if (k > kCutHead) {
+    h.resize(1 + 4 * k);
+    SG_HIP(hipMemcpy(h.data(), ctx->slice_cuts, h.size() * 8, hipMemcpyDeviceToHost));
+  }
+  for (uint64_t j = 0; j < k; j++) out.push_back({h[1 + 4 * j], h[2 + 4 * j], h[3 + 4 * j], h[4 + 4 * j]});
+  return SG_OK;
+}
+
+int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                  uint64_t n, uint64_t nrec, uint8_t* d_rec_new, bool trace) {
+  if (nrec >= 0xFFFFFFFFull || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("bucket triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
+    return SG_EINVAL;
+  }
+  if (nrec) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
+  const uint64_t m = ctx->max_launch_recs;
+  if (nrec <= m && n <= kSliceEntries)
+    return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, d_rec_new, nullptr, 0, trace);
+  std::vector<RecSlice> sl;
+  int rc = record_slices(ctx, d_off, nrec, sl);
+  if (rc) return rc;
+  // every slice's rebased offsets at once (no wait between two slices)
+  const size_t need = nrec + sl.size();
+  if (ctx->slice_off_cap < need) {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
+    ctx->slice_off = nullptr;
+    ctx->slice_off_cap = 0;
+    SG_HIP(hipMalloc(&ctx->slice_off, need * 8));
+    ctx->slice_off_cap = need;
+  }
+  size_t at = 0;
+  for (const RecSlice& x : sl) {
+    // the sequential loop (fuzzer.go:665) cut between two records sees the
+    // same maxSignal at every record; a slice starts at a record boundary (a
+    // trace slice's first entry is a call start)
+    const uint64_t nr = x.r1 - x.r0;
+    uint64_t* roff = ctx->slice_off + at;
+    at += nr + 1;
+    if (x.e1 == x.e0) continue;  // records without entries (flags cleared above)
+    hipLaunchKernelGGL(k_rebase, dim3(div_up(nr + 1, 256)), dim3(256), 0, ctx->stream, d_off + x.r0, nr + 1, x.e0, roff);
+    rc = bucket_triage_one(ctx, mwords, nwords, d_vals + x.e0, roff, x.e1 - x.e0, nr, d_rec_new + x.r0, nullptr, 0,
+                           trace);
+    if (rc) return rc;
   }
   return SG_OK;
 }

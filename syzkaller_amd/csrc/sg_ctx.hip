@@ -542,6 +542,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);
   if (ctx->slice_off) hipFree(ctx->slice_off);
+  if (ctx->slice_cuts) hipFree(ctx->slice_cuts);
   if (ctx->dscal) hipFree(ctx->dscal);
   if (ctx->gen_prob) hipFree(ctx->gen_prob);
   if (ctx->gen_alias) hipFree(ctx->gen_alias);

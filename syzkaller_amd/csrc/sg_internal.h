@@ -106,9 +106,11 @@ struct sg_ctx {
   PrefixSlot prefix[kPrefixSlots];
   bool debug_part = false;
   bool hist_lean = false;  // SG_HIST_LEAN: the lean pass-1 histogram (sg_bucket.hip k_hist_lean)
-  // rebased record offsets of one record slice (grow-only, owned)
+  // rebased record offsets of record slices (grow-only, owned)
   uint64_t* slice_off = nullptr;
   size_t slice_off_cap = 0;
+  // a batch's record-slice cuts, found on the device (sg_bucket.hip k_slice_cuts)
+  uint64_t* slice_cuts = nullptr;
   // small device scalars (counters / flags)
   uint64_t* dscal = nullptr;
   // cached Zipf generator tables (alias method + rank->pc permutation)

@@ -662,9 +662,12 @@ def test_triage_dev_unaligned_input(C):
 def test_triage_record_slices(C, monkeypatch):
     """Batches above the per-launch record limit run as consecutive record
     slices (sg_bucket.hip bucket_triage); the limit is lowered here so that
-    slices start mid-batch, at empty records and at group boundaries."""
+    slices start mid-batch, at empty records and at group boundaries.  The
+    cuts come from the device (k_slice_cuts): up to 64 slices read with their
+    count, more in a second read (3, 300), and past 4096 the host's own walk
+    (1, 5000)."""
     rng = np.random.default_rng(131)
-    for limit, nrec in ((1000, 4321), (100000, 240000), (7, 50)):
+    for limit, nrec in ((1000, 4321), (100000, 240000), (7, 50), (3, 300), (1, 5000)):
         monkeypatch.setenv("SG_TRIAGE_MAX_RECS", str(limit))
         ctx = C.Context(0)  # the switch is read at context creation
         assert ctx.counter("max_launch_records") == limit
