@@ -388,6 +388,17 @@ int sg_exec_signal_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
 int sg_exec_signal_queued_dev(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_call_off,
 			      const uint64_t* d_prog_off, uint64_t nprog, uint64_t ncalls, uint64_t npcs,
 			      const uint8_t* d_rec_new, uint32_t* d_sig_vals, uint64_t* d_sig_off);
+/* The fuzzer's step from host traces in one call: sg_triage_traces (flags and
+ * set updates, set-exact) and the executor-exact signal lists of the queued
+ * calls only (sg_exec_signal_queued_dev), the traces staged once.  Calls are
+ * grouped into programs by prog_off (nprog + 1, prog_off[0] == 0; the
+ * executor's dedup table is per program); rec_new[c] for every call; the
+ * lists in sig_vals / sig_off (ncalls + 1) as sg_exec_signal's, empty for the
+ * calls not queued (fuzzer.go:678-683 copies the signal of queued calls
+ * only).  sig_vals capacity: call_off[ncalls] values. */
+int sg_triage_traces_queued(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* pcs,
+			    const uint64_t* call_off, const uint64_t* prog_off, size_t nprog, uint8_t* rec_new,
+			    uint32_t* sig_vals, uint64_t* sig_off);
 
 /* ---- synthetic Zipf traces (bench / test input generator) ----------------- */
 /* Zipf(s) over `nranks` PC ranks mapped through a permutation seeded by

@@ -102,6 +102,7 @@ SIGNATURES = {
                                    c_void_p]),
     "sg_exec_signal_queued_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
                                           c_void_p, c_void_p]),
+    "sg_triage_traces_queued": (c_int, [c_void_p, c_void_p, c_void_p, P32, P64, P64, c_size_t, P8, P32, P64]),
     "sg_gen_zipf_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_double, c_uint32, c_uint64, c_uint64, c_uint32,
                                        c_uint32, c_void_p]),
     "sg_gen_population_traces_dev": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_double, c_double,

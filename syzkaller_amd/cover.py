@@ -298,6 +298,22 @@ def triage_traces(maxset, newset, pcs, call_off, ctx=None):
     return rec_new
 
 
+def triage_traces_queued(maxset, newset, pcs, call_off, prog_off, ctx=None):
+    """The fuzzer's step from raw traces (sg_triage_traces_queued): the
+    per-call flags of fuzzer.go:645-693 (sets updated, set-exact) and the
+    executor-exact signal list of every queued call (fuzzer.go:678-683;
+    executor.h:389-401), empty for the others.  Returns (rec_new, vals, off)."""
+    p, co, po = _u32(pcs), _u64(call_off), _u64(prog_off)
+    ncalls = co.size - 1
+    rec_new = np.zeros(max(ncalls, 1), dtype=np.uint8)
+    sv = np.empty(max(p.size, 1), dtype=U32)
+    so = np.empty(ncalls + 1, dtype=U64)
+    c = maxset.ctx if ctx is None else ctx
+    call("sg_triage_traces_queued", c.h, maxset.h, newset.h if newset is not None else None, _p32(p), _p64(co),
+         _p64(po), po.size - 1, _p8(rec_new), _p32(sv), _p64(so))
+    return rec_new[:ncalls], sv[: int(so[-1])], so
+
+
 def add_inputs(corpus, maxset, vals, off, ctx=None):
     """syz-fuzzer/fuzzer.go:467-489 addInput over a batch of inputs."""
     vals, off = _u32(vals), _u64(off)

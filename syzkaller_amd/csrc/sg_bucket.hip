@@ -2270,7 +2270,8 @@ __global__ void k_slice_cuts(const uint64_t* __restrict__ off, uint64_t nrec, ui
   out[0] = k;
 }
 
-static int record_slices_host(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
+static int record_slices_host(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out,
+                              uint64_t lim) {
   out.clear();
   const uint64_t m = ctx->max_launch_recs;
   uint64_t e0 = 0;
@@ -2280,14 +2281,14 @@ static int record_slices_host(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec,
     uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
     rc = read_off(ctx, d_off, r1, &e1);
     if (rc) return rc;
-    if (e1 - e0 > kSliceEntries) {
+    if (e1 - e0 > lim) {
       uint64_t lo = r0 + 1, hi = r1;
       while (lo < hi) {
         const uint64_t mid = (lo + hi + 1) / 2;
         uint64_t em = 0;
         rc = read_off(ctx, d_off, mid, &em);
         if (rc) return rc;
-        if (em - e0 <= kSliceEntries)
+        if (em - e0 <= lim)
           lo = mid;
         else
           hi = mid - 1;
@@ -2303,24 +2304,33 @@ static int record_slices_host(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec,
   return SG_OK;
 }
 
-static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out) {
+static int record_slices(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, std::vector<RecSlice>& out,
+                         uint64_t lim = kSliceEntries) {
   out.clear();
   if (nrec == 0) return SG_OK;
   if (!ctx->slice_cuts) SG_HIP(hipMalloc(&ctx->slice_cuts, (1 + 4 * (size_t)kCutCap) * 8));
   hipLaunchKernelGGL(k_slice_cuts, dim3(1), dim3(64), 0, ctx->stream, d_off, nrec, (uint64_t)ctx->max_launch_recs,
-                     kSliceEntries, ctx->slice_cuts);
+                     lim, ctx->slice_cuts);
   SG_HIP(hipGetLastError());
   std::vector<uint64_t> h(1 + 4 * (size_t)kCutHead);
   SG_HIP(hipMemcpyAsync(h.data(), ctx->slice_cuts, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint64_t k = h[0];
-  if (k > kCutCap) return record_slices_host(ctx, d_off, nrec, out);
+  if (k > kCutCap) return record_slices_host(ctx, d_off, nrec, out, lim);
   if (k > kCutHead) {
     h.resize(1 + 4 * k);
     SG_HIP(hipMemcpy(h.data(), ctx->slice_cuts, h.size() * 8, hipMemcpyDeviceToHost));
   }
   for (uint64_t j = 0; j < k; j++) out.push_back({h[1 + 4 * j], h[2 + 4 * j], h[3 + 4 * j], h[4 + 4 * j]});
   return SG_OK;
+}
+
+int record_slice_cuts(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, uint64_t lim, std::vector<uint64_t>& cuts) {
+  std::vector<RecSlice> sl;
+  const int rc = record_slices(ctx, d_off, nrec, sl, lim);
+  cuts.clear();
+  for (const RecSlice& x : sl) cuts.insert(cuts.end(), {x.r0, x.r1, x.e0, x.e1});
+  return rc;
 }
 
 int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,

@@ -487,6 +487,55 @@ int sg_exec_signal(sg_ctx* ctx, const uint32_t* pcs, const uint64_t* call_off, c
   return SG_OK;
 }
 
+// The fuzzer's whole step from host traces: the set-exact triage (flags,
+// maxSignal / newSignal) and the executor-exact signal lists of the queued
+// calls only (the Input.Signal copies, fuzzer.go:678-683), one staging of the
+// traces for both.
+int sg_triage_traces_queued(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* pcs,
+                            const uint64_t* call_off, const uint64_t* prog_off, size_t nprog, uint8_t* rec_new,
+                            uint32_t* sig_vals, uint64_t* sig_off) {
+  if (!ctx || !maxsig || !call_off || !prog_off || !sig_off) {
+    set_error("sg_triage_traces_queued: invalid argument");
+    return SG_EINVAL;
+  }
+  const uint64_t ncalls = prog_off[nprog];
+  const uint64_t npcs = call_off[ncalls];
+  if (prog_off[0] != 0 || call_off[0] != 0 || (npcs && (!pcs || !sig_vals)) || (ncalls && !rec_new)) {
+    set_error("sg_triage_traces_queued: invalid argument (offsets must start at 0; null buffers)");
+    return SG_EINVAL;
+  }
+  char* st = nullptr;
+  const size_t b0 = (npcs * 4 + 255) & ~size_t(255), b1 = ((ncalls + 1) * 8 + 255) & ~size_t(255),
+               b2 = ((nprog + 1) * 8 + 255) & ~size_t(255), b3 = (ncalls + 255) & ~size_t(255);
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    rc = dstage_reserve(ctx, 2 * b0 + 2 * b1 + b2 + b3 + 256);
+    if (rc) return rc;
+    st = (char*)ctx->dstage;
+  }
+  uint32_t* dp = (uint32_t*)st;
+  uint32_t* dsv = (uint32_t*)(st + b0);
+  uint64_t* dco = (uint64_t*)(st + 2 * b0);
+  uint64_t* dso = (uint64_t*)(st + 2 * b0 + b1);
+  uint64_t* dpo = (uint64_t*)(st + 2 * b0 + 2 * b1);
+  uint8_t* drn = (uint8_t*)(st + 2 * b0 + 2 * b1 + b2);
+  if (npcs) SG_HIP(hipMemcpyAsync(dp, pcs, npcs * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dco, call_off, (ncalls + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dpo, prog_off, (nprog + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  int rc = sg_triage_traces_dev(ctx, maxsig, newsig, dp, dco, npcs, ncalls, drn);
+  if (rc) return rc;
+  rc = sg_exec_signal_queued_dev(ctx, dp, dco, dpo, nprog, ncalls, npcs, drn, dsv, dso);
+  if (rc) return rc;
+  if (ncalls) SG_HIP(hipMemcpyAsync(rec_new, drn, ncalls, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipMemcpyAsync(sig_off, dso, (ncalls + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (sig_off[ncalls]) SG_HIP(hipMemcpyAsync(sig_vals, dsv, sig_off[ncalls] * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
 }  // extern "C"
 
 namespace sg {

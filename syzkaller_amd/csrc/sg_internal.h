@@ -217,6 +217,10 @@ struct EmitArgs {
 };
 // Workspace bytes of one partitioned launch over n entries / nrec records.
 size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
+// A batch's record slices (<= max_launch_recs records, <= lim entries unless
+// one record alone holds more), as {r0, r1, e0, e1} quadruples: cuts found on
+// the device, one wait (sg_bucket.hip k_slice_cuts).
+int record_slice_cuts(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, uint64_t lim, std::vector<uint64_t>& cuts);
 // Two-phase triage (sg_bucket.hip): begin ORs into marks_words the batch's
 // signal not in base_words and keeps the batch's partitions (or each such
 // signal's first record) in the slot; end flags the records against

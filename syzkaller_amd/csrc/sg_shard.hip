@@ -345,52 +345,36 @@ int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_val
     rc = bucket_emit(ctx, snapshot->words, d_vals, d_rec_off, nvals, nrec, e, o_plan);
     if (rc) return rc;
   } else if (nvals) {
-    // record slices of <= m records and < 2^31 entries (the 2^32-entry cap
-    // of one partitioned launch holds per slice)
-    if (ctx->slice_off_cap < m + 1) {
+    // record slices of <= m records and < 2^30 entries, cut on the device;
+    // every slice's rebased offsets side by side (no wait between slices)
+    std::vector<uint64_t> cuts;
+    rc = record_slice_cuts(ctx, d_rec_off, nrec, kLaunchEntries - 1, cuts);
+    if (rc) return rc;
+    const size_t ns = cuts.size() / 4, need = nrec + ns;
+    for (size_t j = 0; j < ns; j++)
+      if (cuts[4 * j + 3] - cuts[4 * j + 2] >= kLaunchEntries) {
+        set_error("sg_shard_candidates_dev: a record holds >= 2^30 signal entries");
+        return SG_EINVAL;
+      }
+    if (ctx->slice_off_cap < need) {
       SG_HIP(hipStreamSynchronize(ctx->stream));
       if (ctx->slice_off) SG_HIP(hipFree(ctx->slice_off));
       ctx->slice_off = nullptr;
       ctx->slice_off_cap = 0;
-      SG_HIP(hipMalloc(&ctx->slice_off, (m + 1) * 8));
-      ctx->slice_off_cap = m + 1;
+      SG_HIP(hipMalloc(&ctx->slice_off, need * 8));
+      ctx->slice_off_cap = need;
     }
-    uint64_t e0 = 0;
-    rc = read_u64(ctx, d_rec_off, &e0);
-    if (rc) return rc;
-    for (uint64_t r0 = 0; r0 < nrec;) {
-      uint64_t r1 = nrec - r0 < m ? nrec : r0 + m, e1 = 0;
-      rc = read_u64(ctx, d_rec_off + r1, &e1);
-      if (rc) return rc;
-      if (e1 - e0 >= kLaunchEntries) {  // largest r1 with entries < 2^30 (a record holds < 2^30)
-        uint64_t lo = r0 + 1, hi = r1;
-        while (lo < hi) {
-          const uint64_t mid = (lo + hi + 1) / 2;
-          uint64_t em = 0;
-          rc = read_u64(ctx, d_rec_off + mid, &em);
-          if (rc) return rc;
-          if (em - e0 < kLaunchEntries)
-            lo = mid;
-          else
-            hi = mid - 1;
-        }
-        r1 = lo;
-        rc = read_u64(ctx, d_rec_off + r1, &e1);
-        if (rc) return rc;
-        if (e1 - e0 >= kLaunchEntries) {
-          set_error("sg_shard_candidates_dev: a record holds >= 2^30 signal entries");
-          return SG_EINVAL;
-        }
-      }
+    size_t at = 0;
+    for (size_t j = 0; j < ns; j++) {
+      const uint64_t r0 = cuts[4 * j], r1 = cuts[4 * j + 1], e0 = cuts[4 * j + 2], e1 = cuts[4 * j + 3];
+      uint64_t* roff = ctx->slice_off + at;
+      at += r1 - r0 + 1;
+      if (e1 == e0) continue;
       hipLaunchKernelGGL(k_rebase_off, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_rec_off + r0,
-                         r1 - r0 + 1, e0, ctx->slice_off);
+                         r1 - r0 + 1, e0, roff);
       EmitArgs e{tmp, npairs, (uint32_t)(rec_base + r0), nshards, cnt};
-      rc = bucket_emit(ctx, snapshot->words, d_vals + e0, ctx->slice_off, e1 - e0, r1 - r0, e, o_plan);
+      rc = bucket_emit(ctx, snapshot->words, d_vals + e0, roff, e1 - e0, r1 - r0, e, o_plan);
       if (rc) return rc;
-      // the next slice's offsets overwrite slice_off: wait for this one
-      SG_HIP(hipStreamSynchronize(ctx->stream));
-      r0 = r1;
-      e0 = e1;
     }
   }
   hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long*)cnt, nshards,

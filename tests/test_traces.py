@@ -252,3 +252,34 @@ def test_exec_signal_queued_lists(C, ctx):
     for c in range(48):
         want = es[eo[c]:eo[c + 1]] if fl[c] else np.zeros(0, np.uint32)
         assert np.array_equal(got[got_off[c]:got_off[c + 1]], want), c
+
+
+def test_triage_traces_queued_host(C, ctx):
+    """sg_triage_traces_queued: host traces in, the fuzzer's flags, both set
+    updates and the queued calls' executor-exact lists out, against the
+    oracle (executor.h:389-401 lists, then the loop of fuzzer.go:645-693 over
+    them, which the set-exact triage of the traces equals); three batches in
+    a row on the same sets, with empty calls and an empty program."""
+    rng = np.random.default_rng(909)
+    ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
+    om, on = O.OSet(), O.OSet()
+    m0 = _zipf_pcs(rng, 3000, nranks=1 << 12)
+    C.SignalAdd(ms, m0)
+    om.add(m0)
+    for b in range(3):
+        lens = rng.integers(0, 400, size=60)
+        lens[rng.integers(0, 60, size=8)] = 0
+        call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        prog_off = np.array([0, 7, 7, 20, 33, 41, 60], np.uint64)
+        p = _zipf_pcs(rng, int(call_off[-1]), nranks=1 << 12)
+        es, eo = O.exec_signal(p, call_off, prog_off)
+        ef = O.triage_flags_only(om, on, es, eo)
+        flags, vals, off = C.triage_traces_queued(ms, ns, p, call_off, prog_off, ctx=ctx)
+        assert np.array_equal(flags, ef), b
+        assert 0 < ef.sum() < 60
+        for c in range(60):
+            want = es[eo[c]:eo[c + 1]] if ef[c] else np.zeros(0, np.uint32)
+            assert np.array_equal(vals[off[c]:off[c + 1]], want), (b, c)
+        assert np.array_equal(ms.export(), om.export()) and np.array_equal(ns.export(), on.export())
+    ms.close()
+    ns.close()
