@@ -47,8 +47,14 @@
 
 namespace sg {
 
-constexpr int kPT = 16384;                   // entries per partition tile / chunk
-constexpr int kPThreads = 1024;              // 16 waves
+#ifndef SG_PT
+#define SG_PT 16384
+#endif
+#ifndef SG_PTHREADS
+#define SG_PTHREADS 1024
+#endif
+constexpr int kPT = SG_PT;                   // entries per partition tile / chunk
+constexpr int kPThreads = SG_PTHREADS;       // 16 waves
 constexpr int kPWaves = kPThreads / 64;
 constexpr int kPerWave = kPT / kPWaves;      // 1024 entries per wave, in order
 constexpr int kSteps = kPerWave / 64;        // 16 entries per lane
