@@ -8,7 +8,7 @@
 //
 // The dedup decisions are inherently sequential within a program (each
 // insert can change later lookups), so one wave owns one program and its
-// 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 128
+// 8192-slot table lives in that wave's LDS (32 KiB).  The wave computes 64
 // edges at a time in parallel (pc ^ hash(prev pc) needs only a neighbour
 // shift) and decides their dedup speculatively: all of them probe the table at
 // once, and the decisions are kept up to the first edge whose decision slot an
@@ -242,6 +242,160 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
   }
 }
 
+// The product kernel: k_exec_signal's speculative window with W edges held
+// in K slots per lane (position 64 k + lane in slot k); the mark tables and
+// the decision rules are k_exec_signal's (whose 128-edge window, K = 2, is
+// kept for the pass counters of SG_DEBUG_PART).  One 64-edge window per
+// wave step is fastest: a wider window decides more edges per pass but needs
+// more passes (the first undecided edge ends a pass), a narrower one idles
+// lanes.
+template <int K, int W = 64 * K>
+__global__ __launch_bounds__(64) void k_exec_signal_k(const uint32_t* __restrict__ pcs,
+                                                      const uint64_t* __restrict__ call_off,
+                                                      const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
+                                                      uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
+                                                      const uint8_t* __restrict__ emit) {
+  static_assert(W <= 64 * K && W > 64 * (K - 1), "W edges per window in K slots");
+  __shared__ uint32_t table[kDedupSize];
+  __shared__ unsigned long long markA[kMarkN], markB[kMarkN];
+  const int lane = threadIdx.x;
+  const uint64_t p = blockIdx.x;
+  const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
+  if (c1 <= c0) return;
+  for (uint32_t i = lane; i < kDedupSize; i += 64) table[i] = 0;
+  for (uint32_t i = lane; i < kMarkN; i += 64) markA[i] = markB[i] = kNoMark;
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t pend = call_off[c1];
+  const uint64_t w0 = call_off[c0];
+  uint32_t npc[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint64_t q = w0 + 64 * k + lane;
+    npc[k] = q < pend ? pcs[q] : 0u;
+  }
+  for (uint64_t c = c0; c < c1; c++) {
+    const uint64_t b = call_off[c], e = call_off[c + 1];
+    const bool em = !emit || emit[c] != 0;
+    uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
+    uint64_t outpos = b;
+    for (uint64_t j = b; j < e; j += W) {
+      const int nvalid = (int)((e - j) < (uint64_t)W ? (e - j) : (uint64_t)W);
+      uint32_t pc[K], sig[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) pc[k] = 64 * k + lane < nvalid ? npc[k] : 0u;
+      const uint64_t nj = j + W < e ? j + W : e;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint64_t q = nj + 64 * k + lane;
+        const uint32_t l = pcs[q < pend ? q : pend - 1];
+        npc[k] = q < pend ? l : 0u;
+      }
+      uint32_t h[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) h[k] = exec_hash(pc[k]);
+      uint32_t in = carry;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint32_t hp = (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)h[k], 0x138 /* wave_shr:1 */, 0xF, 0xF,
+                                                                  false);
+        sig[k] = pc[k] ^ hp;  // executor.h:393-395
+        in = __builtin_amdgcn_readlane(h[k], 63);
+      }
+      {
+        const int lastk = (nvalid - 1) >> 6, lastl = (nvalid - 1) & 63;
+        uint32_t cv = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+          if (k == lastk) cv = __builtin_amdgcn_readlane(h[k], lastl);
+        carry = cv;
+      }
+      uint64_t keep[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) keep[k] = 0;
+      for (int start = 0; start < nvalid;) {
+        bool act[K], wr[K], bd[K], dt[K];
+        uint32_t d[K];
+        uint64_t wm[K];
+        int nw = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const int pos = 64 * k + lane;
+          act[k] = pos >= start && pos < nvalid;
+          bool dup;
+          probe(table, sig[k], d[k], dup);
+          wr[k] = act[k] && !dup;
+          wm[k] = __ballot(wr[k]);
+          nw += __popcll(wm[k]);
+          bd[k] = dt[k] = false;
+        }
+        int f = nvalid;
+        if (nw) {
+          if (nw == 1) {  // one writer: compare against it directly
+            uint32_t di = 0, si = 0, iw = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++)
+              if (wm[k]) {
+                const uint32_t l = (uint32_t)(__ffsll((unsigned long long)wm[k]) - 1);
+                di = __builtin_amdgcn_readlane(d[k], l);
+                si = __builtin_amdgcn_readlane(sig[k], l);
+                iw = 64u * k + l;
+              }
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+              const bool ek = act[k] && (uint32_t)(64 * k + lane) > iw && d[k] == di;
+              bd[k] = ek && sig[k] == si;
+              dt[k] = ek && !bd[k];
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < K; k++)
+              if (wr[k]) {
+                const unsigned long long v = mark_val(64u * k + lane, d[k], sig[k]);
+                __hip_atomic_fetch_min(&markA[d[k] & (kMarkN - 1)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_min(&markB[d[k] >> 4], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long ma[K], mb[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+              ma[k] = mark_load(&markA[d[k] & (kMarkN - 1)]);
+              mb[k] = mark_load(&markB[d[k] >> 4]);
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < K; k++)
+              if (wr[k]) markA[d[k] & (kMarkN - 1)] = markB[d[k] >> 4] = kNoMark;
+#pragma unroll
+            for (int k = 0; k < K; k++) resolve(ma[k], mb[k], 64u * k + lane, d[k], sig[k], act[k], bd[k], dt[k]);
+          }
+#pragma unroll
+          for (int k = K - 1; k >= 0; k--) {  // the first undecided position
+            const uint64_t um = __ballot(dt[k]);
+            if (um) f = 64 * k + __ffsll((unsigned long long)um) - 1;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const bool cm = wr[k] && !bd[k] && 64 * k + lane < f;
+          if (cm) table[d[k]] = sig[k];
+          keep[k] |= __ballot(cm);
+        }
+        start = f;
+      }
+      asm volatile("" ::"v"(npc[0]));
+      if (em) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          if ((keep[k] >> lane) & 1ull) tmp[outpos + __popcll(keep[k] & lt)] = sig[k];
+          outpos += __popcll(keep[k]);
+        }
+      }
+    }
+    if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
+  }
+}
+
 // the calls each program has to run for its queued calls' lists: up to and
 // including its last queued call (fuzzer.go:678-683 copies the signal of
 // queued records only); pstop[p] = prog_off[p] when it has none
@@ -421,8 +575,29 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
             (unsigned long long)nprog, h[0], h[1], h[0] ? (double)h[1] / h[0] : 0.0, h[2]);
   } else if (nprog) {
     ScopedTimer tm(ctx, "exec_signal");
-    hipLaunchKernelGGL(k_exec_signal<false>, dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off,
-                       d_prog_off, tmp, cnt, (unsigned long long*)nullptr, (const uint64_t*)pstop, d_rec_new);
+    // window of 64 edges by default (SG_EXEC_K = 2, 3, 4: 64 K edges; 32 / 48:
+    // part-filled windows -- measurements; 1.89 ms per 134M PCs at 64 against
+    // 2.24 at 128, 2.69 at 192, 3.41 at 256, 2.32 at 48 and 3.06 at 32)
+    static const int kx = [] {
+      const char* e = getenv("SG_EXEC_K");
+      return e ? atoi(e) : 1;
+    }();
+    const dim3 g((uint32_t)nprog), t(64);
+    const uint64_t* ps = (const uint64_t*)pstop;
+    if (kx == 2)
+      hipLaunchKernelGGL((k_exec_signal_k<2>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kx == 3)
+      hipLaunchKernelGGL((k_exec_signal_k<3>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kx == 4)
+      hipLaunchKernelGGL((k_exec_signal_k<4>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kx == 32)
+      hipLaunchKernelGGL((k_exec_signal_k<1, 32>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kx == 48)
+      hipLaunchKernelGGL((k_exec_signal_k<1, 48>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else
+      hipLaunchKernelGGL((k_exec_signal_k<1>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
   }
   SG_HIP(hipGetLastError());
   rc = scan_counts(ctx, cnt, d_sig_off, ncalls, scan_off);
