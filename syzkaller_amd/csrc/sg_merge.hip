@@ -776,6 +776,93 @@ __global__ __launch_bounds__(kBlock) void k_sort_unique_chunks(uint32_t* vals, c
   if (threadIdx.x == 0) out_len[seg[blockIdx.x]] = total;
 }
 
+// Lists of <= kWaveList values: one wave per list, sorted by a bitonic
+// network over the wave's registers (E = P / 64 values per lane, element i =
+// lane E + r; partners inside a lane swap in registers, the rest come by
+// __shfl_xor -- no LDS and no barrier), then deduplicated and written back in
+// place with a wave prefix sum.  Four lists per workgroup.  (A workgroup per
+// list, with LDS stages and barriers, spent most of its time on the padding
+// of short lists and on its barriers.)
+constexpr uint32_t kWaveList = 1024;
+
+template <int E>
+__device__ __forceinline__ void canon_wave(uint32_t* __restrict__ vals, const SortChunk& ch, uint64_t* out_len_slot) {
+  const uint32_t lane = threadIdx.x & 63;
+  constexpr uint32_t P = 64 * E;
+  uint32_t v[E];
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const uint32_t i = lane * E + r;
+    v[r] = i < ch.len ? vals[ch.start + i] : kSent;
+  }
+#pragma unroll
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j < (uint32_t)E) {
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          if ((r & j) == 0) {
+            const uint32_t i = lane * E + r;
+            const bool up = (i & k) == 0;
+            const uint32_t x = v[r], y = v[r | j];
+            const bool sw = (x > y) == up;
+            v[r] = sw ? y : x;
+            v[r | j] = sw ? x : y;
+          }
+        }
+      } else {
+        const int m = (int)(j / E);
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const uint32_t i = lane * E + r, y = (uint32_t)__shfl_xor((int)v[r], m);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[r] = keep_min ? min(v[r], y) : max(v[r], y);
+        }
+      }
+    }
+  }
+  // cover.go:31-37: x != the previous sorted value, the first against kSent
+  const uint32_t before = (uint32_t)__shfl_up((int)v[E - 1], 1);
+  uint32_t keep = 0;
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const uint32_t i = lane * E + r;
+    const uint32_t prev = r ? v[r - 1] : (lane ? before : kSent);
+    if (i < ch.len && v[r] != prev) keep |= 1u << r;
+  }
+  const uint32_t c = __popc(keep), incl = sgd::wave_incl_add(c);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  uint32_t pos = incl - c;
+  uint32_t* out = vals + ch.start;
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const uint32_t i = lane * E + r;
+    if ((keep >> r) & 1u) out[pos++] = v[r];
+    if (i >= total && i < ch.len) out[i] = v[r];  // the stale tail: the sorted values (disjoint positions)
+  }
+  if (lane == 0) *out_len_slot = total;
+}
+
+__global__ __launch_bounds__(256) void k_canon_waves(uint32_t* __restrict__ vals, const SortChunk* __restrict__ chunks,
+                                                     const uint32_t* __restrict__ seg, uint32_t n,
+                                                     uint64_t* __restrict__ out_len) {
+  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n) return;  // (a wave leaves whole: no block barrier follows)
+  const SortChunk ch = chunks[w];
+  uint64_t* slot = out_len + seg[w];
+  if (ch.len <= 64)
+    canon_wave<1>(vals, ch, slot);
+  else if (ch.len <= 128)
+    canon_wave<2>(vals, ch, slot);
+  else if (ch.len <= 256)
+    canon_wave<4>(vals, ch, slot);
+  else if (ch.len <= 512)
+    canon_wave<8>(vals, ch, slot);
+  else
+    canon_wave<16>(vals, ch, slot);
+}
+
 struct BigSeg {
   uint64_t start;  // global element index of the segment
   uint64_t len;
@@ -886,24 +973,47 @@ __global__ void k_unique_write(CanonArgs a) {
 // chunks: one per non-empty segment, in segment order
 static int canonicalize_small(sg_ctx* ctx, uint32_t* d_vals, const uint64_t* off, uint64_t nseg,
                               const std::vector<SortChunk>& chunks, uint64_t* out_len) {
-  std::vector<uint32_t> seg;
-  seg.reserve(chunks.size());
+  // lists of <= kWaveList values a wave each (k_canon_waves), longer ones a
+  // workgroup each (k_sort_unique_chunks); chunks are the non-empty segments
+  std::vector<SortChunk> wch, bch;
+  std::vector<uint32_t> wseg, bseg;
+  size_t ci = 0;
   for (uint64_t k = 0; k < nseg; k++)
-    if (off[k + 1] > off[k]) seg.push_back((uint32_t)k);
+    if (off[k + 1] > off[k]) {
+      const SortChunk& c = chunks[ci++];
+      if (c.len <= kWaveList) {
+        wch.push_back(c);
+        wseg.push_back((uint32_t)k);
+      } else {
+        bch.push_back(c);
+        bseg.push_back((uint32_t)k);
+      }
+    }
   WsPlan p;
-  const size_t o_ch = p.add(chunks.size() * sizeof(SortChunk)), o_seg = p.add(seg.size() * 4), o_len = p.add(nseg * 8);
+  const size_t o_wch = p.add(wch.size() * sizeof(SortChunk)), o_wseg = p.add(wseg.size() * 4),
+               o_bch = p.add(bch.size() * sizeof(SortChunk)), o_bseg = p.add(bseg.size() * 4), o_len = p.add(nseg * 8);
   int rc = ws_reserve(ctx, p.total);
   if (rc) return rc;
-  SortChunk* dch = (SortChunk*)ws_at(ctx, o_ch);
-  uint32_t* dseg = (uint32_t*)ws_at(ctx, o_seg);
   uint64_t* dlen = (uint64_t*)ws_at(ctx, o_len);
   SG_HIP(hipMemsetAsync(dlen, 0, nseg * 8, ctx->stream));  // (empty segments)
-  if (!chunks.empty()) {
-    SG_HIP(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(SortChunk), hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipMemcpyAsync(dseg, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (!wch.empty() || !bch.empty()) {
     ScopedTimer tm(ctx, "canon_sort");
-    hipLaunchKernelGGL(k_sort_unique_chunks, dim3((uint32_t)chunks.size()), dim3(kBlock), 0, ctx->stream, d_vals, dch,
-                       dseg, dlen);
+    if (!wch.empty()) {
+      SortChunk* dch = (SortChunk*)ws_at(ctx, o_wch);
+      uint32_t* dseg = (uint32_t*)ws_at(ctx, o_wseg);
+      SG_HIP(hipMemcpyAsync(dch, wch.data(), wch.size() * sizeof(SortChunk), hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(dseg, wseg.data(), wseg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+      hipLaunchKernelGGL(k_canon_waves, dim3((uint32_t)div_up(wch.size(), 4)), dim3(256), 0, ctx->stream, d_vals,
+                         (const SortChunk*)dch, (const uint32_t*)dseg, (uint32_t)wch.size(), dlen);
+    }
+    if (!bch.empty()) {
+      SortChunk* dch = (SortChunk*)ws_at(ctx, o_bch);
+      uint32_t* dseg = (uint32_t*)ws_at(ctx, o_bseg);
+      SG_HIP(hipMemcpyAsync(dch, bch.data(), bch.size() * sizeof(SortChunk), hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(dseg, bseg.data(), bseg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+      hipLaunchKernelGGL(k_sort_unique_chunks, dim3((uint32_t)bch.size()), dim3(kBlock), 0, ctx->stream, d_vals, dch,
+                         dseg, dlen);
+    }
   }
   SG_HIP(hipGetLastError());
   SG_HIP(hipMemcpyAsync(out_len, dlen, nseg * 8, hipMemcpyDeviceToHost, ctx->stream));

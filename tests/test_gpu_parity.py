@@ -217,6 +217,9 @@ def test_canonicalize_batch_tile_segments(C):
     4096-element segments, and many short lists."""
     rng = np.random.default_rng(132)
     lens = [0, 1, 4096, 0, 3, 4095, 64, 65, 2] + [int(x) for x in rng.integers(0, 300, size=400)] + [0]
+    # the wave-per-list sizes (<= 1024: 64-1024-slot networks) and their edges
+    lens += [127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 2048]
+    lens += [int(x) for x in rng.integers(0, 1100, size=200)]
     segs = []
     for k, L in enumerate(lens):
         v = rng.integers(0, [4, 1000, 1 << 32][k % 3], size=L, dtype=np.uint64).astype(np.uint32)
