@@ -120,6 +120,74 @@ __global__ __launch_bounds__(256) void k_enc_write(const uint32_t* __restrict__ 
   }
 }
 
+// Encode, one wave per list (four per workgroup): the list in steps of 64
+// values, each lane's delta against the value before it (across a step: the
+// previous step's lane 63), and its varint.  Pass A: the list's byte count
+// (and the sortedness check); pass B, after a scan of the counts: each value's
+// bytes at the list's start + a wave prefix sum of the lengths.  No per-value
+// list search (the per-element form looks its list up for every value).
+__device__ __forceinline__ uint32_t list_delta(const uint32_t* v, uint64_t i, uint64_t e0, uint32_t x, uint32_t prev,
+                                               bool& bad) {
+  if (i == e0) return x;
+  bad |= x < prev;
+  return x - prev;
+}
+
+__global__ __launch_bounds__(256) void k_enc_list_len(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                                                      uint64_t n, uint32_t* __restrict__ lbytes,
+                                                      uint32_t* __restrict__ err) {
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t e0 = off[k], e1 = off[k + 1];
+  uint32_t carry = 0, tot = 0;
+  bool bad = false;
+  for (uint64_t b = e0; b < e1; b += 64) {
+    const uint64_t i = b + lane;
+    const uint32_t x = i < e1 ? v[i] : 0u;
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+    uint32_t len = 0;
+    if (i < e1) len = varint_len(list_delta(v, i, e0, x, up, bad));
+    tot += __builtin_amdgcn_readlane(sgd::wave_incl_add(len), 63);
+    carry = __builtin_amdgcn_readlane(x, 63);
+  }
+  if (lane == 0) lbytes[k] = tot;
+  if (__any(bad) && lane == 0) atomicOr(err, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_enc_list_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
+                                                        uint64_t n, const uint64_t* __restrict__ boff,
+                                                        uint8_t* __restrict__ out) {
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t e0 = off[k], e1 = off[k + 1];
+  uint64_t pos = boff[k];
+  uint32_t carry = 0;
+  bool bad = false;  // (checked by pass A)
+  for (uint64_t b = e0; b < e1; b += 64) {
+    const uint64_t i = b + lane;
+    const uint32_t x = i < e1 ? v[i] : 0u;
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x, 0x138, 0xF, 0xF, false);
+    uint32_t d = 0, len = 0;
+    if (i < e1) {
+      d = list_delta(v, i, e0, x, up, bad);
+      len = varint_len(d);
+    }
+    const uint32_t incl = sgd::wave_incl_add(len);
+    if (i < e1) {
+      uint8_t* o = out + pos + (incl - len);
+      while (d >= 0x80u) {  // binary.PutUvarint
+        *o++ = (uint8_t)(d | 0x80u);
+        d >>= 7;
+      }
+      *o = (uint8_t)d;
+    }
+    pos += __builtin_amdgcn_readlane(incl, 63);
+    carry = __builtin_amdgcn_readlane(x, 63);
+  }
+}
+
 // byte offsets of the lists: out_off[k] = gbase[g] + the bytes of group g's
 // elements before off[k] (g = off[k] / 64)
 __global__ void k_list_bpos(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
@@ -252,6 +320,85 @@ __global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t*
   }
 }
 
+// Pass 2 (one wave per list, four per workgroup): the list's bytes in steps
+// of 64 x 16 (16 consecutive bytes per lane plus the 5 before, for runs that
+// open earlier); each terminator decodes its run backwards (LEB128: the
+// earlier byte holds the lower bits), the lanes' value counts and 64-bit delta
+// sums are scanned across the wave, and each value is written as the
+// running sum at the list's value offset (pass 1).  One read of the payload,
+// one write of the values, no per-value arrays.  Checks (binary.Uvarint, then
+// the running sum): a run of <= 5 bytes fitting 32 bits, the list ending on a
+// terminator, every sum within 32 bits.
+constexpr int kDecB = 16, kDecPre = 5;
+__global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                   const uint64_t* __restrict__ voff, uint64_t n,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;  // (a wave leaves whole)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = in_off[k], b1 = in_off[k + 1];
+  uint64_t vi = voff[k], run = 0;
+  bool bad = false;
+  for (uint64_t cb = b0; cb < b1; cb += 64 * kDecB) {
+    const uint64_t base = cb + (uint64_t)lane * kDecB;
+    uint32_t c[kDecPre + kDecB];
+#pragma unroll
+    for (int j = 0; j < kDecPre + kDecB; j++) {
+      const uint64_t p = base + j - kDecPre;  // (wraps below 0 only where base < kDecPre, then p >= b1 or < b0)
+      // before the list: a stop for the walk back; past it: never a terminator
+      c[j] = (base + j >= b0 + kDecPre && p < b1) ? (uint32_t)in[p] : (p >= b1 && base + j >= b0 + kDecPre ? 0x80u : 0u);
+    }
+    uint32_t tmask = 0;
+#pragma unroll
+    for (int i = 0; i < kDecB; i++)
+      if (base + i < b1 && !(c[kDecPre + i] & 0x80u)) tmask |= 1u << i;
+    uint32_t d[kDecB];
+    uint64_t t = 0;
+#pragma unroll
+    for (int i = 0; i < kDecB; i++) {
+      d[i] = 0;
+      if ((tmask >> i) & 1u) {
+        const int j = kDecPre + i;
+        uint64_t v = c[j] & 0x7Fu;
+        bool open = true;
+#pragma unroll
+        for (int q = 1; q <= kDecPre; q++) {
+          const uint32_t cc = c[j - q];
+          if (open && (cc & 0x80u)) {
+            if (q == kDecPre) bad = true;  // a sixth byte: more than binary.Uvarint's 32-bit range here
+            v = (v << 7) | (cc & 0x7Fu);
+          } else {
+            open = false;
+          }
+        }
+        bad |= v > 0xFFFFFFFFull;
+        d[i] = (uint32_t)v;
+        t += v;
+      }
+    }
+    const uint32_t cnt = __popc(tmask), ex = sgd::wave_incl_add(cnt) - cnt;
+    uint64_t sc = t;  // inclusive scan of the lanes' delta sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(sc, o);
+      if (lane >= (uint32_t)o) sc += y;
+    }
+    uint64_t acc = run + (sc - t);
+    uint64_t idx = vi + ex;
+#pragma unroll
+    for (int i = 0; i < kDecB; i++)
+      if ((tmask >> i) & 1u) {
+        acc += d[i];
+        bad |= acc > 0xFFFFFFFFull;
+        out[idx++] = (uint32_t)acc;
+      }
+    run += __shfl(sc, 63);
+    vi += __builtin_amdgcn_readlane(ex + cnt, 63);
+  }
+  if (lane == 0 && b1 > b0 && (in[b1 - 1] & 0x80u)) bad = true;  // the list ends inside a value
+  if (__any(bad) && lane == 0) atomicOr(err, 1u);
+}
+
 __global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __restrict__ off,
                          const uint64_t* __restrict__ kw, uint64_t n, uint64_t N, uint64_t* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -263,6 +410,16 @@ __global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __res
       out[k + 1 + e] = (0xFFFFFFFFull << 32) + cov[e];  // RestorePC(pc, 0xffffffff), cover.go:23-25
     }
   }
+}
+
+static bool enc_elems() {  // read at each call (tests switch it)
+  const char* e = getenv("SG_RPC_ENCODE_ELEMS");
+  return e && atoi(e) != 0;
+}
+
+static bool dec_blocks() {  // read at each call (tests switch it)
+  const char* e = getenv("SG_RPC_DECODE_BLOCKS");
+  return e && atoi(e) != 0;
 }
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::min<uint64_t>(div_up(n ? n : 1, 256), 16384); }
@@ -282,9 +439,9 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
   WsPlan p;
   const uint64_t ng = (N + 63) / 64;
   const size_t o_len = p.add(ng * 4 + 4), o_pos = p.add((ng + 1) * 8), o_lo = p.add((n + 1) * 8), o_err = p.add(8),
-               o_out = p.add(N * 5 + 8), o_kw = p.add((N + 31) / 32 * 8);
+               o_out = p.add(N * 5 + 8), o_kw = p.add((N + 31) / 32 * 8), o_lb = p.add(n * 4 + 4);
   const size_t scan_off = p.total;
-  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(N));
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(std::max(N, n)));
   if (rc) return rc;
   uint32_t* len = (uint32_t*)ws_at(ctx, o_len);
   uint64_t* pos = (uint64_t*)ws_at(ctx, o_pos);
@@ -293,7 +450,18 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
   uint8_t* out = (uint8_t*)ws_at(ctx, o_out);
   uint64_t* kw = (uint64_t*)ws_at(ctx, o_kw);
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
-  {
+  // (a list's byte count is a u32: the per-list form when 5 N cannot overflow it)
+  if (!enc_elems() && N * 5 < (1ull << 32)) {
+    ScopedTimer tm(ctx, "rpc_encode");
+    uint32_t* lbytes = (uint32_t*)ws_at(ctx, o_lb);
+    hipLaunchKernelGGL(k_enc_list_len, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_v, d_off, n, lbytes,
+                       err);
+    rc = scan_counts(ctx, lbytes, lo, n, scan_off);  // lo = list byte offsets (lo[n] = total)
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_enc_list_write, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_v, d_off, n,
+                       (const uint64_t*)lo, out);
+  } else {
+    // (SG_RPC_ENCODE_ELEMS=1: the per-element form)
     ScopedTimer tm(ctx, "rpc_encode");
     if (N) {
       hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_off, n, N, kw);
@@ -353,17 +521,25 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
     set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
     return SG_EINVAL;
   }
-  if (nb) {
-    SG_HIP(hipMemsetAsync(heads, 0, nblk * 4 + 4, ctx->stream));
-    hipLaunchKernelGGL(k_byte_heads, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_in_off, n, heads);
-    hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, heads, nb, vbase, delta, err);
-  }
-  rc = scan_counts(ctx, delta, excl, N, scan_off);
-  if (rc) return rc;
-  if (N) {
-    hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_voff, n, N, kwv);
-    hipLaunchKernelGGL(k_dec_values, dim3(grid_for(N)), dim3(256), 0, ctx->stream, delta, excl, d_voff, kwv, N, d_vals,
-                       err);
+  if (nb && !dec_blocks()) {
+    hipLaunchKernelGGL(k_dec_lists, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_in, d_in_off,
+                       (const uint64_t*)d_voff, n, d_vals, err);
+  } else {
+    // (SG_RPC_DECODE_BLOCKS=1: the per-block form -- runs per 32-byte block,
+    // then a scan of the deltas)
+    if (nb) {
+      SG_HIP(hipMemsetAsync(heads, 0, nblk * 4 + 4, ctx->stream));
+      hipLaunchKernelGGL(k_byte_heads, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_in_off, n, heads);
+      hipLaunchKernelGGL(k_dec_runs, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, heads, nb, vbase, delta,
+                         err);
+    }
+    rc = scan_counts(ctx, delta, excl, N, scan_off);
+    if (rc) return rc;
+    if (N) {
+      hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_voff, n, N, kwv);
+      hipLaunchKernelGGL(k_dec_values, dim3(grid_for(N)), dim3(256), 0, ctx->stream, delta, excl, d_voff, kwv, N,
+                         d_vals, err);
+    }
   }
   SG_HIP(hipGetLastError());
   uint32_t herr = 0;

@@ -47,8 +47,12 @@ def _lists(rng, n):
 
 
 @pytest.mark.gpu
-def test_delta_batch_vs_oracle(ctx):
+@pytest.mark.parametrize("blocks", ["0", "1"])  # the wave-per-list codec / the per-block and per-element forms
+def test_delta_batch_vs_oracle(ctx, monkeypatch, blocks):
     from syzkaller_amd import cover as C
+
+    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
+    monkeypatch.setenv("SG_RPC_ENCODE_ELEMS", blocks)
 
     rng = np.random.default_rng(42)
     lists = _lists(rng, 200)
@@ -62,6 +66,15 @@ def test_delta_batch_vs_oracle(ctx):
     from syzkaller_amd._lib import SyzSigError
     with pytest.raises(SyzSigError):
         C.delta_encode(np.array([5, 3], np.uint32), np.array([0, 2], np.uint64), ctx=ctx)
+    # a descent exactly across the encoder's 64-value step, in the 2nd list
+    u = np.arange(300, dtype=np.uint32)
+    u[64] = 62
+    with pytest.raises(SyzSigError):
+        C.delta_encode(np.concatenate([u[:10], u]), np.array([0, 10, 310], np.uint64), ctx=ctx)
+    # ... but a list may start below the previous one's end
+    w = np.concatenate([np.arange(100, 200, dtype=np.uint32), np.arange(0, 64, dtype=np.uint32)])
+    wd, wo = C.delta_encode(w, np.array([0, 100, 164], np.uint64), ctx=ctx)
+    assert wd.tobytes() == O.delta_encode(w[:100]) + O.delta_encode(w[100:])
     # malformed payloads -> rejected
     for bad in (b"\x05\x80", b"\xff\xff\xff\xff\x1f", b"\xff\xff\xff\xff\x0f\x01", b"\xff\xff\xff\xff\xff\x01"):
         with pytest.raises(SyzSigError):
@@ -111,18 +124,21 @@ def test_sancov_batch_vs_oracle(ctx):
 
 
 @pytest.mark.gpu
-def test_delta_decode_corrupted_payloads_vs_oracle(ctx):
+@pytest.mark.parametrize("blocks", ["0", "1"])
+def test_delta_decode_corrupted_payloads_vs_oracle(ctx, monkeypatch, blocks):
     """Decode accepts / rejects exactly what binary.Uvarint + a running sum do
     (oracle), on payloads with flipped high bits and cut ends, including runs
-    that cross the decoder's 32-byte blocks and list boundaries."""
+    that cross the decoder's 32-byte blocks, its 1 KiB wave steps and list
+    boundaries."""
     from syzkaller_amd import cover as C
     from syzkaller_amd._lib import SyzSigError
 
+    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
     rng = np.random.default_rng(7)
-    for t in range(120):
+    for t in range(160):
         parts = []
         for _ in range(int(rng.integers(1, 4))):
-            m = int(rng.integers(0, 60))
+            m = int(rng.integers(0, 60 if t < 120 else 1500))
             v = np.sort(rng.integers(0, 1 << 32, size=m, dtype=np.uint64)).astype(np.uint32)
             parts.append(bytearray(O.delta_encode(v)))
         for p in parts:
