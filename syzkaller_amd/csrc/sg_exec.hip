@@ -214,6 +214,10 @@ __global__ __launch_bounds__(64) void k_exec_signal(const uint32_t* __restrict__
           }
           const uint64_t um0 = __ballot(dt0), um1 = __ballot(dt1);
           f = um0 ? __ffsll((unsigned long long)um0) - 1 : (um1 ? 64 + __ffsll((unsigned long long)um1) - 1 : nvalid);
+          // a zero signal's overwrite empties its slot (see k_exec_signal_k)
+          const uint64_t zm0 = __ballot(wr0 && sig0 == 0u), zm1 = __ballot(wr1 && sig1 == 0u);
+          const int fz = zm0 ? __ffsll((unsigned long long)zm0) : (zm1 ? 64 + __ffsll((unsigned long long)zm1) : nvalid);
+          f = fz < f ? fz : f;
         }
         const bool cm0 = wr0 && !bd0 && (int)pos0 < f, cm1 = wr1 && !bd1 && (int)pos1 < f;
         if (cm0) table[d0] = sig0;
@@ -374,6 +378,17 @@ __global__ __launch_bounds__(64) void k_exec_signal_k(const uint32_t* __restrict
             const uint64_t um = __ballot(dt[k]);
             if (um) f = 64 * k + __ffsll((unsigned long long)um) - 1;
           }
+          // A zero signal writes only when its four slots are taken, and then
+          // overwrites slot 0 with 0: it EMPTIES a slot, which can change any
+          // later edge's outcome (the rules above assume slots stay taken).
+          // The pass ends after the first zero writer.
+          int fz = nvalid;
+#pragma unroll
+          for (int k = K - 1; k >= 0; k--) {
+            const uint64_t zm = __ballot(wr[k] && sig[k] == 0u);
+            if (zm) fz = 64 * k + __ffsll((unsigned long long)zm);
+          }
+          f = fz < f ? fz : f;
         }
 #pragma unroll
         for (int k = 0; k < K; k++) {
@@ -382,6 +397,189 @@ __global__ __launch_bounds__(64) void k_exec_signal_k(const uint32_t* __restrict
           keep[k] |= __ballot(cm);
         }
         start = f;
+      }
+      asm volatile("" ::"v"(npc[0]));
+      if (em) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          if ((keep[k] >> lane) & 1ull) tmp[outpos + __popcll(keep[k] & lt)] = sig[k];
+          outpos += __popcll(keep[k]);
+        }
+      }
+    }
+    if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
+  }
+}
+
+// Slot regions (r04): lane r of the wave owns the 128 table slots
+// [128 r, 128 r + 127] and decides, in program order, the window's edges whose
+// home slot sig % 8192 lies there.  An edge reads and writes only its probe
+// slots home .. home + 3, so two edges can interact only when those ranges
+// meet: edges of one region (one lane, taken in order), or an edge whose
+// range runs into the next region (home % 128 >= 125, "spanning") and an edge
+// of that next region with home % 128 <= 2 ("low": the only ones that reach
+// slots 0..2 of their region).  A low edge waits until the lane to its left
+// has decided every edge before it, a spanning edge until the lane to its
+// right has; the earliest undecided edge of the window is always free, so
+// every step decides at least one edge, and any two edges sharing a slot are
+// decided in program order: the table ends each window exactly as the
+// sequential loop leaves it, and each edge sees exactly what it would.
+//
+// Per window of W = 64 K edges: each edge ORs its bit into its (row, region)
+// mask; the masks give every edge its place in a region-major list of
+// (position, signal) (regions' bases by a wave scan of their counts, the
+// rank inside a region by popcounts of the masks), so a lane then walks its
+// region's entries in program order with one LDS round trip per step (the
+// four probe slots and the next entry together); the decisions are bytes per
+// position, read back per row for the compaction stores.  Steps per window =
+// the most edges any region holds plus the waits (C2 traces, W = 256: ~25
+// edges per step, against ~28 per speculative pass of several LDS round trips
+// in k_exec_signal_k).
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+
+template <int K>
+__global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__ pcs,
+                                                    const uint64_t* __restrict__ call_off,
+                                                    const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
+                                                    uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
+                                                    const uint8_t* __restrict__ emit) {
+  constexpr int W = 64 * K;
+  // slots 8192..8194 mirror slots 0..2 (a probe reads 4 consecutive words);
+  // 8196 is a dummy slot that predicated-off writes go to
+  __shared__ uint32_t table[kDedupSize + 8];
+  __shared__ unsigned long long wlist[W];  // position << 32 | signal, region-major
+  __shared__ unsigned long long wmask[K][64];
+  __shared__ uint8_t wres[W + 4];  // the decision of position 64 k + l at l K + k; W: dummy
+  const int lane = threadIdx.x;
+  const uint64_t p = blockIdx.x;
+  const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
+  if (c1 <= c0) return;
+  for (uint32_t i = lane; i < kDedupSize + 8; i += 64) table[i] = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) wmask[k][lane] = 0;
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t pend = call_off[c1];
+  const uint64_t w0 = call_off[c0];
+  uint32_t npc[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint64_t q = w0 + 64 * k + lane;
+    npc[k] = q < pend ? pcs[q] : 0u;
+  }
+  for (uint64_t c = c0; c < c1; c++) {
+    const uint64_t b = call_off[c], e = call_off[c + 1];
+    const bool em = !emit || emit[c] != 0;
+    uint32_t carry = 0;  // hash of the previous PC; prev = 0 at call start (executor.h:389)
+    uint64_t outpos = b;
+    for (uint64_t j = b; j < e; j += W) {
+      const int nvalid = (int)((e - j) < (uint64_t)W ? (e - j) : (uint64_t)W);
+      uint32_t pc[K], sig[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) pc[k] = 64 * k + lane < nvalid ? npc[k] : 0u;
+      const uint64_t nj = j + W < e ? j + W : e;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint64_t q = nj + 64 * k + lane;
+        const uint32_t l = pcs[q < pend ? q : pend - 1];
+        npc[k] = q < pend ? l : 0u;
+      }
+      uint32_t h[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) h[k] = exec_hash(pc[k]);
+      uint32_t in = carry;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint32_t hp = (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)h[k], 0x138 /* wave_shr:1 */, 0xF, 0xF,
+                                                                  false);
+        sig[k] = pc[k] ^ hp;  // executor.h:393-395
+        in = __builtin_amdgcn_readlane(h[k], 63);
+      }
+      {
+        const int lastk = (nvalid - 1) >> 6, lastl = (nvalid - 1) & 63;
+        uint32_t cv = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+          if (k == lastk) cv = __builtin_amdgcn_readlane(h[k], lastl);
+        carry = cv;
+      }
+      uint32_t rg[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        rg[k] = (sig[k] >> 7) & 63u;
+        if (64 * k + lane < nvalid)
+          __hip_atomic_fetch_or(&wmask[k][rg[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // (one wave: its LDS operations complete in issue order, so relaxed
+      // atomic loads after the wave barrier see every lane's OR; no
+      // __syncthreads, whose fence would also wait for the next window's PC loads)
+      __builtin_amdgcn_wave_barrier();
+      uint64_t em_[K], om[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        em_[k] = __hip_atomic_load(&wmask[k][rg[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        om[k] = __hip_atomic_load(&wmask[k][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        __hip_atomic_store(&wmask[k][lane], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // region lane: its count, its base in the list, each row's start in it
+      uint32_t n_r = 0, rowb[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        rowb[k] = n_r;
+        n_r += (uint32_t)__popcll(om[k]);
+      }
+      const uint32_t base = sgd::wave_incl_add(n_r) - n_r;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint32_t at = (uint32_t)__shfl((int)(base + rowb[k]), (int)rg[k]);
+        if (64 * k + lane < nvalid)
+          wlist[at + (uint32_t)__popcll(em_[k] & lt)] = ((unsigned long long)(64u * k + lane) << 32) | sig[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t iend = base + n_r;
+      uint32_t i = base;
+      unsigned long long cur = wlist[i < iend ? i : 0];
+      uint32_t pos = i < iend ? (uint32_t)(cur >> 32) : kNoPos;
+      uint32_t s = (uint32_t)cur;
+      // branch-free steps: every lane probes and writes, a lane with nothing
+      // to decide into the dummy slot / byte
+      while (__ballot(pos != kNoPos)) {
+        // the neighbours' next undecided positions (kNoPos: none left)
+        const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
+        const uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
+        const uint32_t hr = s & 127u;
+        const bool go = (pos != kNoPos) & ((hr > 2u) | (left > pos)) & ((hr < 125u) | (right > pos));
+        const uint32_t i2 = i + (go ? 1u : 0u);
+        const uint32_t home = s & (kDedupSize - 1);
+        const uint32_t t0 = table[home], t1 = table[home + 1], t2 = table[home + 2], t3 = table[home + 3];
+        const unsigned long long nx = wlist[i2 < iend ? i2 : 0];
+        // executor.h:509-525: the first of the four slots holding s (dup) or
+        // empty (insert there); all four taken: overwrite the home slot
+        const bool h0 = (t0 == s) | (t0 == 0u), h1 = (t1 == s) | (t1 == 0u), h2 = (t2 == s) | (t2 == 0u);
+        const uint32_t q = h0 ? 0u : h1 ? 1u : h2 ? 2u : ((t3 == s) | (t3 == 0u)) ? 3u : 0u;
+        const uint32_t tq = h0 ? t0 : h1 ? t1 : h2 ? t2 : t3;
+        const bool dup = (tq == s) & (h0 | h1 | h2 | (t3 == s) | (t3 == 0u));
+        const bool wr = go & !dup;
+        const uint32_t d = home + q;  // < 8195; slots 8192.. are the mirror of 0..2
+        const uint32_t dd = d & (kDedupSize - 1);
+        table[wr ? dd : kDedupSize + 4] = s;
+        table[wr && dd < 3u ? dd + kDedupSize : kDedupSize + 4] = s;
+        wres[go ? (pos & 63u) * K + (pos >> 6) : (uint32_t)W] = dup ? 0 : 1;
+        i = i2;
+        pos = i < iend ? (uint32_t)(nx >> 32) : kNoPos;
+        s = (uint32_t)nx;
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint64_t keep[K];
+      {
+        uint8_t rb[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) rb[k] = wres[lane * K + k];
+#pragma unroll
+        for (int k = 0; k < K; k++) keep[k] = __ballot(64 * k + lane < nvalid && rb[k] != 0);
       }
       asm volatile("" ::"v"(npc[0]));
       if (em) {
@@ -582,9 +780,25 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
       const char* e = getenv("SG_EXEC_K");
       return e ? atoi(e) : 1;
     }();
+    // slot-region kernel: SG_EXEC_REGION = rows per window (0: the speculative kernel)
+    const int kr = [] {  // (read at each call: tests switch it)
+      const char* e = getenv("SG_EXEC_REGION");
+      return e ? atoi(e) : 0;
+    }();
     const dim3 g((uint32_t)nprog), t(64);
     const uint64_t* ps = (const uint64_t*)pstop;
-    if (kx == 2)
+    if (kr == 1)
+      hipLaunchKernelGGL((k_exec_region<1>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kr == 2)
+      hipLaunchKernelGGL((k_exec_region<2>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kr == 4)
+      hipLaunchKernelGGL((k_exec_region<4>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kr == 8)
+      hipLaunchKernelGGL((k_exec_region<8>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
+    else if (kr == 16)
+      hipLaunchKernelGGL((k_exec_region<16>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kx == 2)
       hipLaunchKernelGGL((k_exec_signal_k<2>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
     else if (kx == 3)
       hipLaunchKernelGGL((k_exec_signal_k<3>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);

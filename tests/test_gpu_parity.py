@@ -606,6 +606,52 @@ def test_exec_signal_random_vs_oracle(C):
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
 
 
+def _exec_hash(a):  # executor.h:497-505
+    a = (a ^ 61) ^ (a >> 16)
+    a = (a + (a << 3)) & 0xFFFFFFFF
+    a = a ^ (a >> 4)
+    a = (a * 0x27D4EB2D) & 0xFFFFFFFF
+    return a ^ (a >> 15)
+
+
+def _trace_for_signals(sigs, call_off):
+    """PCs whose edge signals (pc ^ hash(prev pc), prev = 0 at call start) are `sigs`."""
+    pcs = np.zeros(len(sigs), np.uint32)
+    for c in range(len(call_off) - 1):
+        prev = 0
+        for i in range(int(call_off[c]), int(call_off[c + 1])):
+            pc = int(sigs[i]) ^ prev
+            pcs[i] = pc
+            prev = _exec_hash(pc)
+    return pcs
+
+
+@pytest.mark.parametrize("rows", ["0", "1", "2", "4", "8", "16"])  # 0: the speculative kernel
+def test_exec_signal_region_boundaries_vs_oracle(C, monkeypatch, rows):
+    """Signals crowded onto the slots where the slot-region kernel's lanes meet
+    (home % 128 in 124..127 and 0..3, table wrap-around 8189..8191 -> 0..2), a
+    few distinct high parts so probe windows fill and home slots get
+    overwritten, the zero signal, repeats: every window's decisions in
+    program order, as executor.h:507-526 takes them."""
+    monkeypatch.setenv("SG_EXEC_REGION", rows)
+    rng = np.random.default_rng(117)
+    homes = np.array([(r * 128 + d) % 8192 for r in (0, 1, 2, 31, 63) for d in range(-4, 4)], np.uint64)
+    for nprog, calls, pcs, nhigh in [(2, 3, 700, 3), (6, 4, 1500, 6), (3, 2, 5000, 40)]:
+        lens = rng.integers(1, 2 * pcs, size=nprog * calls).astype(np.uint64)
+        call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        n = int(call_off[-1])
+        hi = rng.integers(0, nhigh, size=n).astype(np.uint64) * 8192 + 8192 * 977
+        sigs = (hi + rng.choice(homes, size=n)) & 0xFFFFFFFF
+        sigs[rng.random(n) < 0.02] = 0
+        far = rng.random(n) < 0.3  # anywhere in the table
+        sigs[far] = rng.integers(0, 1 << 32, size=int(far.sum()), dtype=np.uint64)
+        trace = _trace_for_signals(sigs.astype(np.uint32), call_off)
+        prog_off = (np.arange(nprog + 1) * calls).astype(np.uint64)
+        a = C.exec_signal(trace, call_off, prog_off)
+        b = O.exec_signal(trace, call_off, prog_off)
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
+
+
 # ---- cover report (syz-manager/cover.go:257-307) ------------------------------------
 def _symtab(rng, nsym, base=0xffffffff81000000):
     starts = base + 16 * np.sort(rng.choice(nsym * 8, size=nsym, replace=False)).astype(np.uint64)
