@@ -437,12 +437,17 @@ __global__ __launch_bounds__(64) void k_exec_signal_k(const uint32_t* __restrict
 // in k_exec_signal_k).
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
+// stats (nullable, SG_DEBUG_PART): [0] windows, [1] steps, [2] cycles in
+// the steps, [3] cycles in the whole program loop, [4] edges
 template <int K>
 __global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__ pcs,
                                                     const uint64_t* __restrict__ call_off,
                                                     const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
                                                     uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
-                                                    const uint8_t* __restrict__ emit) {
+                                                    const uint8_t* __restrict__ emit,
+                                                    unsigned long long* __restrict__ stats = nullptr) {
+  unsigned long long n_win = 0, n_step = 0, cy_step = 0, n_edge = 0;
+  const unsigned long long cy0 = stats ? clock64() : 0;
   constexpr int W = 64 * K;
   // slots 8192..8194 mirror slots 0..2 (a probe reads 4 consecutive words);
   // 8196 is a dummy slot that predicated-off writes go to
@@ -546,7 +551,13 @@ __global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__
       uint32_t s = (uint32_t)cur;
       // branch-free steps: every lane probes and writes, a lane with nothing
       // to decide into the dummy slot / byte
+      const unsigned long long cs0 = stats ? clock64() : 0;
+      if (stats) {
+        n_win++;
+        n_edge += nvalid;
+      }
       while (__ballot(pos != kNoPos)) {
+        if (stats) n_step++;
         // the neighbours' next undecided positions (kNoPos: none left)
         const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
         const uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
@@ -572,6 +583,7 @@ __global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__
         pos = i < iend ? (uint32_t)(nx >> 32) : kNoPos;
         s = (uint32_t)nx;
       }
+      if (stats) cy_step += clock64() - cs0;
       __builtin_amdgcn_wave_barrier();
       uint64_t keep[K];
       {
@@ -591,6 +603,13 @@ __global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__
       }
     }
     if (lane == 0) cnt[c] = (uint32_t)(outpos - b);
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], n_win);
+    atomicAdd(&stats[1], n_step);
+    atomicAdd(&stats[2], cy_step);
+    atomicAdd(&stats[3], clock64() - cy0);
+    atomicAdd(&stats[4], n_edge);
   }
 }
 
@@ -760,7 +779,25 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   if (pstop && nprog)
     hipLaunchKernelGGL(k_prog_stop, dim3(div_up(nprog, 256)), dim3(256), 0, ctx->stream, d_prog_off, d_rec_new, nprog,
                        pstop);
-  if (nprog && ctx->debug_part) {  // diagnostics: speculative passes per 128-edge window (syncs)
+  const int kr = [] {  // slot-region kernel: SG_EXEC_REGION = rows per window (0: the speculative kernel;
+    const char* e = getenv("SG_EXEC_REGION");  // read at each call: tests switch it)
+    return e ? atoi(e) : 0;
+  }();
+  if (nprog && ctx->debug_part && kr == 4) {  // diagnostics: steps and cycles of the slot-region kernel (syncs)
+    unsigned long long* st = nullptr;
+    SG_HIP(hipMalloc(&st, 40));
+    SG_HIP(hipMemsetAsync(st, 0, 40, ctx->stream));
+    hipLaunchKernelGGL((k_exec_region<4>), dim3((uint32_t)nprog), dim3(64), 0, ctx->stream, d_pcs, d_call_off, d_prog_off,
+                       tmp, cnt, (const uint64_t*)pstop, d_rec_new, st);
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    SG_HIP(hipMemcpy(h, st, 40, hipMemcpyDeviceToHost));
+    SG_HIP(hipFree(st));
+    fprintf(stderr,
+            "sg exec region: programs %llu windows %llu steps %llu (%.2f per window, %.1f edges per step) "
+            "cycles per step %.0f, per window %.0f (steps %.0f)\n",
+            (unsigned long long)nprog, h[0], h[1], h[0] ? (double)h[1] / h[0] : 0.0, h[1] ? (double)h[4] / h[1] : 0.0,
+            h[1] ? (double)h[2] / h[1] : 0.0, h[0] ? (double)h[3] / h[0] : 0.0, h[0] ? (double)h[2] / h[0] : 0.0);
+  } else if (nprog && ctx->debug_part) {  // diagnostics: speculative passes per 128-edge window (syncs)
     unsigned long long* st = nullptr;
     SG_HIP(hipMalloc(&st, 32));
     SG_HIP(hipMemsetAsync(st, 0, 32, ctx->stream));
@@ -781,10 +818,6 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
       return e ? atoi(e) : 1;
     }();
     // slot-region kernel: SG_EXEC_REGION = rows per window (0: the speculative kernel)
-    const int kr = [] {  // (read at each call: tests switch it)
-      const char* e = getenv("SG_EXEC_REGION");
-      return e ? atoi(e) : 0;
-    }();
     const dim3 g((uint32_t)nprog), t(64);
     const uint64_t* ps = (const uint64_t*)pstop;
     if (kr == 1)
