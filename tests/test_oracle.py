@@ -164,6 +164,27 @@ def test_exec_signal_vs_compiled_reference():
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+def test_exec_signal_crafted_vs_compiled_reference():
+    """Signals crowded onto a few home slots (full probe windows, home-slot
+    overwrites) and the zero signal, whose overwrite empties slot 0: the
+    oracle against the reference's own dedup loop on the same traces."""
+    if O.ref_executor() is None:
+        pytest.skip("reference executor not built here (no reference checkout)")
+    from tests.test_gpu_parity import _trace_for_signals
+    rng = np.random.default_rng(117)
+    homes = np.array([(r * 128 + d) % 8192 for r in (0, 1, 63) for d in range(-4, 4)], np.uint64)
+    call_off = np.array([0, 700, 1900, 1900, 5000], np.uint64)
+    n = int(call_off[-1])
+    sigs = (rng.integers(0, 6, size=n).astype(np.uint64) * 8192 + 8192 * 977 + rng.choice(homes, size=n)) & 0xFFFFFFFF
+    sigs[rng.random(n) < 0.03] = 0
+    trace = _trace_for_signals(sigs.astype(np.uint32), call_off)
+    prog_off = np.array([0, 2, 4], np.uint64)
+    a = O.exec_signal(trace, call_off, prog_off)
+    b = O.ref_exec_signal(trace, call_off, prog_off)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert (a[0] == 0).any()  # a zero signal did overwrite
+
+
 def test_merge_poll_and_accept_vs_python():
     rng = np.random.default_rng(9)
     for _ in range(100):
