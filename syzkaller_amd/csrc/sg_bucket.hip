@@ -47,6 +47,9 @@
 
 namespace sg {
 
+#ifndef SG_HT_ABL
+#define SG_HT_ABL 0
+#endif
 #ifndef SG_PT
 #define SG_PT 16384
 #endif
@@ -519,16 +522,24 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
   for (int i = tid; i < kPT / 32; i += kPThreads) cs[i] = 0;
   for (int i = tid; i < (int)kTraceDedup; i += kPThreads) dd[i] = ~0ull;
   __syncthreads();
+#if SG_HT_ABL != 2  // (SG_HT_ABL: timing ablations, wrong results)
   trace_starts(rec_off, nrec, trec[t], s0, s1, cs, tid);
+#endif
   __syncthreads();
   uint32_t live = 0;
 #pragma unroll
   for (int k = 0; k < kS; k++) {
     const uint32_t p = k * kPThreads + tid, e = s0 + p;
+#if SG_HT_ABL == 3
+    x[k] = x[k] ^ ((cs[p >> 5] >> (p & 31)) & 1u) ^ xp[k];
+#else
     x[k] = trace_sig(x[k], trace_prev(x[k], xp[k]), (cs[p >> 5] >> (p & 31)) & 1u);
+#endif
     if (e < s1 && x[k] != 0) {
       live |= 1u << k;
+#if SG_HT_ABL != 1
       atomicMin(&dd[dedup_slot(x[k])], ((unsigned long long)p << 32) | x[k]);
+#endif
     }
   }
   __syncthreads();
@@ -538,7 +549,11 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
   for (int k = 0; k < kS; k++) {
     const uint32_t p = k * kPThreads + tid;
     if ((live >> k) & 1u) {
+#if SG_HT_ABL == 1
+      const unsigned long long v = ((unsigned long long)p << 32) | x[k];
+#else
       const unsigned long long v = dd[dedup_slot(x[k])];
+#endif
       if ((uint32_t)v != x[k] || (uint32_t)(v >> 32) == p) {
         kmask |= 1u << k;
         atomicAdd(&rc[p1_digit(x[k]) * 32 + cp], 1u);
