@@ -219,6 +219,7 @@ struct ChunkArgs {
   uint64_t* jstart;        // [nch + 2] scan of jparts
   uint64_t* qoff;          // [nch + 2] each chunk's first slot
   uint2* grouped;          // [ncov] (cov, query index) grouped by chunk
+  uint16_t* qchunk;        // [ncov] each query's chunk (written by the count kernel; null: recomputed)
   uint32_t* first_q;
   uint32_t* last_del;
 };
@@ -340,7 +341,11 @@ __global__ __launch_bounds__(kQT) void k_q_count(ChunkArgs a) {
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint64_t i = q0 + (uint64_t)k * kQT;
-    if (i < a.ncov) atomicAdd(&hist[chunk_of(a, L, query_pc(a.hi32, a.cov[i]))], 1u);
+    if (i < a.ncov) {
+      const uint32_t c = chunk_of(a, L, query_pc(a.hi32, a.cov[i]));
+      atomicAdd(&hist[c], 1u);
+      if (a.qchunk) a.qchunk[i] = (uint16_t)c;  // (kMaxChunks + 1 <= 2^16)
+    }
   }
   __syncthreads();
   const uint32_t col = tile_col(blockIdx.x, a.tw);
@@ -367,7 +372,7 @@ __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
   __shared__ uint2 stage[kStaged ? kT : 1];
   __shared__ uint16_t cid[kStaged ? kT : 1];
   __shared__ uint32_t wsum[kQT / 64 + 1];
-  load_chunks(a, L);
+  if (!a.qchunk) load_chunks(a, L);
   for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
   __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kT;
@@ -379,10 +384,12 @@ __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
     ch[k] = 0xFFFFFFFFu;
     if (i < a.ncov) {
       cv[k] = a.cov[i];
-      ch[k] = chunk_of(a, L, query_pc(a.hi32, cv[k]));
-      rk[k] = atomicAdd(&hist[ch[k]], 1u);
+      ch[k] = a.qchunk ? (uint32_t)a.qchunk[i] : chunk_of(a, L, query_pc(a.hi32, cv[k]));
     }
   }
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (ch[k] != 0xFFFFFFFFu) rk[k] = atomicAdd(&hist[ch[k]], 1u);
   __syncthreads();
   uint32_t* base = reinterpret_cast<uint32_t*>(L.bnd);  // (the bounds are no longer needed)
   if (!kStaged) {
@@ -800,6 +807,11 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
                o_si = p.add((uint64_t)nch * (kSiteIdx + 1) * 2), o_sy = p.add(chunked ? nall * 4 : 4),
                o_tc = p.add(ntc * 4), o_to = p.add((ntc + 1) * 8), o_jp = p.add(((uint64_t)nch + 1) * 4),
                o_js = p.add(((uint64_t)nch + 2) * 8), o_srt = p.add(4);
+  // the count kernel's per-query chunks, read back by the staged scatter
+  // (SG_REPORT_QCHUNK=0: the scatter searches each query's chunk again)
+  const char* qchunk_env = getenv("SG_REPORT_QCHUNK");
+  const bool qchunk = chunked && staged && !(qchunk_env && !atoi(qchunk_env));
+  const size_t o_qc = p.add(qchunk ? ncov * 2 : 2);
   size_t scan_off = p.total;
   rc = ws_reserve(ctx, p.total + std::max(scan_ws_bytes(nchunks), scan_ws_bytes(ntc)));
   if (rc) return rc;
@@ -872,6 +884,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     k.toff = (uint64_t*)ws_at(ctx, o_to);
     k.qoff = (uint64_t*)ws_at(ctx, o_qo);
     k.grouped = (uint2*)ws_at(ctx, o_gq);
+    k.qchunk = qchunk ? (uint16_t*)ws_at(ctx, o_qc) : nullptr;
     k.first_q = a.first_q;
     k.last_del = a.last_del;
     // queries in PC order (the reference's canonical covers) need no regrouping

@@ -810,8 +810,9 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
     spans more symbols than it holds in LDS (many site-less symbols: global
     symbol search), queries below the first and above the last call site,
     site counts at and around the 4096-site chunk size; the same queries in
-    PC order (no regrouping), with one store per query (SG_REPORT_STAGED=0)
-    and through the direct per-query passes (SG_REPORT_DIRECT=1)."""
+    PC order (no regrouping), with one store per query (SG_REPORT_STAGED=0),
+    with the scatter searching the chunks again (SG_REPORT_QCHUNK=0) and
+    through the direct per-query passes (SG_REPORT_DIRECT=1)."""
     rng = np.random.default_rng(143)
     hi32 = np.uint64(0xffffffff) << np.uint64(32)
     base = np.uint64(0xffffffff81000000)
@@ -839,6 +840,10 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
         monkeypatch.setenv("SG_REPORT_STAGED", "0")  # one store per query
         got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
         monkeypatch.delenv("SG_REPORT_STAGED")
+        assert np.array_equal(got, exp), sites.size
+        monkeypatch.setenv("SG_REPORT_QCHUNK", "0")  # the scatter searching each query's chunk again
+        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
+        monkeypatch.delenv("SG_REPORT_QCHUNK")
         assert np.array_equal(got, exp), sites.size
         monkeypatch.setenv("SG_REPORT_DIRECT", "1")
         got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
