@@ -613,6 +613,229 @@ __global__ __launch_bounds__(64) void k_exec_region(const uint32_t* __restrict__
   }
 }
 
+// Slot regions with a producer wave (r04): k_exec_region's decisions, with
+// everything but the steps moved to a second wave of the workgroup.  Wave 0
+// only walks the region lists of window i; wave 1 meanwhile compacts window
+// i - 1's kept signals into the output and builds window i + 1 (PC loads a
+// window ahead, hashes, the region masks and the region-major list) into the
+// other of two buffers.  One barrier per window (LDS only: the producer's PC
+// loads stay in flight across it).  39 KiB of LDS: four programs per CU, as
+// the one-wave kernels.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int K>
+__global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict__ pcs,
+                                                      const uint64_t* __restrict__ call_off,
+                                                      const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
+                                                      uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
+                                                      const uint8_t* __restrict__ emit) {
+  constexpr int W = 64 * K;
+  __shared__ uint32_t table[kDedupSize + 8];        // + mirror of slots 0..2, dummy slot 8196
+  __shared__ unsigned long long wlist[2][W];        // position << 32 | signal, region-major
+  __shared__ uint32_t wbc[2][64];                   // region lane: base << 16 | count
+  __shared__ uint32_t wlive[2];                     // buffer holds a window to decide
+  __shared__ unsigned long long wmask[K][64];       // producer scratch
+  __shared__ uint8_t wres[2][W + 4];                // decision of position 64 k + l at l K + k; W: dummy
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool prod = tid >= 64;
+  const uint64_t p = blockIdx.x;
+  const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
+  if (c1 <= c0) return;
+  for (uint32_t i = tid; i < kDedupSize + 8; i += 128) table[i] = 0;
+  if (prod) {
+#pragma unroll
+    for (int k = 0; k < K; k++) wmask[k][lane] = 0;
+  }
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // producer state: the window to build (call bc, start bj), the carried hash
+  uint64_t bc = c0, bj = call_off[c0];
+  uint32_t carry = 0;
+  const uint64_t pend = call_off[c1];
+  uint32_t npc[K];  // the PCs of the window to build
+  // pending windows: d = being decided, q = decided, to compact
+  uint32_t sd[K], sq[K];
+  int nd = 0, nq = 0;                 // valid positions (0: no window)
+  uint64_t cd = 0, cq = 0;            // their calls
+  bool ld = false, lq = false;        // last window of its call
+  bool fd = false, fq = false;        // first window of its call
+  uint64_t outpos = 0;
+  if (prod) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t q = bj + 64 * k + lane;
+      npc[k] = q < pend ? pcs[q] : 0u;
+    }
+  }
+  // the producer: build the next window into buffer nb (kNoPos-free: wlive[nb] = 0 when none)
+  auto build = [&](uint32_t nb, uint32_t (&sb)[K], int& nv, uint64_t& cb, bool& lb, bool& fb) {
+    // skip empty calls (their count is 0), find the window
+    while (bc < c1 && bj >= call_off[bc + 1]) {
+      if (lane == 0 && bj == call_off[bc]) cnt[bc] = 0;  // an empty call
+      bc++;
+      carry = 0;
+    }
+    if (bc >= c1) {
+      nv = 0;
+      if (lane == 0) wlive[nb] = 0;
+      return;
+    }
+    const uint64_t b = call_off[bc], e = call_off[bc + 1];
+    fb = bj == b;
+    if (fb) carry = 0;  // prev = 0 at call start (executor.h:389)
+    nv = (int)((e - bj) < (uint64_t)W ? (e - bj) : (uint64_t)W);
+    cb = bc;
+    lb = bj + (uint64_t)nv >= e;
+    uint32_t pc[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) pc[k] = 64 * k + lane < nv ? npc[k] : 0u;
+    const uint64_t nj = bj + (uint64_t)nv;  // the next window's first position (this call's next, or the next call's)
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t q = nj + 64 * k + lane;
+      const uint32_t l = pcs[q < pend ? q : pend - 1];
+      npc[k] = q < pend ? l : 0u;
+    }
+    uint32_t h[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) h[k] = exec_hash(pc[k]);
+    uint32_t in = carry;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t hp = (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)h[k], 0x138 /* wave_shr:1 */, 0xF, 0xF,
+                                                                false);
+      sb[k] = pc[k] ^ hp;  // executor.h:393-395
+      in = __builtin_amdgcn_readlane(h[k], 63);
+    }
+    {
+      const int lastk = (nv - 1) >> 6, lastl = (nv - 1) & 63;
+      uint32_t cv = 0;
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        if (k == lastk) cv = __builtin_amdgcn_readlane(h[k], lastl);
+      carry = cv;
+    }
+    bj = nj;
+    uint32_t rg[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      rg[k] = (sb[k] >> 7) & 63u;
+      if (64 * k + lane < nv)
+        __hip_atomic_fetch_or(&wmask[k][rg[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint64_t em_[K], om[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      em_[k] = __hip_atomic_load(&wmask[k][rg[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      om[k] = __hip_atomic_load(&wmask[k][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      __hip_atomic_store(&wmask[k][lane], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t n_r = 0, rowb[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      rowb[k] = n_r;
+      n_r += (uint32_t)__popcll(om[k]);
+    }
+    const uint32_t base = sgd::wave_incl_add(n_r) - n_r;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t at = (uint32_t)__shfl((int)(base + rowb[k]), (int)rg[k]);
+      if (64 * k + lane < nv)
+        wlist[nb][at + (uint32_t)__popcll(em_[k] & lt)] = ((unsigned long long)(64u * k + lane) << 32) | sb[k];
+    }
+    wbc[nb][lane] = (base << 16) | n_r;
+    if (lane == 0) wlive[nb] = 1;
+  };
+  // the producer: the decided window's kept signals into the output
+  auto compact = [&](uint32_t qb) {
+    if (fq) outpos = call_off[cq];
+    uint64_t keep[K];
+    {
+      uint8_t rb[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) rb[k] = wres[qb][lane * K + k];
+#pragma unroll
+      for (int k = 0; k < K; k++) keep[k] = __ballot(64 * k + lane < nq && rb[k] != 0);
+    }
+    const bool em = !emit || emit[cq] != 0;
+    if (em) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if ((keep[k] >> lane) & 1ull) tmp[outpos + __popcll(keep[k] & lt)] = sq[k];
+        outpos += __popcll(keep[k]);
+      }
+    }
+    if (lq && lane == 0) cnt[cq] = (uint32_t)(outpos - call_off[cq]);
+  };
+  if (prod) build(0, sd, nd, cd, ld, fd);
+  lds_sync();
+  for (uint32_t it = 0;; it++) {
+    const uint32_t buf = it & 1;
+    const bool live = __hip_atomic_load(&wlive[buf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+    if (!prod) {
+      if (live) {
+        const uint32_t bcw = wbc[buf][lane];
+        const uint32_t base = bcw >> 16, iend = base + (bcw & 0xFFFFu);
+        uint32_t i = base;
+        unsigned long long cur = wlist[buf][i < iend ? i : 0];
+        uint32_t pos = i < iend ? (uint32_t)(cur >> 32) : kNoPos;
+        uint32_t s = (uint32_t)cur;
+        while (__ballot(pos != kNoPos)) {
+          const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
+          const uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
+          const uint32_t hr = s & 127u;
+          const bool go = (pos != kNoPos) & ((hr > 2u) | (left > pos)) & ((hr < 125u) | (right > pos));
+          const uint32_t i2 = i + (go ? 1u : 0u);
+          const uint32_t home = s & (kDedupSize - 1);
+          const uint32_t t0 = table[home], t1 = table[home + 1], t2 = table[home + 2], t3 = table[home + 3];
+          const unsigned long long nx = wlist[buf][i2 < iend ? i2 : 0];
+          const bool h0 = (t0 == s) | (t0 == 0u), h1 = (t1 == s) | (t1 == 0u), h2 = (t2 == s) | (t2 == 0u);
+          const bool h3 = (t3 == s) | (t3 == 0u);
+          const uint32_t q = h0 ? 0u : h1 ? 1u : h2 ? 2u : h3 ? 3u : 0u;
+          const uint32_t tq = h0 ? t0 : h1 ? t1 : h2 ? t2 : t3;
+          const bool dup = (tq == s) & (h0 | h1 | h2 | h3);
+          const bool wr = go & !dup;
+          const uint32_t dd = (home + q) & (kDedupSize - 1);
+          table[wr ? dd : kDedupSize + 4] = s;
+          table[wr && dd < 3u ? dd + kDedupSize : kDedupSize + 4] = s;
+          wres[buf][go ? (pos & 63u) * K + (pos >> 6) : (uint32_t)W] = dup ? 0 : 1;
+          i = i2;
+          pos = i < iend ? (uint32_t)(nx >> 32) : kNoPos;
+          s = (uint32_t)nx;
+        }
+      }
+    } else {
+      if (nq) compact(buf ^ 1);  // the window decided in the last iteration
+      uint32_t sb[K];
+      int nb_ = 0;
+      uint64_t cb = 0;
+      bool lb = false, fb = false;
+      if (live) build(buf ^ 1, sb, nb_, cb, lb, fb);
+      // shift: decided -> to compact, being decided -> decided next, built -> being decided
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        sq[k] = sd[k];
+        sd[k] = sb[k];
+      }
+      nq = live ? nd : 0;
+      cq = cd;
+      lq = ld;
+      fq = fd;
+      nd = nb_;
+      cd = cb;
+      ld = lb;
+      fd = fb;
+    }
+    lds_sync();
+    if (!live) break;
+  }
+  // (the last decided window: compacted in the iteration that found no window to decide)
+}
+
 // the calls each program has to run for its queued calls' lists: up to and
 // including its last queued call (fuzzer.go:678-683 copies the signal of
 // queued records only); pstop[p] = prog_off[p] when it has none
@@ -779,9 +1002,13 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   if (pstop && nprog)
     hipLaunchKernelGGL(k_prog_stop, dim3(div_up(nprog, 256)), dim3(256), 0, ctx->stream, d_prog_off, d_rec_new, nprog,
                        pstop);
-  const int kr = [] {  // slot-region kernel: SG_EXEC_REGION = rows per window (0: the speculative kernel;
-    const char* e = getenv("SG_EXEC_REGION");  // read at each call: tests switch it)
-    return e ? atoi(e) : 0;
+  // SG_EXEC_REGION (read at each call: tests switch it): 104 (default) the
+  // slot-region kernel with a producer wave, 256-edge windows; 102 the same at
+  // 128; 1 / 2 / 4 / 8 / 16 the one-wave slot-region kernel at 64 K-edge
+  // windows; 0 the speculative kernel (SG_EXEC_K picks its window)
+  const int kr = [] {
+    const char* e = getenv("SG_EXEC_REGION");
+    return e ? atoi(e) : 104;
   }();
   if (nprog && ctx->debug_part && kr == 4) {  // diagnostics: steps and cycles of the slot-region kernel (syncs)
     unsigned long long* st = nullptr;
@@ -830,6 +1057,12 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
       hipLaunchKernelGGL((k_exec_region<8>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
     else if (kr == 16)
       hipLaunchKernelGGL((k_exec_region<16>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kr == 102)  // (102 / 104: the producer-wave kernel, 2 / 4 rows per window)
+      hipLaunchKernelGGL((k_exec_region2<2>), g, dim3(128), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kr == 104)
+      hipLaunchKernelGGL((k_exec_region2<4>), g, dim3(128), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
                          d_rec_new);
     else if (kx == 2)
       hipLaunchKernelGGL((k_exec_signal_k<2>), g, t, 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps, d_rec_new);
