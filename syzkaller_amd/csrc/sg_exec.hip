@@ -648,17 +648,26 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
   }
   __syncthreads();
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // producer state: the window to build (call bc, start bj), the carried hash
+  // producer state: the window to build (call bc, start bj), the carried hash;
+  // the call's bounds and emit flag, and the next call's, loaded a call ahead
+  // (a global load waited for inside the loop would also wait for the PC
+  // loads in flight)
   uint64_t bc = c0, bj = call_off[c0];
+  // (loads a call ahead are unconditional and clamped, and tested only when
+  // used: a select on a value just loaded would wait for it there)
+  uint64_t cb_b = bj, cb_e = call_off[c0 + 1], nx_e = call_off[c0 + 2 < c1 ? c0 + 2 : c1];
+  bool cb_em = !emit || emit[c0] != 0;
+  uint32_t nx_em = 1;
+  if (emit) nx_em = emit[c0 + 1 < c1 ? c0 + 1 : c1 - 1];
   uint32_t carry = 0;
   const uint64_t pend = call_off[c1];
   uint32_t npc[K];  // the PCs of the window to build
-  // pending windows: d = being decided, q = decided, to compact
+  // pending windows: d = being decided, q = decided, to compact; per window its
+  // call, the call's first position, emit flag, first / last window of the call
   uint32_t sd[K], sq[K];
   int nd = 0, nq = 0;                 // valid positions (0: no window)
-  uint64_t cd = 0, cq = 0;            // their calls
-  bool ld = false, lq = false;        // last window of its call
-  bool fd = false, fq = false;        // first window of its call
+  uint64_t cd = 0, cq = 0, bd = 0, bq = 0;
+  bool ld = false, lq = false, fd = false, fq = false, ed = false, eq = false;
   uint64_t outpos = 0;
   if (prod) {
 #pragma unroll
@@ -668,33 +677,39 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
     }
   }
   // the producer: build the next window into buffer nb (kNoPos-free: wlive[nb] = 0 when none)
-  auto build = [&](uint32_t nb, uint32_t (&sb)[K], int& nv, uint64_t& cb, bool& lb, bool& fb) {
-    // skip empty calls (their count is 0), find the window
-    while (bc < c1 && bj >= call_off[bc + 1]) {
-      if (lane == 0 && bj == call_off[bc]) cnt[bc] = 0;  // an empty call
+  auto build = [&](uint32_t nb, uint32_t (&sb)[K], int& nv, uint64_t& cb, uint64_t& bb, bool& lb, bool& fb,
+                   bool& eb) {
+    // past the call's end: the next call (an empty one's count stays 0, from the memset)
+    while (bc < c1 && bj >= cb_e) {
       bc++;
-      carry = 0;
+      if (bc >= c1) break;
+      cb_b = cb_e;
+      cb_e = nx_e;
+      cb_em = nx_em != 0;
+      nx_e = call_off[bc + 2 < c1 ? bc + 2 : c1];
+      if (emit) nx_em = emit[bc + 1 < c1 ? bc + 1 : c1 - 1];
     }
     if (bc >= c1) {
       nv = 0;
       if (lane == 0) wlive[nb] = 0;
       return;
     }
-    const uint64_t b = call_off[bc], e = call_off[bc + 1];
-    fb = bj == b;
+    const uint64_t e = cb_e;
+    fb = bj == cb_b;
     if (fb) carry = 0;  // prev = 0 at call start (executor.h:389)
     nv = (int)((e - bj) < (uint64_t)W ? (e - bj) : (uint64_t)W);
     cb = bc;
+    bb = cb_b;
+    eb = cb_em;
     lb = bj + (uint64_t)nv >= e;
     uint32_t pc[K];
 #pragma unroll
     for (int k = 0; k < K; k++) pc[k] = 64 * k + lane < nv ? npc[k] : 0u;
     const uint64_t nj = bj + (uint64_t)nv;  // the next window's first position (this call's next, or the next call's)
 #pragma unroll
-    for (int k = 0; k < K; k++) {
+    for (int k = 0; k < K; k++) {  // (past the program: a clamped load; the next build zeroes past its window)
       const uint64_t q = nj + 64 * k + lane;
-      const uint32_t l = pcs[q < pend ? q : pend - 1];
-      npc[k] = q < pend ? l : 0u;
+      npc[k] = pcs[q < pend ? q : pend - 1];
     }
     uint32_t h[K];
 #pragma unroll
@@ -752,7 +767,7 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
   };
   // the producer: the decided window's kept signals into the output
   auto compact = [&](uint32_t qb) {
-    if (fq) outpos = call_off[cq];
+    if (fq) outpos = bq;
     uint64_t keep[K];
     {
       uint8_t rb[K];
@@ -761,17 +776,16 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
 #pragma unroll
       for (int k = 0; k < K; k++) keep[k] = __ballot(64 * k + lane < nq && rb[k] != 0);
     }
-    const bool em = !emit || emit[cq] != 0;
-    if (em) {
+    if (eq) {
 #pragma unroll
       for (int k = 0; k < K; k++) {
         if ((keep[k] >> lane) & 1ull) tmp[outpos + __popcll(keep[k] & lt)] = sq[k];
         outpos += __popcll(keep[k]);
       }
     }
-    if (lq && lane == 0) cnt[cq] = (uint32_t)(outpos - call_off[cq]);
+    if (lq && lane == 0) cnt[cq] = (uint32_t)(outpos - bq);
   };
-  if (prod) build(0, sd, nd, cd, ld, fd);
+  if (prod) build(0, sd, nd, cd, bd, ld, fd, ed);
   lds_sync();
   for (uint32_t it = 0;; it++) {
     const uint32_t buf = it & 1;
@@ -812,9 +826,9 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
       if (nq) compact(buf ^ 1);  // the window decided in the last iteration
       uint32_t sb[K];
       int nb_ = 0;
-      uint64_t cb = 0;
-      bool lb = false, fb = false;
-      if (live) build(buf ^ 1, sb, nb_, cb, lb, fb);
+      uint64_t cb = 0, bb = 0;
+      bool lb = false, fb = false, eb = false;
+      if (live) build(buf ^ 1, sb, nb_, cb, bb, lb, fb, eb);
       // shift: decided -> to compact, being decided -> decided next, built -> being decided
 #pragma unroll
       for (int k = 0; k < K; k++) {
@@ -823,17 +837,304 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
       }
       nq = live ? nd : 0;
       cq = cd;
+      bq = bd;
       lq = ld;
       fq = fd;
+      eq = ed;
       nd = nb_;
       cd = cb;
+      bd = bb;
       ld = lb;
       fd = fb;
+      ed = eb;
     }
     lds_sync();
     if (!live) break;
   }
   // (the last decided window: compacted in the iteration that found no window to decide)
+}
+
+// Slot regions over D deciding waves (r04): k_exec_region2 with 64 D regions
+// of 128 / D slots, wave w's lane l deciding region 64 w + l.  More regions
+// split a window's edges finer (C2 traces, 256-edge windows: 10.0 steps per
+// window at 64 regions, 7.4 at 128, 5.9 at 256) and the waves step in
+// parallel.  A region edge between two waves (lane 63 of wave w and lane 0
+// of wave w + 1, cyclically) is checked through LDS: lanes 0 and 63 publish
+// their next undecided position every step and read the neighbouring wave's.
+// A value read late is smaller than the current one, so the check only
+// waits longer; the producer zeroes the window's published positions before
+// the window starts (nothing decided yet), and a wave publishes "none left"
+// when it is done.  LDS order makes the neighbour's table writes visible
+// before the position it publishes after them.  The producer places the
+// edges into the region-major list in two passes (counts, then row by row in
+// program order), with one row's masks at a time.
+template <int K, int D>
+__global__ __launch_bounds__(64 * (D + 1)) void k_exec_region3(const uint32_t* __restrict__ pcs,
+                                                               const uint64_t* __restrict__ call_off,
+                                                               const uint64_t* __restrict__ prog_off,
+                                                               uint32_t* __restrict__ tmp, uint32_t* __restrict__ cnt,
+                                                               const uint64_t* __restrict__ pstop,
+                                                               const uint8_t* __restrict__ emit) {
+  constexpr int W = 64 * K;
+  constexpr uint32_t R = 64 * D, S = kDedupSize / R;  // regions, slots per region
+  static_assert(W <= 256, "positions fit a byte");
+  __shared__ uint32_t table[kDedupSize + 4];  // + mirror of slots 0..2, dummy slot 8195
+  __shared__ uint32_t wsig[2][W];             // region-major
+  __shared__ uint8_t wpos[2][W];
+  __shared__ uint32_t wbc[2][R];              // region: base << 16 | count
+  __shared__ uint32_t pubp[2][2][D];          // [buf][lane 0 / lane 63][wave]: next undecided position
+  __shared__ uint32_t wlive[2];
+  __shared__ unsigned long long wmask[R];     // producer scratch: one row's masks
+  __shared__ uint32_t run[R];                 // producer scratch: counts, then running slots
+  __shared__ uint8_t wres[2][W + 1];          // decision of position 64 k + l at l K + k; W: dummy
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool prod = wv == D;
+  const uint64_t p = blockIdx.x;
+  const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
+  if (c1 <= c0) return;
+  for (uint32_t i = tid; i < kDedupSize + 4; i += 64 * (D + 1)) table[i] = 0;
+  if (prod) {
+    for (uint32_t r = lane; r < R; r += 64) {
+      wmask[r] = 0;
+      run[r] = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t bc = c0, bj = call_off[c0];
+  uint64_t cb_b = bj, cb_e = call_off[c0 + 1], nx_e = call_off[c0 + 2 < c1 ? c0 + 2 : c1];
+  bool cb_em = !emit || emit[c0] != 0;
+  uint32_t nx_em = 1;
+  if (emit) nx_em = emit[c0 + 1 < c1 ? c0 + 1 : c1 - 1];
+  uint32_t carry = 0;
+  const uint64_t pend = call_off[c1];
+  uint32_t npc[K];
+  uint32_t sd[K], sq[K];
+  int nd = 0, nq = 0;
+  uint64_t cd = 0, cq = 0, bd = 0, bq = 0;
+  bool ld = false, lq = false, fd = false, fq = false, ed = false, eq = false;
+  uint64_t outpos = 0;
+  if (prod) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t q = bj + 64 * k + lane;
+      npc[k] = pcs[q < pend ? q : pend - 1];
+    }
+  }
+  auto build = [&](uint32_t nb, uint32_t (&sb)[K], int& nv, uint64_t& cb, uint64_t& bb, bool& lb, bool& fb,
+                   bool& eb) {
+    while (bc < c1 && bj >= cb_e) {
+      bc++;
+      if (bc >= c1) break;
+      cb_b = cb_e;
+      cb_e = nx_e;
+      cb_em = nx_em != 0;
+      nx_e = call_off[bc + 2 < c1 ? bc + 2 : c1];
+      if (emit) nx_em = emit[bc + 1 < c1 ? bc + 1 : c1 - 1];
+    }
+    if (bc >= c1) {
+      nv = 0;
+      if (lane == 0) wlive[nb] = 0;
+      return;
+    }
+    const uint64_t e = cb_e;
+    fb = bj == cb_b;
+    if (fb) carry = 0;  // prev = 0 at call start (executor.h:389)
+    nv = (int)((e - bj) < (uint64_t)W ? (e - bj) : (uint64_t)W);
+    cb = bc;
+    bb = cb_b;
+    eb = cb_em;
+    lb = bj + (uint64_t)nv >= e;
+    uint32_t pc[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) pc[k] = 64 * k + lane < nv ? npc[k] : 0u;
+    const uint64_t nj = bj + (uint64_t)nv;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t q = nj + 64 * k + lane;
+      npc[k] = pcs[q < pend ? q : pend - 1];
+    }
+    uint32_t h[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) h[k] = exec_hash(pc[k]);
+    uint32_t in = carry;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t hp = (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)h[k], 0x138 /* wave_shr:1 */, 0xF, 0xF,
+                                                                false);
+      sb[k] = pc[k] ^ hp;  // executor.h:393-395
+      in = __builtin_amdgcn_readlane(h[k], 63);
+    }
+    {
+      const int lastk = (nv - 1) >> 6, lastl = (nv - 1) & 63;
+      uint32_t cv = 0;
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        if (k == lastk) cv = __builtin_amdgcn_readlane(h[k], lastl);
+      carry = cv;
+    }
+    bj = nj;
+    uint32_t rg[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      rg[k] = ((sb[k] & (kDedupSize - 1)) * R) >> 13;
+      if (64 * k + lane < nv) __hip_atomic_fetch_add(&run[rg[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // each region's base (regions d 64 + lane of this lane: a wave scan of their sum)
+    uint32_t cr[D], tot = 0;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      cr[d] = __hip_atomic_load(&run[d * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      tot += cr[d];
+    }
+    uint32_t at = sgd::wave_incl_add(tot) - tot;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      wbc[nb][d * 64 + lane] = (at << 16) | cr[d];
+      __hip_atomic_store(&run[d * 64 + lane], at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      at += cr[d];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // row by row in program order: the row's masks give each edge its rank in its region
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const bool ok = 64 * k + lane < nv;
+      if (ok) __hip_atomic_fetch_or(&wmask[rg[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t m = __hip_atomic_load(&wmask[rg[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t r0 = __hip_atomic_load(&run[rg[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint64_t om[D];
+      uint32_t orun[D];
+#pragma unroll
+      for (int d = 0; d < D; d++) {
+        om[d] = __hip_atomic_load(&wmask[d * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        orun[d] = __hip_atomic_load(&run[d * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (ok) {
+        const uint32_t slot = r0 + (uint32_t)__popcll(m & lt);
+        wsig[nb][slot] = sb[k];
+        wpos[nb][slot] = (uint8_t)(64 * k + lane);
+      }
+#pragma unroll
+      for (int d = 0; d < D; d++) {
+        __hip_atomic_store(&run[d * 64 + lane], orun[d] + (uint32_t)__popcll(om[d]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&wmask[d * 64 + lane], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int d = 0; d < D; d++)
+      __hip_atomic_store(&run[d * 64 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane < 2 * D) pubp[nb][lane / D][lane % D] = 0;  // nothing decided yet
+    if (lane == 0) wlive[nb] = 1;
+  };
+  auto compact = [&](uint32_t qb) {
+    if (fq) outpos = bq;
+    uint64_t keep[K];
+    {
+      uint8_t rb[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) rb[k] = wres[qb][lane * K + k];
+#pragma unroll
+      for (int k = 0; k < K; k++) keep[k] = __ballot(64 * k + lane < nq && rb[k] != 0);
+    }
+    if (eq) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if ((keep[k] >> lane) & 1ull) tmp[outpos + __popcll(keep[k] & lt)] = sq[k];
+        outpos += __popcll(keep[k]);
+      }
+    }
+    if (lq && lane == 0) cnt[cq] = (uint32_t)(outpos - bq);
+  };
+  if (prod) build(0, sd, nd, cd, bd, ld, fd, ed);
+  lds_sync();
+  for (uint32_t it = 0;; it++) {
+    const uint32_t buf = it & 1;
+    const bool live = __hip_atomic_load(&wlive[buf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+    if (!prod) {
+      if (live) {
+        const uint32_t r = (uint32_t)wv * 64 + lane;
+        const uint32_t bcw = wbc[buf][r];
+        const uint32_t base = bcw >> 16, iend = base + (bcw & 0xFFFFu);
+        uint32_t i = base;
+        uint32_t pos = i < iend ? (uint32_t)wpos[buf][i] : kNoPos;
+        uint32_t s = wsig[buf][i < iend ? i : 0];
+        // lanes 0 / 63: their slot in pubp, and the neighbouring wave's to read
+        const uint32_t wl = (uint32_t)(wv + D - 1) % D, wr = (uint32_t)(wv + 1) % D;
+        uint32_t* pub_mine = lane == 0 ? &pubp[buf][0][wv] : lane == 63 ? &pubp[buf][1][wv] : nullptr;
+        const uint32_t* pub_nb = lane == 0 ? &pubp[buf][1][wl] : lane == 63 ? &pubp[buf][0][wr] : nullptr;
+        while (__ballot(pos != kNoPos)) {
+          uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
+          uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
+          if (D > 1) {
+            // (compiler barriers: the last step's table writes stay before the
+            // published position, the neighbour's position is read before this
+            // step's table reads; the LDS keeps one wave's operations in order)
+            asm volatile("" ::: "memory");
+            if (pub_mine) __hip_atomic_store(pub_mine, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (pub_nb) {
+              const uint32_t x = __hip_atomic_load(pub_nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (lane == 0) left = x;
+              else right = x;
+            }
+            asm volatile("" ::: "memory");
+          }
+          const uint32_t hr = s & (S - 1);
+          const bool go = (pos != kNoPos) & ((hr > 2u) | (left > pos)) & ((hr < S - 3) | (right > pos));
+          const uint32_t i2 = i + (go ? 1u : 0u);
+          const uint32_t home = s & (kDedupSize - 1);
+          const uint32_t t0 = table[home], t1 = table[home + 1], t2 = table[home + 2], t3 = table[home + 3];
+          const uint32_t ni = i2 < iend ? i2 : 0;
+          const uint32_t nsg = wsig[buf][ni];
+          const uint32_t npo = wpos[buf][ni];
+          const bool h0 = (t0 == s) | (t0 == 0u), h1 = (t1 == s) | (t1 == 0u), h2 = (t2 == s) | (t2 == 0u);
+          const bool h3 = (t3 == s) | (t3 == 0u);
+          const uint32_t q = h0 ? 0u : h1 ? 1u : h2 ? 2u : h3 ? 3u : 0u;
+          const uint32_t tq = h0 ? t0 : h1 ? t1 : h2 ? t2 : t3;
+          const bool dup = (tq == s) & (h0 | h1 | h2 | h3);
+          const bool wr_ = go & !dup;
+          const uint32_t dd = (home + q) & (kDedupSize - 1);
+          table[wr_ ? dd : kDedupSize + 3] = s;
+          table[wr_ && dd < 3u ? dd + kDedupSize : kDedupSize + 3] = s;
+          wres[buf][go ? (pos & 63u) * K + (pos >> 6) : (uint32_t)W] = dup ? 0 : 1;
+          i = i2;
+          pos = i < iend ? npo : kNoPos;
+          s = nsg;
+        }
+        if (D > 1 && pub_mine) __hip_atomic_store(pub_mine, kNoPos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else {
+      if (nq) compact(buf ^ 1);
+      uint32_t sb[K];
+      int nb_ = 0;
+      uint64_t cb = 0, bb = 0;
+      bool lb = false, fb = false, eb = false;
+      if (live) build(buf ^ 1, sb, nb_, cb, bb, lb, fb, eb);
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        sq[k] = sd[k];
+        sd[k] = sb[k];
+      }
+      nq = live ? nd : 0;
+      cq = cd;
+      bq = bd;
+      lq = ld;
+      fq = fd;
+      eq = ed;
+      nd = nb_;
+      cd = cb;
+      bd = bb;
+      ld = lb;
+      fd = fb;
+      ed = eb;
+    }
+    lds_sync();
+    if (!live) break;
+  }
 }
 
 // the calls each program has to run for its queued calls' lists: up to and
@@ -1060,6 +1361,15 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
                          d_rec_new);
     else if (kr == 102)  // (102 / 104: the producer-wave kernel, 2 / 4 rows per window)
       hipLaunchKernelGGL((k_exec_region2<2>), g, dim3(128), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kr == 142)  // (1KD: the D-wave kernel, K rows per window)
+      hipLaunchKernelGGL((k_exec_region3<4, 2>), g, dim3(192), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kr == 141)
+      hipLaunchKernelGGL((k_exec_region3<4, 1>), g, dim3(128), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
+                         d_rec_new);
+    else if (kr == 144)
+      hipLaunchKernelGGL((k_exec_region3<4, 4>), g, dim3(320), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,
                          d_rec_new);
     else if (kr == 104)
       hipLaunchKernelGGL((k_exec_region2<4>), g, dim3(128), 0, ctx->stream, d_pcs, d_call_off, d_prog_off, tmp, cnt, ps,

@@ -626,7 +626,7 @@ def _trace_for_signals(sigs, call_off):
     return pcs
 
 
-@pytest.mark.parametrize("rows", ["0", "1", "2", "4", "8", "16", "102", "104"])  # 0: the speculative kernel; 10x: producer wave
+@pytest.mark.parametrize("rows", ["0", "1", "2", "4", "8", "16", "102", "104", "141", "142", "144"])  # 0: speculative; 10K: producer wave; 14D: D deciding waves
 def test_exec_signal_region_boundaries_vs_oracle(C, monkeypatch, rows):
     """Signals crowded onto the slots where the slot-region kernel's lanes meet
     (home % 128 in 124..127 and 0..3, table wrap-around 8189..8191 -> 0..2), a
