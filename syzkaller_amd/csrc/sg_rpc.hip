@@ -321,37 +321,60 @@ __global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t*
 }
 
 // Pass 2 (one wave per list, four per workgroup): the list's bytes in steps
-// of 64 x 16 (16 consecutive bytes per lane plus the 5 before, for runs that
-// open earlier); each terminator decodes its run backwards (LEB128: the
-// earlier byte holds the lower bits), the lanes' value counts and 64-bit delta
-// sums are scanned across the wave, and each value is written as the
-// running sum at the list's value offset (pass 1).  One read of the payload,
-// one write of the values, no per-value arrays.  Checks (binary.Uvarint, then
-// the running sum): a run of <= 5 bytes fitting 32 bits, the list ending on a
-// terminator, every sum within 32 bits.
+// of 64 x 16, each lane an aligned 16-B load (steps start at the list's first
+// byte rounded down to 16; bytes before the list stop a run's walk back,
+// bytes after it are never terminators), the 5 bytes before a lane's 16 from
+// the lane before (DPP) or the step before (lane 63, carried).  Each
+// terminator decodes its run backwards (LEB128: the earlier byte holds the
+// lower bits), the lanes' value counts and 64-bit delta sums are scanned
+// across the wave, each value goes to LDS at its place in the step as the
+// running sum, and the step's values leave as consecutive dwords at the
+// list's value offset (pass 1).  Checks (binary.Uvarint, then the running
+// sum): a run of <= 5 bytes fitting 32 bits, the list ending on a terminator,
+// every sum within 32 bits.  The input buffer is padded to 16 bytes.
 constexpr int kDecB = 16, kDecPre = 5;
 __global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                   const uint64_t* __restrict__ voff, uint64_t n,
+                                                   const uint64_t* __restrict__ voff, uint64_t n, uint64_t cap,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
-  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint32_t stage[4][64 * kDecB];  // a step's values (at most one per byte)
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + w;
   if (k >= n) return;  // (a wave leaves whole)
+  if (voff[n] > cap) {  // the values would not fit: the host reports it, nothing is written
+    if (k == 0 && (threadIdx.x & 63) == 0) atomicOr(err, 2u);
+    return;
+  }
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t b0 = in_off[k], b1 = in_off[k + 1];
   uint64_t vi = voff[k], run = 0;
   bool bad = false;
-  for (uint64_t cb = b0; cb < b1; cb += 64 * kDecB) {
+  uint32_t cz = 0, cw = 0;  // the step before's lane 63: dwords 2 and 3 of its 16 bytes
+  uint32_t* st = stage[w];
+  for (uint64_t cb = b0 & ~15ull; cb < b1; cb += 64 * kDecB) {
     const uint64_t base = cb + (uint64_t)lane * kDecB;
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (base < b1) q = *reinterpret_cast<const uint4*>(in + base);
+    const uint32_t pz = (uint32_t)__builtin_amdgcn_update_dpp((int)cz, (int)q.z, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+    const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp((int)cw, (int)q.w, 0x138, 0xF, 0xF, false);
+    cz = __builtin_amdgcn_readlane(q.z, 63);
+    cw = __builtin_amdgcn_readlane(q.w, 63);
     uint32_t c[kDecPre + kDecB];
+    c[0] = pz >> 24;  // byte base - 5
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[1 + j] = (pw >> (8 * j)) & 0xFFu;
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < kDecB; j++) c[kDecPre + j] = (qw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
 #pragma unroll
     for (int j = 0; j < kDecPre + kDecB; j++) {
-      const uint64_t p = base + j - kDecPre;  // (wraps below 0 only where base < kDecPre, then p >= b1 or < b0)
+      const uint64_t pj = base + j;  // position + kDecPre
       // before the list: a stop for the walk back; past it: never a terminator
-      c[j] = (base + j >= b0 + kDecPre && p < b1) ? (uint32_t)in[p] : (p >= b1 && base + j >= b0 + kDecPre ? 0x80u : 0u);
+      c[j] = pj < b0 + kDecPre ? 0u : (pj >= b1 + kDecPre ? 0x80u : c[j]);
     }
-    uint32_t tmask = 0;
+    uint32_t tmask = 0;  // terminators inside the list (past it: 0x80 above; before it: excluded here)
 #pragma unroll
     for (int i = 0; i < kDecB; i++)
-      if (base + i < b1 && !(c[kDecPre + i] & 0x80u)) tmask |= 1u << i;
+      if (base + i >= b0 && !(c[kDecPre + i] & 0x80u)) tmask |= 1u << i;
     uint32_t d[kDecB];
     uint64_t t = 0;
 #pragma unroll
@@ -362,10 +385,10 @@ __global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ i
         uint64_t v = c[j] & 0x7Fu;
         bool open = true;
 #pragma unroll
-        for (int q = 1; q <= kDecPre; q++) {
-          const uint32_t cc = c[j - q];
+        for (int qq = 1; qq <= kDecPre; qq++) {
+          const uint32_t cc = c[j - qq];
           if (open && (cc & 0x80u)) {
-            if (q == kDecPre) bad = true;  // a sixth byte: more than binary.Uvarint's 32-bit range here
+            if (qq == kDecPre) bad = true;  // a sixth byte: more than binary.Uvarint's 32-bit range here
             v = (v << 7) | (cc & 0x7Fu);
           } else {
             open = false;
@@ -384,16 +407,20 @@ __global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ i
       if (lane >= (uint32_t)o) sc += y;
     }
     uint64_t acc = run + (sc - t);
-    uint64_t idx = vi + ex;
+    uint32_t idx = ex;
 #pragma unroll
     for (int i = 0; i < kDecB; i++)
       if ((tmask >> i) & 1u) {
         acc += d[i];
         bad |= acc > 0xFFFFFFFFull;
-        out[idx++] = (uint32_t)acc;
+        st[idx++] = (uint32_t)acc;
       }
+    const uint32_t tot = __builtin_amdgcn_readlane(ex + cnt, 63);
+    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
+    for (uint32_t e = lane; e < tot; e += 64) out[vi + e] = st[e];
+    __builtin_amdgcn_wave_barrier();
     run += __shfl(sc, 63);
-    vi += __builtin_amdgcn_readlane(ex + cnt, 63);
+    vi += tot;
   }
   if (lane == 0 && b1 > b0 && (in[b1 - 1] & 0x80u)) bad = true;  // the list ends inside a value
   if (__any(bad) && lane == 0) atomicOr(err, 1u);
@@ -412,14 +439,23 @@ __global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __res
   }
 }
 
-static bool enc_elems() {  // read at each call (tests switch it)
+// One wave per list walks each list in order: right for many lists of
+// moderate length (per-call signal), wrong for a few long ones (a set's
+// members as one payload: one wave would walk all of it).  The per-element /
+// per-block forms spread any list over the whole chip; they take batches of
+// fewer than 256 lists or more than 64 Ki values (bytes) per list on average.
+constexpr uint64_t kWaveListsMin = 256, kWaveListAvg = 65536;
+
+static bool enc_elems(uint64_t n, uint64_t N) {  // read at each call (tests switch it)
   const char* e = getenv("SG_RPC_ENCODE_ELEMS");
-  return e && atoi(e) != 0;
+  if (e) return atoi(e) != 0;
+  return n < kWaveListsMin || N / n > kWaveListAvg;
 }
 
-static bool dec_blocks() {  // read at each call (tests switch it)
+static bool dec_blocks(uint64_t n, uint64_t nb) {  // read at each call (tests switch it)
   const char* e = getenv("SG_RPC_DECODE_BLOCKS");
-  return e && atoi(e) != 0;
+  if (e) return atoi(e) != 0;
+  return n < kWaveListsMin || nb / n > kWaveListAvg;
 }
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::min<uint64_t>(div_up(n ? n : 1, 256), 16384); }
@@ -451,7 +487,7 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
   uint64_t* kw = (uint64_t*)ws_at(ctx, o_kw);
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   // (a list's byte count is a u32: the per-list form when 5 N cannot overflow it)
-  if (!enc_elems() && N * 5 < (1ull << 32)) {
+  if (!enc_elems(n, N) && N * 5 < (1ull << 32)) {
     ScopedTimer tm(ctx, "rpc_encode");
     uint32_t* lbytes = (uint32_t*)ws_at(ctx, o_lb);
     hipLaunchKernelGGL(k_enc_list_len, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_v, d_off, n, lbytes,
@@ -515,16 +551,19 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   hipLaunchKernelGGL(k_list_vpos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vbase, tmask,
                      d_voff);
   SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  const uint64_t N = h_off[n];
-  if (N > cap) {
-    set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
-    return SG_EINVAL;
-  }
-  if (nb && !dec_blocks()) {
+  const bool lists = nb && !dec_blocks(n, nb);
+  if (lists) {
+    // no host wait between the passes: the kernel checks the capacity itself
+    // (error bit 2: nothing written)
     hipLaunchKernelGGL(k_dec_lists, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_in, d_in_off,
-                       (const uint64_t*)d_voff, n, d_vals, err);
+                       (const uint64_t*)d_voff, n, cap, d_vals, err);
   } else {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    const uint64_t N = h_off[n];
+    if (N > cap) {
+      set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
+      return SG_EINVAL;
+    }
     // (SG_RPC_DECODE_BLOCKS=1: the per-block form -- runs per 32-byte block,
     // then a scan of the deltas)
     if (nb) {
@@ -545,6 +584,10 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   uint32_t herr = 0;
   SG_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (lists && h_off[n] > cap) {
+    set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)h_off[n], (unsigned long long)cap);
+    return SG_EINVAL;
+  }
   if (herr) {
     set_error("sg_delta_decode: malformed payload (unterminated value, value over 32 bits, or sum over 32 bits)");
     return SG_EINVAL;
