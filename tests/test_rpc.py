@@ -85,6 +85,39 @@ def test_delta_batch_vs_oracle(ctx, monkeypatch, blocks):
 
 
 @pytest.mark.gpu
+def test_delta_codec_list_edges(ctx, monkeypatch):
+    """The per-list codec at every 16-byte / 4-value alignment: lists of 0-9
+    and 255-257 values (steps of 256 values and 1 KiB, loads aligned down to
+    the list's first value / byte), values 0 and 0xFFFFFFFF, long zero runs
+    (1-byte varints) and maximal deltas (5-byte varints), 300 lists so the
+    default routing takes the per-list kernels."""
+    from syzkaller_amd import cover as C
+
+    monkeypatch.delenv("SG_RPC_DECODE_BLOCKS", raising=False)
+    monkeypatch.delenv("SG_RPC_ENCODE_ELEMS", raising=False)
+    rng = np.random.default_rng(48)
+    lists = []
+    for k in range(300):
+        m = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 255, 256, 257][k % 13]
+        kind = k % 3
+        if kind == 0:
+            v = np.zeros(m, np.uint32)
+        elif kind == 1:
+            v = np.sort(rng.integers(0, 1 << 32, size=m, dtype=np.uint64)).astype(np.uint32)
+            if m:
+                v[0], v[-1] = 0, 0xFFFFFFFF
+        else:
+            v = np.sort(rng.integers(0, 300, size=m)).astype(np.uint32)
+        lists.append(np.sort(v))
+    vals, off = C.to_csr(lists)
+    data, doff = C.delta_encode(vals, off, ctx=ctx)
+    exp = b"".join(O.delta_encode(v) for v in lists)
+    assert data.tobytes() == exp
+    gv, go = C.delta_decode(data, doff, ctx=ctx)
+    assert np.array_equal(go, off) and np.array_equal(gv, vals)
+
+
+@pytest.mark.gpu
 def test_set_payload_round_trip(ctx):
     from syzkaller_amd import cover as C
 
