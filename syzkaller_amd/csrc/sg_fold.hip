@@ -167,6 +167,68 @@ __global__ __launch_bounds__(kFuThreads) void k_fold_write(const uint64_t* __res
   }
 }
 
+// One group of canonical lists (no value repeats inside a list, jb = 0; the
+// corpus fold of html.go:306 is one) whose values span at most 2^28: the fold
+// is the set of values seen, ascending, the sentinel dropped (cover.go:63-70,
+// :97 with every count 1), i.e. a byte map over [AND, OR] of the values --
+// byte stores of 1 (no atomics; repeats across lists store the same byte),
+// then one ordered compaction of the map -- instead of sorting 64-bit keys.
+constexpr uint64_t kFoldMapMax = 1ull << 28;
+constexpr int kFmThreads = 256;
+constexpr uint32_t kFmTile = kFmThreads * 16;  // map bytes per compaction tile
+
+__global__ void k_fold_mark(const uint32_t* __restrict__ v, uint64_t n, uint32_t lo, uint8_t* __restrict__ map) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t x = v[i];
+    if (x != 0xFFFFFFFFu) map[x - lo] = 1;
+  }
+}
+
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w) {  // nonzero bytes of w (bytes are 0 or 1)
+  return (uint32_t)__popc(w & 0x01010101u);
+}
+
+__global__ __launch_bounds__(kFmThreads) void k_fold_map_count(const uint8_t* __restrict__ map, uint64_t range,
+                                                               uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t ws[kFmThreads / 64];
+  const uint64_t b = (uint64_t)blockIdx.x * kFmTile + threadIdx.x * 16u;
+  uint32_t c = 0;
+  if (b < range) {  // (the map is padded to whole tiles, zeroed)
+    const uint4 q = *reinterpret_cast<const uint4*>(map + b);
+    c = nz_bytes(q.x) + nz_bytes(q.y) + nz_bytes(q.z) + nz_bytes(q.w);
+  }
+  c = sgd::wave_incl_add(c);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < kFmThreads / 64; i++) t += ws[i];
+    tcnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kFmThreads) void k_fold_map_write(const uint8_t* __restrict__ map, uint64_t range,
+                                                               uint32_t lo, const uint64_t* __restrict__ tpos,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ uint32_t ws[kFmThreads / 64];
+  const uint64_t b = (uint64_t)blockIdx.x * kFmTile + threadIdx.x * 16u;
+  uint4 q = make_uint4(0, 0, 0, 0);
+  if (b < range) q = *reinterpret_cast<const uint4*>(map + b);
+  const uint32_t c = nz_bytes(q.x) + nz_bytes(q.y) + nz_bytes(q.z) + nz_bytes(q.w);
+  const uint32_t incl = sgd::wave_incl_add(c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int i = 0; i < w; i++) before += ws[i];
+  uint64_t at = tpos[blockIdx.x] + before + incl - c;
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int j = 0; j < 16; j++)
+    if ((qw[j >> 2] >> (8 * (j & 3))) & 0xFFu) out[at++] = lo + (uint32_t)(b + j);
+}
+
 constexpr int SG_EOVERFLOW_FOLD = 1;  // internal: the keys do not fit 64 bits
 
 static uint32_t bits_for(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
@@ -212,6 +274,47 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint32_t jb = bits_for(st[0]);
   if (gb + 32 + jb > 64) return SG_EOVERFLOW_FOLD;
+  const char* map_env = getenv("SG_FOLD_MAP");  // (SG_FOLD_MAP=0: always the sort)
+  const uint64_t range = st[2] - st[1] + 1;     // values lie in [AND, OR]
+  if (ngroups == 1 && jb == 0 && range <= kFoldMapMax && !(map_env && !atoi(map_env))) {
+    const uint64_t nt = div_up(range, (uint64_t)kFmTile);
+    WsPlan q;
+    const size_t qM = q.add(nt * kFmTile), qC = q.add(nt * 4), qP = q.add((nt + 1) * 8), qO = q.add(N * 4);
+    rc = ws_reserve(ctx, q.total + scan_ws_bytes(nt));
+    if (rc) return rc;
+    uint8_t* map = (uint8_t*)ws_at(ctx, qM);
+    uint32_t* mc = (uint32_t*)ws_at(ctx, qC);
+    uint64_t* mp = (uint64_t*)ws_at(ctx, qP);
+    uint32_t* mo = (uint32_t*)ws_at(ctx, qO);
+    const uint32_t lo = (uint32_t)st[1];
+    {
+      ScopedTimer tm(ctx, "union_fold");
+      ScopedTimer tk(ctx, "fold_map");
+      SG_HIP(hipMemsetAsync(map, 0, nt * kFmTile, ctx->stream));
+      hipLaunchKernelGGL(k_fold_mark, dim3((uint32_t)std::min<uint64_t>(div_up(N, 256), 8192)), dim3(256), 0,
+                         ctx->stream, dv, N, lo, map);
+      hipLaunchKernelGGL(k_fold_map_count, dim3((uint32_t)nt), dim3(kFmThreads), 0, ctx->stream, map, range, mc);
+      rc = scan_counts(ctx, mc, mp, nt, q.total);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_fold_map_write, dim3((uint32_t)nt), dim3(kFmThreads), 0, ctx->stream, map, range, lo,
+                         (const uint64_t*)mp, mo);
+      SG_HIP(hipGetLastError());
+    }
+    uint64_t total = 0;
+    SG_HIP(hipMemcpyAsync(&total, mp + nt, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    out_off[0] = 0;
+    out_off[1] = total;
+    if (total > cap) {
+      set_error("sg_union_fold: %llu values, capacity %zu", (unsigned long long)total, cap);
+      return SG_EINVAL;
+    }
+    if (total == 0) return SG_OK;
+    if (!out_vals) return SG_EINVAL;
+    SG_HIP(hipMemcpyAsync(out_vals, mo, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return SG_OK;
+  }
   // the key bits that vary: the group's, the values' (AND vs OR), the copy index's
   const uint64_t vary = ((gb ? ((1ull << gb) - 1) : 0ull) << (32 + jb)) | ((st[1] ^ st[2]) << jb) |
                         (jb ? (1ull << jb) - 1 : 0ull);

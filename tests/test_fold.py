@@ -110,3 +110,33 @@ def test_union_fold_zipf_corpus(ctx):
         gv, go = C.union_fold(vals, off, grp, ng, ctx=ctx)
         ev, eo = O.union_fold(vals, off, grp, ng)
         assert np.array_equal(go, eo) and np.array_equal(gv, ev)
+
+
+@pytest.mark.gpu
+def test_union_fold_byte_map_edges(ctx, monkeypatch):
+    """One group of canonical lists takes the byte map over [AND, OR] of the
+    values: value 0, spans just under and over 2^28 (the latter sorts), the
+    sentinel (dropped; its presence widens the span, so the fold sorts), lists
+    sharing most values; each equal to the oracle and to the sort
+    (SG_FOLD_MAP=0)."""
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(57)
+    for span in (1, 4096, (1 << 28) - 5, (1 << 28) + 5, 1 << 32):
+        lo = int(rng.integers(0, (1 << 32) - min(span, 1 << 32) + 1))
+        covs = []
+        for k in range(60):
+            m = int(rng.integers(0, 400))
+            v = lo + rng.integers(0, span, size=m, dtype=np.uint64)
+            covs.append(np.unique(v.astype(np.uint32)))
+        covs[0] = np.array([lo, min(lo + span - 1, 0xFFFFFFFF)], np.uint32)
+        if span == 1 << 32:
+            covs[1] = np.array([0, 0xFFFFFFFF], np.uint32)
+        vals, off = C.to_csr(covs)
+        ev, eo = O.union_fold(vals, off)
+        gv, go = C.union_fold(vals, off, ctx=ctx)
+        assert np.array_equal(go, eo) and np.array_equal(gv, ev), span
+        monkeypatch.setenv("SG_FOLD_MAP", "0")
+        sv, so = C.union_fold(vals, off, ctx=ctx)
+        monkeypatch.delenv("SG_FOLD_MAP")
+        assert np.array_equal(so, eo) and np.array_equal(sv, ev), span
