@@ -791,6 +791,12 @@ def run_steady_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):
         traces.append(g.trace.clone())
     so = torch.empty(g.ncalls + 1, dtype=torch.int64, device="cuda")
     states = [SignalSet(ctx) for _ in traces]
+    # warm the queued-lists path (a kernel's first launch in the process loads
+    # its code): nothing queued, so every program stops before its first call
+    rec_new.zero_()
+    call("sg_exec_signal_queued_dev", ctx.h, traces[0].data_ptr(), g.call_off.data_ptr(), g.prog_off.data_ptr(),
+         cfg["programs"], g.ncalls, g.npcs, rec_new.data_ptr(), g.sig.data_ptr(), so.data_ptr())
+    torch.cuda.synchronize()
     res = {}
     queued = []
     for mode in ("flags", "flags+queued", "flags+all"):
