@@ -368,35 +368,6 @@ __global__ __launch_bounds__(kPThreads) void k_hist_rep(const uint32_t* __restri
   }
 }
 
-// A lean pass-1 histogram: 256 threads, 2 KiB of LDS, a few registers -- a
-// kernel that can share the CUs with the persistent bucket kernel of the
-// previous batch (which leaves ~13 KiB of LDS and 32 VGPRs per SIMD lane of
-// each CU free), so batch i+1's histogram can overlap batch i's bucket stage.
-// Same output as k_hist_rep<false>.  Unaligned input is fine (dword loads).
-constexpr int kLeanT = 256;
-__global__ __launch_bounds__(kLeanT) void k_hist_lean(const uint32_t* __restrict__ v, const uint32_t* __restrict__ start,
-                                                      uint32_t T, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t cnt[2][256];
-  const int tid = threadIdx.x;
-  const uint32_t t = xcd_tile(blockIdx.x, T), s0 = start[t], s1 = start[t + 1];
-  cnt[0][tid] = 0;
-  cnt[1][tid] = 0;
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t re =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(v + s0), 0, (int)((s1 - s0) * 4u), 0x00020000);
-  const uint32_t n = s1 - s0, cp = (uint32_t)tid & 1u;
-  for (uint32_t i = 0; i < n; i += kLeanT * 8) {
-    uint32_t x[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b32(re, (i + u * kLeanT + tid) * 4u, 0, 0);
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (i + u * kLeanT + tid < n) atomicAdd(&cnt[cp][p1_digit(x[u])], 1u);
-  }
-  __syncthreads();
-  hist[(uint64_t)tid * T + t] = cnt[0][tid] + cnt[1][tid];
-}
-
 // Pass-2 histogram from the byte plane: hist[b * ncols + col] = count of
 // byte b over the chunk's positions [s0, s1).  The chunk's <= kPT bytes are
 // read as 16-B quads from s0 rounded down (<= kPT / 16 + 1 quads; the plane
@@ -1176,16 +1147,12 @@ __device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t sl, uint32_t r
   return false;  // map (nearly) full: the bucket spills
 }
 
-// A ticket: atomicAdd(p, 1) whose result is waited for later, by take_wait.
-// (The compiler's atomic optimizer scans a plain atomicAdd's result across the
-// wave at once, so thread 0's wave waited a global round trip at every bucket
-// install while the other waves waited for it at the next barrier.)
-__device__ __forceinline__ uint32_t take_ticket(uint32_t* p) {
-  uint32_t r;
-  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(1u) : "memory");
-  return r;
-}
-__device__ __forceinline__ void take_wait(uint32_t& r) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r)::"memory"); }
+// A ticket: a plain atomicAdd, its result read at the next install.  (An
+// inline-asm atomic waited for only there measured the same, 2.32-2.34 ms,
+// and leaves the compiler unaware that its result register is pending: r05
+// removed it.)
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* p) { return atomicAdd(p, 1u); }
+__device__ __forceinline__ void take_wait(uint32_t&) {}
 
 template <bool kDbg, bool kEmit>
 __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWaves))) void k_bucket(BucketArgs a) {
@@ -1224,11 +1191,6 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
     sh_b[1] = list_bucket(a, gridDim.x + blockIdx.x, nl, &q1);
     sh_q[1] = q1;
     pend_t = take_ticket(a.ticket);
-    // (waited for here, once: a ticket register flowing into the loop may be
-    // copied by the compiler before the atomic returns; inside the loop it is
-    // written by the atomic and read at the next install only -- check the ISA
-    // for a v_mov of it after any change here)
-    take_wait(pend_t);
   }
   __syncthreads();
   uint32_t b = uni(sh_b[0]), b1 = uni(sh_b[1]);
@@ -1903,8 +1865,6 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
     if (trace)
       hipLaunchKernelGGL(k_hist_trace, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals, d_off, nrec,
                          (const uint32_t*)tstart, (const uint32_t*)trec, T, hist1, (uint64_t*)ws_at(ctx, bp.oKM));
-    else if (ctx->hist_lean)  // (SG_HIST_LEAN: the histogram that can share CUs with a bucket stage)
-      hipLaunchKernelGGL(k_hist_lean, dim3(T), dim3(kLeanT), 0, ctx->stream, d_vals, (const uint32_t*)tstart, T, hist1);
     else if (((uintptr_t)d_vals & 15) == 0)
       hipLaunchKernelGGL(k_hist_rep<false>, dim3(T), dim3(kPThreads), 0, ctx->stream, d_vals,
                          (const uint32_t*)tstart, (const uint4*)nullptr, T, (const uint32_t*)nullptr, hist1);

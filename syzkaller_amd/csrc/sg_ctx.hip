@@ -68,6 +68,7 @@ int pin_reserve(sg_ctx* ctx, size_t bytes) {
   while (cap < bytes) cap *= 2;
   if (ctx->pin) {
     SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->copy_stream) SG_HIP(hipStreamSynchronize(ctx->copy_stream));  // (the host pipeline's DMAs)
     SG_HIP(hipHostFree(ctx->pin));
     ctx->pin = nullptr;
     ctx->pin_cap = 0;
@@ -83,6 +84,7 @@ int dstage_reserve(sg_ctx* ctx, size_t bytes) {
   while (cap < bytes) cap *= 2;
   if (ctx->dstage) {
     SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->copy_stream) SG_HIP(hipStreamSynchronize(ctx->copy_stream));  // (the host pipeline's DMAs)
     SG_HIP(hipFree(ctx->dstage));
     ctx->dstage = nullptr;
     ctx->dstage_cap = 0;
@@ -504,7 +506,6 @@ int sg_ctx_create(int device, sg_ctx** out) {
     if (v > 0 && v < c->owner_key_space) c->owner_key_space = v;
   }
   c->debug_part = getenv("SG_DEBUG_PART") != nullptr;
-  c->hist_lean = getenv("SG_HIST_LEAN") != nullptr && getenv("SG_HIST_LEAN")[0] != '0';
   int rc = ensure_device(c);
   if (rc) {
     delete c;
@@ -530,6 +531,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->copy_stream) hipStreamSynchronize(ctx->copy_stream);  // (before the buffers its DMAs use go)
   for (auto& r : ctx->timer.pending) {
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);

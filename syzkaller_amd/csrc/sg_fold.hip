@@ -274,9 +274,14 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint32_t jb = bits_for(st[0]);
   if (gb + 32 + jb > 64) return SG_EOVERFLOW_FOLD;
-  const char* map_env = getenv("SG_FOLD_MAP");  // (SG_FOLD_MAP=0: always the sort)
+  const char* map_env = getenv("SG_FOLD_MAP");  // (SG_FOLD_MAP=0: always the sort -- a test hook)
   const uint64_t range = st[2] - st[1] + 1;     // values lie in [AND, OR]
-  if (ngroups == 1 && jb == 0 && range <= kFoldMapMax && !(map_env && !atoi(map_env))) {
+  // the map's passes cost ~3 bytes of traffic per value of the range, the
+  // sort ~48 per key: the map only for a range dense enough (a few thousand
+  // PCs spread over 2^28 would memset and scan 256 MiB -- and keep it in the
+  // grow-only workspace -- to fold what the sort folds in microseconds)
+  const bool dense = range <= kFoldMapMax && range <= std::max<uint64_t>(1ull << 20, 16 * N);
+  if (ngroups == 1 && jb == 0 && dense && !(map_env && !atoi(map_env))) {
     const uint64_t nt = div_up(range, (uint64_t)kFmTile);
     WsPlan q;
     const size_t qM = q.add(nt * kFmTile), qC = q.add(nt * 4), qP = q.add((nt + 1) * 8), qO = q.add(N * 4);

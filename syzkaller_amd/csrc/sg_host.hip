@@ -86,6 +86,8 @@ int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = ensure_device(ctx);
   if (rc) return rc;
+  // (the staging buffers may still be read by an earlier call's copies)
+  if (ctx->copy_stream) SG_HIP(hipStreamSynchronize(ctx->copy_stream));
   rc = pin_reserve(ctx, 2 * b_slot);
   if (rc) return rc;
   rc = dstage_reserve(ctx, 2 * b_slot + b_flag);
@@ -99,8 +101,6 @@ int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
   uint8_t* dflag = (uint8_t*)(dst + 2 * b_slot);
   hipEvent_t* ev_dma = ctx->pipe_ev;      // slot k's DMA done (pinned k free, device k filled)
   hipEvent_t* ev_tri = ctx->pipe_ev + 2;  // slot k's triage done (device k free)
-  // (the staging buffers may still be read by an earlier call's copies)
-  SG_HIP(hipStreamSynchronize(ctx->copy_stream));
   for (size_t i = 0; i < sl.size(); i++) {
     const HostSlice& s = sl[i];
     const int k = (int)(i & 1);
@@ -118,7 +118,10 @@ int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     SG_HIP(hipEventRecord(ev_dma[k], ctx->copy_stream));
     SG_HIP(hipStreamWaitEvent(ctx->stream, ev_dma[k], 0));
     rc = bucket_triage(ctx, mwords, nwords, (const uint32_t*)dv, dof, n, nr, dflag + s.r0, trace);
-    if (rc) return rc;
+    if (rc) {  // (no DMA may still be reading pinned or writing device staging when this call returns)
+      hipStreamSynchronize(ctx->copy_stream);
+      return rc;
+    }
     SG_HIP(hipEventRecord(ev_tri[k], ctx->stream));
   }
   if (nrec) SG_HIP(hipMemcpyAsync(rec_new, dflag, nrec, hipMemcpyDeviceToHost, ctx->stream));

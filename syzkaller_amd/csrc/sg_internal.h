@@ -105,7 +105,6 @@ struct sg_ctx {
   // two-phase triage state (prefix_begin / prefix_end, sg_bucket.hip)
   PrefixSlot prefix[kPrefixSlots];
   bool debug_part = false;
-  bool hist_lean = false;  // SG_HIST_LEAN: the lean pass-1 histogram (sg_bucket.hip k_hist_lean)
   // rebased record offsets of record slices (grow-only, owned)
   uint64_t* slice_off = nullptr;
   size_t slice_off_cap = 0;

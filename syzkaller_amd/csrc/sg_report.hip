@@ -29,9 +29,6 @@
 #include <algorithm>
 #include <cstdlib>
 
-#ifndef SG_REPORT_DIAG
-#define SG_REPORT_DIAG 0
-#endif
 
 namespace sg {
 
@@ -188,8 +185,7 @@ constexpr uint32_t kChunkIdx = 8192;     // radix buckets over the chunk bounds
 constexpr uint32_t kSiteIdx = 1024;      // radix buckets over one chunk's sites
 constexpr uint32_t kSymCap = 1024;       // symbols of a chunk held in LDS
 constexpr int kQT = 1024;                // threads of the count / scatter kernels
-constexpr int kQPer = 16;                // queries per thread there (kSQPer when staged)
-constexpr int kSQPer = 8;
+constexpr int kSQPer = 8;                // queries per thread there
 constexpr int kCT = 512;                 // threads of the chunk kernel
 constexpr uint32_t kCTile = 32768;       // grouped queries per chunk-kernel tile
 
@@ -219,7 +215,7 @@ struct ChunkArgs {
   uint64_t* jstart;        // [nch + 2] scan of jparts
   uint64_t* qoff;          // [nch + 2] each chunk's first slot
   uint2* grouped;          // [ncov] (cov, query index) grouped by chunk
-  uint16_t* qchunk;        // [ncov] each query's chunk (written by the count kernel; null: recomputed)
+  uint16_t* qchunk;        // [ncov] each query's chunk (written by the count kernel)
   uint32_t* first_q;
   uint32_t* last_del;
 };
@@ -344,7 +340,7 @@ __global__ __launch_bounds__(kQT) void k_q_count(ChunkArgs a) {
     if (i < a.ncov) {
       const uint32_t c = chunk_of(a, L, query_pc(a.hi32, a.cov[i]));
       atomicAdd(&hist[c], 1u);
-      if (a.qchunk) a.qchunk[i] = (uint16_t)c;  // (kMaxChunks + 1 <= 2^16)
+      a.qchunk[i] = (uint16_t)c;  // (kMaxChunks + 1 <= 2^16)
     }
   }
   __syncthreads();
@@ -360,19 +356,20 @@ __global__ void k_q_chunk_off(ChunkArgs a) {
 }
 
 // (cov, query index) into the chunk's range: per workgroup a rank per chunk
-// (LDS atomics) on top of the (chunk, tile) offset from the scan.  kStaged:
-// the tile is staged in LDS in chunk order, then written out slot by slot, so
-// a wave's stores are runs of consecutive addresses (the LDS it needs leaves
-// one workgroup per CU); otherwise every query is one 8-B store.
-template <int kPer, bool kStaged>
+// (LDS atomics) on top of the (chunk, tile) offset from the scan; each
+// query's chunk comes from the count kernel.  The tile is staged in LDS in
+// chunk order, then written out slot by slot, so a wave's stores are runs of
+// consecutive addresses.  (Measured and removed in r05: one 8-B store per
+// query, 1.08 ms against 0.84 per 100M queries; the chunk searched again
+// instead of read back, +0.27 ms.)
+template <int kPer>
 __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
   constexpr uint32_t kT = kQT * kPer;
-  __shared__ ChunkLds L;
   __shared__ uint32_t hist[kMaxChunks + 1];  // counts, then the tile's chunk offsets
-  __shared__ uint2 stage[kStaged ? kT : 1];
-  __shared__ uint16_t cid[kStaged ? kT : 1];
+  __shared__ uint32_t base[kMaxChunks + 1];  // each chunk's first slot for this tile
+  __shared__ uint2 stage[kT];
+  __shared__ uint16_t cid[kT];
   __shared__ uint32_t wsum[kQT / 64 + 1];
-  if (!a.qchunk) load_chunks(a, L);
   for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
   __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kT;
@@ -384,30 +381,13 @@ __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
     ch[k] = 0xFFFFFFFFu;
     if (i < a.ncov) {
       cv[k] = a.cov[i];
-      ch[k] = a.qchunk ? (uint32_t)a.qchunk[i] : chunk_of(a, L, query_pc(a.hi32, cv[k]));
+      ch[k] = a.qchunk[i];
     }
   }
 #pragma unroll
   for (int k = 0; k < kPer; k++)
     if (ch[k] != 0xFFFFFFFFu) rk[k] = atomicAdd(&hist[ch[k]], 1u);
   __syncthreads();
-  uint32_t* base = reinterpret_cast<uint32_t*>(L.bnd);  // (the bounds are no longer needed)
-  if (!kStaged) {
-    for (uint32_t c = threadIdx.x; c <= a.nch; c += kQT)
-      base[c] = hist[c] ? (uint32_t)a.toff[(uint64_t)c * a.tw + tile_col(blockIdx.x, a.tw)] : 0u;
-    __syncthreads();
-#if SG_REPORT_DIAG
-    // diagnostics: linear stores (the scatter's pattern removed; results wrong)
-#pragma unroll
-    for (int k = 0; k < kPer; k++)
-      if (ch[k] != 0xFFFFFFFFu) a.grouped[q0 + (uint64_t)k * kQT] = make_uint2(cv[k], base[ch[k]] + rk[k]);
-#else
-#pragma unroll
-    for (int k = 0; k < kPer; k++)
-      if (ch[k] != 0xFFFFFFFFu) a.grouped[base[ch[k]] + rk[k]] = make_uint2(cv[k], (uint32_t)(q0 + (uint64_t)k * kQT));
-#endif
-    return;
-  }
   // per thread kPerT consecutive chunks: the (chunk, tile) base and the
   // exclusive scan of the counts (the chunk's first staging slot)
   constexpr uint32_t kPerT = (kMaxChunks + 1 + kQT - 1) / kQT;
@@ -790,15 +770,15 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   plan_idx(nsym, sym_end[0], sym_end[nsym - 1], iend);
   plan_idx(nall, all_pcs[0], all_pcs[nall - 1], ipcs);
   const size_t o_ie = p.add(((uint64_t)iend.nb + 1) * 4), o_ip = p.add(((uint64_t)ipcs.nb + 1) * 4);
-  // chunked query path (k_q_*) up to kMaxChunks chunks of call sites;
-  // SG_REPORT_DIRECT=1 forces the per-query search passes (k_rep_first / k_rep_del)
+  // chunked query path (k_q_*) up to kMaxChunks chunks of call sites, the
+  // per-query search passes (k_rep_first / k_rep_del) past them;
+  // SG_REPORT_DIRECT=1 takes the latter at any size (a test hook for the
+  // > 16M-site regime)
   const char* direct_env = getenv("SG_REPORT_DIRECT");
   const bool chunked = nall <= (uint64_t)kSites * kMaxChunks && !(direct_env && atoi(direct_env));
   const uint32_t nch = div_up(nall, kSites);
-  // query tiles: 16K queries (8K staged) per count / scatter workgroup
-  const char* staged_env = getenv("SG_REPORT_STAGED");
-  const bool staged = !staged_env || atoi(staged_env);  // (SG_REPORT_STAGED=0: one store per query)
-  const uint32_t ntq = div_up(ncov, (uint64_t)kQT * (staged ? kSQPer : kQPer));
+  // query tiles: 8K queries per count / scatter workgroup
+  const uint32_t ntq = div_up(ncov, (uint64_t)kQT * kSQPer);
   const uint32_t tw = 8 * div_up(ntq, 8);
   const uint64_t ntc = chunked ? ((uint64_t)nch + 1) * tw : 1;
   const size_t o_bnd = p.add((uint64_t)nch * 8), o_sr = p.add(((uint64_t)nch + 1) * 8),
@@ -807,11 +787,8 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
                o_si = p.add((uint64_t)nch * (kSiteIdx + 1) * 2), o_sy = p.add(chunked ? nall * 4 : 4),
                o_tc = p.add(ntc * 4), o_to = p.add((ntc + 1) * 8), o_jp = p.add(((uint64_t)nch + 1) * 4),
                o_js = p.add(((uint64_t)nch + 2) * 8), o_srt = p.add(4);
-  // the count kernel's per-query chunks, read back by the staged scatter
-  // (SG_REPORT_QCHUNK=0: the scatter searches each query's chunk again)
-  const char* qchunk_env = getenv("SG_REPORT_QCHUNK");
-  const bool qchunk = chunked && staged && !(qchunk_env && !atoi(qchunk_env));
-  const size_t o_qc = p.add(qchunk ? ncov * 2 : 2);
+  // the count kernel's per-query chunks, read back by the scatter
+  const size_t o_qc = p.add(chunked ? ncov * 2 : 2);
   size_t scan_off = p.total;
   rc = ws_reserve(ctx, p.total + std::max(scan_ws_bytes(nchunks), scan_ws_bytes(ntc)));
   if (rc) return rc;
@@ -884,7 +861,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     k.toff = (uint64_t*)ws_at(ctx, o_to);
     k.qoff = (uint64_t*)ws_at(ctx, o_qo);
     k.grouped = (uint2*)ws_at(ctx, o_gq);
-    k.qchunk = qchunk ? (uint16_t*)ws_at(ctx, o_qc) : nullptr;
+    k.qchunk = (uint16_t*)ws_at(ctx, o_qc);
     k.first_q = a.first_q;
     k.last_del = a.last_del;
     // queries in PC order (the reference's canonical covers) need no regrouping
@@ -917,10 +894,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
       hipLaunchKernelGGL(k_site_index, dim3(div_up((uint64_t)nch * (kSiteIdx + 1), 256)), dim3(256), 0, ctx->stream,
                          k);
       if (tw != ntq) SG_HIP(hipMemsetAsync(k.tcount, 0, ntc * 4, ctx->stream));  // (the padding columns)
-      if (staged)
-        hipLaunchKernelGGL(k_q_count<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
-      else
-        hipLaunchKernelGGL(k_q_count<kQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_q_count<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
       rc = scan_counts(ctx, k.tcount, k.toff, ntc, scan_off);
       if (rc) return rc;
       hipLaunchKernelGGL(k_q_chunk_off, dim3(div_up((uint64_t)nch + 2, 256)), dim3(256), 0, ctx->stream, k);
@@ -929,10 +903,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     }
     if (unsorted) {
       ScopedTimer tm(ctx, "report_scatter_q");
-      if (staged)
-        hipLaunchKernelGGL((k_q_scatter<kSQPer, true>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
-      else
-        hipLaunchKernelGGL((k_q_scatter<kQPer, false>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      hipLaunchKernelGGL(k_q_scatter<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
     }
     {
       ScopedTimer tm(ctx, "report_chunks");

@@ -117,12 +117,12 @@ def test_union_fold_byte_map_edges(ctx, monkeypatch):
     """One group of canonical lists takes the byte map over [AND, OR] of the
     values: value 0, spans just under and over 2^28 (the latter sorts), the
     sentinel (dropped; its presence widens the span, so the fold sorts), lists
-    sharing most values; each equal to the oracle and to the sort
-    (SG_FOLD_MAP=0)."""
+    sharing most values, a wide span over few values (too sparse for the map:
+    sorts); each equal to the oracle and to the sort (SG_FOLD_MAP=0)."""
     from syzkaller_amd import cover as C
 
     rng = np.random.default_rng(57)
-    for span in (1, 4096, (1 << 28) - 5, (1 << 28) + 5, 1 << 32):
+    for span in (1, 4096, 1 << 24, (1 << 28) - 5, (1 << 28) + 5, 1 << 32):
         lo = int(rng.integers(0, (1 << 32) - min(span, 1 << 32) + 1))
         covs = []
         for k in range(60):
@@ -130,6 +130,8 @@ def test_union_fold_byte_map_edges(ctx, monkeypatch):
             v = lo + rng.integers(0, span, size=m, dtype=np.uint64)
             covs.append(np.unique(v.astype(np.uint32)))
         covs[0] = np.array([lo, min(lo + span - 1, 0xFFFFFFFF)], np.uint32)
+        if span in ((1 << 28) - 5, (1 << 28) + 5):  # dense enough for the map (range <= 16 N)
+            covs[2] = np.arange(lo, lo + span, 15, dtype=np.uint64).astype(np.uint32)
         if span == 1 << 32:
             covs[1] = np.array([0, 0xFFFFFFFF], np.uint32)
         vals, off = C.to_csr(covs)

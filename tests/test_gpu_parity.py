@@ -626,18 +626,17 @@ def _trace_for_signals(sigs, call_off):
     return pcs
 
 
-@pytest.mark.parametrize("rows", ["0", "1", "2", "4", "8", "16", "102", "104", "141", "142", "144"])  # 0: speculative; 10K: producer wave; 14D: D deciding waves
-def test_exec_signal_region_boundaries_vs_oracle(C, monkeypatch, rows):
+def test_exec_signal_region_boundaries_vs_oracle(C):
     """Signals crowded onto the slots where the slot-region kernel's lanes meet
     (home % 128 in 124..127 and 0..3, table wrap-around 8189..8191 -> 0..2), a
     few distinct high parts so probe windows fill and home slots get
-    overwritten, the zero signal, repeats: every window's decisions in
-    program order, as executor.h:507-526 takes them."""
-    monkeypatch.setenv("SG_EXEC_REGION", rows)
+    overwritten, the zero signal, repeats, empty calls: every window's
+    decisions in program order, as executor.h:507-526 takes them."""
     rng = np.random.default_rng(117)
     homes = np.array([(r * 128 + d) % 8192 for r in (0, 1, 2, 31, 63) for d in range(-4, 4)], np.uint64)
     for nprog, calls, pcs, nhigh in [(2, 3, 700, 3), (6, 4, 1500, 6), (3, 2, 5000, 40)]:
         lens = rng.integers(1, 2 * pcs, size=nprog * calls).astype(np.uint64)
+        lens[rng.random(lens.size) < 0.2] = 0  # empty calls between full ones
         call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
         n = int(call_off[-1])
         hi = rng.integers(0, nhigh, size=n).astype(np.uint64) * 8192 + 8192 * 977
@@ -810,9 +809,8 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
     spans more symbols than it holds in LDS (many site-less symbols: global
     symbol search), queries below the first and above the last call site,
     site counts at and around the 4096-site chunk size; the same queries in
-    PC order (no regrouping), with one store per query (SG_REPORT_STAGED=0),
-    with the scatter searching the chunks again (SG_REPORT_QCHUNK=0) and
-    through the direct per-query passes (SG_REPORT_DIRECT=1)."""
+    PC order (no regrouping), and through the direct per-query passes of the
+    > 16M-site regime (SG_REPORT_DIRECT=1)."""
     rng = np.random.default_rng(143)
     hi32 = np.uint64(0xffffffff) << np.uint64(32)
     base = np.uint64(0xffffffff81000000)
@@ -837,14 +835,6 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
         qs = np.sort(q)
         assert np.array_equal(C.cover_uncovered(qs, 0xffffffff, starts, ends, sites),
                               O.cover_uncovered(qs, 0xffffffff, starts, ends, sites)), sites.size
-        monkeypatch.setenv("SG_REPORT_STAGED", "0")  # one store per query
-        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
-        monkeypatch.delenv("SG_REPORT_STAGED")
-        assert np.array_equal(got, exp), sites.size
-        monkeypatch.setenv("SG_REPORT_QCHUNK", "0")  # the scatter searching each query's chunk again
-        got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
-        monkeypatch.delenv("SG_REPORT_QCHUNK")
-        assert np.array_equal(got, exp), sites.size
         monkeypatch.setenv("SG_REPORT_DIRECT", "1")
         got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
         monkeypatch.delenv("SG_REPORT_DIRECT")
