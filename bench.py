@@ -856,6 +856,8 @@ def main():
                     help="C3 protocol: bitmap prefixes (default) or candidate pairs hash-sharded by signal")
     ap.add_argument("--c3-form", choices=["auto", "kept", "pairs"], default="auto",
                     help="the prefix protocol's per-batch step-1 form (auto: by the last batch's novelty)")
+    ap.add_argument("--c3-exchange", choices=["auto", "dense", "sparse"], default="auto",
+                    help="the prefix protocol's exchange: bitmaps, candidate lists, or by the agreed novelty")
     ap.add_argument("--c3-steady", action="store_true",
                     help="measurement: C3 over steady-state batches (a fixed population with flaky coverage)")
     ap.add_argument("--c3-two-phase", action="store_true",

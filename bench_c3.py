@@ -94,10 +94,11 @@ def run_c3(ctx, args, cfg, rank, world):
             with torch.cuda.stream(side):
                 side_st = HipStages(side_ctx)
         tri = PrefixTriage(HipStages(ctx), Comm(), two_phase_at_one=two_phase, side_stages=side_st, side_stream=side,
-                           form=getattr(args, "c3_form", "auto"))
+                           form=getattr(args, "c3_form", "auto"), exchange=getattr(args, "c3_exchange", "auto"))
     else:
         tri = ShardedTriage(HipStages(ctx), Comm())
     forms = []  # the prefix protocol's step-1 form per batch
+    xchg = []   # its exchange form and bytes per rank, per batch (warm-up batches included)
     rec_base = rank * nprog * calls
     nrec_total = world * nprog * calls
     # every step runs against the restored snapshot: overlapped steps use a
@@ -115,10 +116,13 @@ def run_c3(ctx, args, cfg, rank, world):
                 ms = states[i]
             if not pipelined:
                 tri.step(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
+                if prefix:
+                    xchg.append((tri.last.get("exchange", "local"), tri.last.get("exchange_bytes", 0)))
                 continue
             p = tri.start(ms, newsig, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_news[i % 2], nrec_total)
             if prefix:
                 forms.append(p["last"].get("form"))
+                xchg.append((p["last"].get("exchange", "local"), p["last"].get("exchange_bytes", 0)))
             if pend is not None:
                 tri.finish(pend)
             pend = p
@@ -208,7 +212,12 @@ def run_c3(ctx, args, cfg, rank, world):
         if world > 1:
             dist.barrier()
     if prefix:
-        xgmi = last.get("exchange_bytes", 0)
+        # per exchange form, the mean bytes a rank sent per step (dense: bitmaps
+        # whatever the novelty; sparse: the candidate lists)
+        by = {}
+        for f, nb in xchg:
+            by.setdefault(f, []).append(nb)
+        xgmi = {f: sum(v) / len(v) for f, v in by.items()}
     else:
         xgmi = 8 * acct["pairs_sent"] / world + 4 * (acct["n_rec"] / 32) / world + 4 * last["new_signal"]
     if rank != 0:
@@ -248,6 +257,7 @@ def run_c3(ctx, args, cfg, rank, world):
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,
         "prefix_forms": forms[-args.steps:] if prefix and forms else None,
+        "exchange_forms": [f for f, _ in xchg[-args.steps:]] if prefix else None,
         "path": ("prefix (syzkaller_amd/shard.py PrefixTriage)" if prefix else
                  "sharded (syzkaller_amd/shard.py ShardedTriage + sg_shard.hip)"),
         "gen_s": round(t_gen, 2),

@@ -196,6 +196,14 @@ int sg_shard_flags_dev(sg_ctx* ctx, const uint32_t* d_bits, uint32_t nparts, uin
 /* SignalAdd of n device-resident values (fuzzer.go:673-674 for the new signal
  * every shard found). */
 int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
+/* maxsig |= the n device values; newsig (nullable) gains those maxsig lacked
+ * before this call (fuzzer.go:673-674: newSignal.Merge(diff), diff =
+ * maxSignal.Diff(sig)), duplicates in the values included.  The sparse form of
+ * the prefix protocol's set updates (syzkaller_amd/shard.py). */
+int sg_set_add_new_dev(sg_set* newsig, sg_set* maxsig, const uint32_t* d_vals, uint64_t n);
+/* Clears the bits of the n device values (the sparse prefix protocol clears
+ * the prefix bits it set, so the bitmap stays zero between batches). */
+int sg_set_del_dev(sg_set* set, const uint32_t* d_vals, uint64_t n);
 /* Bitmap prefix exchange of the prefix protocol (syzkaller_amd/shard.py
  * PrefixTriage): d_parts holds nparts bitmap slices of `words` u32 words each,
  * part k from rank k.  d_prefix[k] = OR of parts 0..k-1 (part 0: zero),
@@ -244,6 +252,12 @@ int sg_prefix_begin_form_dev(sg_ctx* ctx, uint32_t slot, uint32_t form, sg_set* 
 			     uint64_t* d_ncand);
 int sg_prefix_end_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix, sg_set* newsig,
 		      uint8_t* d_rec_new);
+/* The signals of a pairs-form begin's kept pairs (slot's batch: each
+ * distinct signal of the batch not in base, once), d_out[i] for i < min(n,
+ * cap), n = the count begin wrote to d_ncand.  The candidate lists the sparse
+ * prefix exchange all-gathers (shard.py PrefixTriage) instead of bitmaps;
+ * fuzzer.go:665-691 over one batch spread across ranks. */
+int sg_prefix_cands_dev(sg_ctx* ctx, uint32_t slot, uint32_t* d_out, uint64_t cap);
 int sg_prefix_flags_dev(sg_ctx* ctx, uint32_t slot, sg_set* maxsig, const uint32_t* d_prefix,
 			uint8_t* d_rec_new);
 

@@ -192,6 +192,32 @@ def put_uvarint(x):
     return bytes(out)
 
 
+def delta_encode_batch(vals, off):
+    """delta_encode of every list of a CSR batch at once, vectorised (the same
+    bytes as delta_encode list by list; checked against it in
+    tests/test_rpc.py): (payload bytes, byte offsets per list)."""
+    v = _u32(vals).astype(np.int64)
+    o = _u64(off).astype(np.int64)
+    prev = np.zeros_like(v)
+    prev[1:] = v[:-1]
+    lens = np.diff(o)
+    prev[o[:-1][lens > 0]] = 0  # each list's first value is encoded whole
+    d = v - prev
+    assert (d >= 0).all(), "sorted lists"
+    nb = np.ones(d.size, np.int64)
+    x = d >> 7
+    while x.any():  # Uvarint: 7 bits per byte, high bit = more bytes follow
+        nb += x > 0
+        x >>= 7
+    pos = np.cumsum(nb) - nb
+    out = np.empty(int(nb.sum()), np.uint8)
+    for k in range(int(nb.max()) if nb.size else 0):
+        m = nb > k
+        out[pos[m] + k] = (((d[m] >> (7 * k)) & 0x7F) | ((nb[m] > k + 1) << 7)).astype(np.uint8)
+    cb = np.concatenate([[0], np.cumsum(nb)])
+    return out, cb[o].astype(np.uint64)
+
+
 def delta_encode(lst):
     """The RPC payload of a sorted []uint32 (pkg/rpctype/rpctype.go:8-63 fields):
     PutUvarint of the first value, then of each successive difference."""

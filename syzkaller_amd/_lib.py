@@ -67,6 +67,9 @@ SIGNATURES = {
     "sg_shard_owners_dev": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "sg_shard_flags_dev": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_uint64, c_uint64, c_void_p]),
     "sg_set_add_dev": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "sg_set_add_new_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
+    "sg_set_del_dev": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "sg_prefix_cands_dev": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64]),
     "sg_bitmap_prefix_or_dev": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "sg_bitmap_prefix_or_rank_dev": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p]),
     "sg_set_or_new_or_dev": (c_int, [c_void_p, c_void_p, c_void_p]),

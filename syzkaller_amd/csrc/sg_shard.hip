@@ -191,6 +191,34 @@ __global__ void k_set_add_vals(uint32_t* __restrict__ words, const uint32_t* __r
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sgd::set_bit(words, v[i]);
 }
 
+// maxsig |= v; newsig (nullable) gains the values maxsig lacked (fuzzer.go:673-674).
+// The atomic's old word decides: of several copies of one value only the
+// first setter sees its bit clear.
+__global__ void k_set_add_new_vals(uint32_t* __restrict__ nwords, uint32_t* __restrict__ mwords,
+                                   const uint32_t* __restrict__ v, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t s = v[i], w = sgd::set_pos(s) >> 5, b = 1u << (s & 31);
+    const uint32_t old = atomicOr(&mwords[w], b);
+    if (nwords && !(old & b)) atomicOr(&nwords[w], b);
+  }
+}
+
+__global__ void k_set_del_vals(uint32_t* __restrict__ words, const uint32_t* __restrict__ v, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t s = v[i];
+    atomicAnd(&words[sgd::set_pos(s) >> 5], ~(1u << (s & 31)));
+  }
+}
+
+// the signals of a pairs-form begin's kept pairs {s, first record}, <= cap
+__global__ void k_pair_sigs(const uint2* __restrict__ pairs, const unsigned long long* __restrict__ np, uint64_t cap,
+                            uint32_t* __restrict__ out) {
+  const uint64_t n = *np < cap ? *np : cap, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = pairs[i].x;
+}
+
 // exclusive prefix-OR over the parts, word by word, and the total
 __global__ void k_prefix_or(const uint32_t* __restrict__ parts, uint32_t nparts, uint64_t words,
                             uint32_t* __restrict__ prefix, uint32_t* __restrict__ total) {
@@ -560,6 +588,57 @@ int sg_set_add_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {
   ScopedTimer tm(ctx, "set_add");
   hipLaunchKernelGGL(k_set_add_vals, dim3(std::min<uint64_t>(div_up(n, 256), 16384)), dim3(256), 0, ctx->stream,
                      set->words, d_vals, n);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_set_add_new_dev(sg_set* newsig, sg_set* maxsig, const uint32_t* d_vals, uint64_t n) {
+  if (!maxsig || (n && !d_vals) || (newsig && (newsig->ctx != maxsig->ctx || newsig == maxsig))) {
+    set_error("sg_set_add_new_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = maxsig->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "set_add");
+  hipLaunchKernelGGL(k_set_add_new_vals, dim3(std::min<uint64_t>(div_up(n, 256), 16384)), dim3(256), 0, ctx->stream,
+                     newsig ? newsig->words : nullptr, maxsig->words, d_vals, n);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_set_del_dev(sg_set* set, const uint32_t* d_vals, uint64_t n) {
+  if (!set || (n && !d_vals)) return SG_EINVAL;
+  if (n == 0) return SG_OK;
+  sg_ctx* ctx = set->ctx;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  ScopedTimer tm(ctx, "set_add");
+  hipLaunchKernelGGL(k_set_del_vals, dim3(std::min<uint64_t>(div_up(n, 256), 16384)), dim3(256), 0, ctx->stream,
+                     set->words, d_vals, n);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+int sg_prefix_cands_dev(sg_ctx* ctx, uint32_t slot, uint32_t* d_out, uint64_t cap) {
+  if (!ctx || slot >= kPrefixSlots || (cap && !d_out)) {
+    set_error("sg_prefix_cands_dev: invalid argument");
+    return SG_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = ensure_device(ctx);
+  if (rc) return rc;
+  const PrefixSlot& S = ctx->prefix[slot];
+  if (!S.open || S.keep) {
+    set_error("sg_prefix_cands_dev: slot %u holds no pairs-form batch", slot);
+    return SG_EINVAL;
+  }
+  if (!cap || !S.n) return SG_OK;
+  hipLaunchKernelGGL(k_pair_sigs, dim3(std::min<uint64_t>(div_up(cap, 256), 8192)), dim3(256), 0, ctx->stream,
+                     (const uint2*)((char*)S.ws + 256), (const unsigned long long*)S.ws, cap, d_out);
   SG_HIP(hipGetLastError());
   return SG_OK;
 }

@@ -179,6 +179,20 @@ class HipStages:
         if n:
             call("sg_set_add_dev", sset.h, vals.data_ptr(), n)
 
+    def add_new(self, newset, sset, vals, n):
+        """sset |= vals[:n]; newset (nullable) gains those sset lacked."""
+        if n:
+            call("sg_set_add_new_dev", newset.h if newset is not None else None, sset.h, vals.data_ptr(), n)
+
+    def delete(self, sset, vals, n):
+        """Clears the bits of vals[:n]."""
+        if n:
+            call("sg_set_del_dev", sset.h, vals.data_ptr(), n)
+
+    def prefix_cands(self, out, cap, slot=0):
+        """out[:min(count, cap)] = the signals of the slot's pairs-form batch."""
+        call("sg_prefix_cands_dev", self.ctx.h, slot, out.data_ptr() if cap else None, cap)
+
     # the prefix protocol's stages (PrefixTriage)
     words = 1 << 27  # a set's 2^32-bit bitmap
 
@@ -354,9 +368,21 @@ class PrefixTriage:
          triage is the loop itself, so the flags are the loop's.
       4. maxSignal = M0 | T and newSignal |= T on every rank (step 3 left
          maxSignal between M0 and M0 | T).
-    Per rank and step the exchange moves about 2.5 bitmaps (512 MiB each)
-    whatever the novelty, where ShardedTriage moves 8 B per candidate; at one
-    rank it is the plain local triage.
+    Per rank and step the dense exchange moves about 2.5 bitmaps (512 MiB
+    each) whatever the novelty, where ShardedTriage moves 8 B per candidate; at
+    one rank it is the plain local triage.
+
+    The sparse exchange (route only the candidates s not in
+    M0) moves C_k as a list instead: step 1 in its pairs form keeps each s of
+    C_k once, every rank all-gathers the lists (4 B per candidate, after an
+    all-gather of the counts), P_k is set in a zeroed bitmap from the lists of
+    the ranks before k (and cleared again after step 3, so it stays zero), and
+    step 4 adds every list to maxSignal / newSignal.  The fuzzer's steady
+    state (139K candidates per C2-sized step) exchanges ~0.5 MB per rank
+    instead of ~1 GB.  Every rank gathers its (candidates, entries) after step
+    1; the form of batch b is agreed from those counts of batch b - 2 (the
+    same numbers on every rank, long arrived): sparse while every rank's
+    candidates stay below sparse_below of its entries.
 
     start() runs steps 1-2 and leaves the exchange running on RCCL's stream
     (the prefix-OR on a side stream between the collectives); finish() runs
@@ -380,7 +406,7 @@ class PrefixTriage:
     contracts: HipStages."""
 
     def __init__(self, stages, comm=None, device="cuda", two_phase_at_one=False, side_stages=None, side_stream=None,
-                 gather=None, form="auto", pairs_below=0.05):
+                 gather=None, form="auto", pairs_below=0.05, exchange="auto", sparse_below=None):
         self.st = stages
         self.comm = comm if comm is not None else Comm()
         self.device = device
@@ -405,7 +431,7 @@ class PrefixTriage:
                     # (this rank's P_k and T only; at one rank T is C itself)
                     C = torch.zeros(W, dtype=torch.int32, device=device)
                     b = {"C": C, "allc": torch.empty(G * W, dtype=torch.int32, device=device) if G > 1 else C,
-                         "P": torch.empty(W, dtype=torch.int32, device=device) if self.comm.rank > 0 else None,
+                         "P": torch.zeros(W, dtype=torch.int32, device=device) if self.comm.rank > 0 else None,
                          "T": torch.empty(W, dtype=torch.int32, device=device) if G > 1 else C}
                 else:
                     b = {k: torch.zeros(n, dtype=torch.int32, device=device) for k in ("C", "P", "T")}
@@ -415,10 +441,22 @@ class PrefixTriage:
                 b["cset"] = stages.wrap(b["C"])
                 b["ncand"] = torch.zeros(1, dtype=torch.int64, device=device)
                 b["ncand_h"] = torch.zeros(1, dtype=torch.int64, pin_memory=(device != "cpu"))
+                # every rank's (candidates, entries) of the slot's batch (the sparse form's
+                # counts and the agreed form two batches later); P zero between sparse uses
+                b["cnt"] = torch.zeros(2, dtype=torch.int64, device=device)
+                b["cnts"] = torch.zeros(2 * G, dtype=torch.int64, device=device)
+                b["cnts_h"] = torch.zeros(2 * G, dtype=torch.int64, pin_memory=(device != "cpu"))
+                P = b["P"] if self.comm.rank > 0 else None
+                b["pset"] = stages.wrap(P) if P is not None else None
+                b["pclean"] = True
                 self.slots.append(b)
         self.next_slot = 0
         self.last = {}
         self.form, self.pairs_below = form, pairs_below
+        self.exchange = exchange
+        self.sparse_below = 0.05 if sparse_below is None else sparse_below
+        self.counted = []  # (slot, event) of the gathered counts of the last two started batches
+        self._bufs = {}
         self.novelty = None  # |C_k| / entries of the last batch whose count has come back
         self._nov = None     # (slot, entries, event) of the count in flight
 
@@ -436,6 +474,27 @@ class PrefixTriage:
                 self.novelty = float(self.slots[slot]["ncand_h"].item()) / max(n, 1)
                 self._nov = None
         return 1 if self.novelty is not None and self.novelty < self.pairs_below else 0
+
+    def _exchange_form(self):
+        """This batch's exchange ("dense" or "sparse"), the same on every rank:
+        from the gathered counts of the batch started two starts ago."""
+        if self.exchange in ("dense", "sparse"):
+            return self.exchange
+        if len(self.counted) < 2:
+            return "dense"
+        slot, ev = self.counted[-2]
+        if ev is not None:
+            ev.synchronize()
+        c = self.slots[slot]["cnts_h"].view(-1, 2).tolist()
+        frac = max(n / max(e, 1) for n, e in c)
+        return "sparse" if frac < self.sparse_below else "dense"
+
+    def _buf(self, name, n, dtype=torch.int32):
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 1), dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b
 
     def step(self, maxsig, newsig, vals, off, nvals, nrec, rec_base, rec_new, nrec_total=None):
         """Same contract as ShardedTriage.step."""
@@ -458,8 +517,9 @@ class PrefixTriage:
         slot = self.next_slot
         self.next_slot ^= 1
         b = self.slots[slot]
+        xform = self._exchange_form()  # (reads this slot's counts of two batches ago)
         # 1. this rank's new signal against M0 (its partitions, or its pairs, kept for 3.)
-        form = self._form()
+        form = 1 if xform == "sparse" else self._form()
         if form is None:
             st.prefix_begin(maxsig, b["cset"], vals, off, nvals, nrec, slot)
         else:
@@ -473,6 +533,38 @@ class PrefixTriage:
                 else:
                     b["ncand_h"].copy_(b["ncand"])
                 self._nov = (slot, nvals, ev)
+        # every rank's (candidates, entries): the sparse form's counts now, the
+        # agreed form two batches on
+        if form is None:
+            b["ncand"].zero_()
+        b["cnt"][:1].copy_(b["ncand"])
+        b["cnt"][1] = nvals
+        c.all_gather_equal(b["cnts"], b["cnt"])
+        if b["cnts"].is_cuda:
+            b["cnts_h"].copy_(b["cnts"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            b["cnts_h"].copy_(b["cnts"])
+            ev = None
+        self.counted = (self.counted + [(slot, ev)])[-2:]
+        pend["slot"] = slot
+        if xform == "sparse":
+            # 2. the candidate lists of every rank (padded to the longest)
+            counts = b["cnts"].view(-1, 2)[:, 0].tolist()  # (waits for step 1 and the counts)
+            m = max(counts)
+            cand = self._buf(("cand", slot), m)
+            st.prefix_cands(cand, m, slot)
+            allc = self._buf(("allc", slot), G * m)
+            if m:
+                c.all_gather_equal(allc[: G * m], cand[:m])
+            pend["sparse"] = (allc, counts, m)
+            pend["got_p"] = pend["got_t"] = _Done()
+            pend["last"] = {"nrec_total": nrec_total, "exchange": "sparse", "form": "pairs",
+                            "exchange_bytes": (4 * m + 16) * (G - 1), "candidates": counts}
+            return pend
+        if c.rank > 0:
+            b["pclean"] = False  # (the dense prefix lands in P)
         # 2. exclusive prefix and total over the ranks (slice by slice, or
         # whole bitmaps in gather mode)
         if self.gather:
@@ -500,15 +592,36 @@ class PrefixTriage:
                 pend["side_done"].record(self.side)
         else:
             exchange(st)
-        pend["slot"] = slot
         xb = 4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))
-        pend["last"] = {"nrec_total": nrec_total, "exchange_bytes": xb,
+        pend["last"] = {"nrec_total": nrec_total, "exchange": "dense", "exchange_bytes": xb + 16 * (G - 1),
                         "form": {0: "kept", 1: "pairs", None: "default"}[form]}
         return pend
 
     def finish(self, pend):
         """Steps 3-4 of a started batch; returns the batch's record count."""
         st = self.st
+        if "sparse" in pend:
+            b, slot = self.slots[pend["slot"]], pend["slot"]
+            maxsig, newsig = pend["maxsig"], pend["newsig"]
+            allc, counts, m = pend["sparse"]
+            k = self.comm.rank
+            # 3. the flags against M0 | P_k, P_k set from the lists of the ranks before this one
+            P = None
+            if k > 0:
+                if not b["pclean"]:
+                    st.clear(b["pset"])
+                    b["pclean"] = True
+                for j in range(k):
+                    st.add(b["pset"], allc[j * m:], counts[j])
+                P = b["P"]
+            st.prefix_flags(maxsig, P, pend["rec_new"], slot)
+            # 4. every list into the replicated sets (newSignal: what maxSignal lacked)
+            for j in range(len(counts)):
+                st.add_new(newsig, maxsig, allc[j * m:], counts[j])
+            for j in range(k):  # (P back to zero)
+                st.delete(b["pset"], allc[j * m:], counts[j])
+            self.last = pend["last"]
+            return pend["nrec_total"]
         if "slot" in pend:
             b, slot = self.slots[pend["slot"]], pend["slot"]
             maxsig, newsig = pend["maxsig"], pend["newsig"]

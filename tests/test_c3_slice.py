@@ -14,7 +14,9 @@ rank 0's records then rank 1's:
     all-gather, so start() / finish() -- sg_prefix_begin_dev over the whole
     slice (two record slices of <= 2^30 entries kept in a slot),
     sg_bitmap_prefix_or_dev, sg_prefix_end_dev against M0 | P_1 with a
-    non-empty prefix, the set updates -- run at full size;
+    non-empty prefix, the set updates -- run at full size; then again with
+    the sparse exchange (rank 0's candidate list handed in: the pairs form,
+    sg_prefix_cands_dev, P_1 set from the list, sg_set_add_new_dev);
   * the pair protocol's stages (sg_shard_candidates_dev over each slice,
     sg_shard_owners_dev per shard over the pairs routed to it,
     sg_shard_flags_dev), the routing done here.
@@ -46,13 +48,16 @@ def _signal(call, ctx, trace, nprog):
 
 
 class _RankOneOfTwo:
-    """Comm of rank 1 in a 2-rank group whose only collective (gather mode's
-    all-gather of the C bitmaps) returns rank 0's C_0 beside this rank's."""
+    """Comm of rank 1 in a 2-rank group whose collectives return rank 0's part
+    beside this rank's: gather mode's all-gather of the C bitmaps (C_0), the
+    all-gather of the (candidates, entries) counts, and the sparse exchange's
+    all-gather of the candidate lists (cands0: rank 0's, sorted; None: rank 0
+    reports as many candidates as entries, which keeps the exchange dense)."""
 
     world, rank, host, local = 2, 1, False, False
 
-    def __init__(self, c0):
-        self.c0 = c0
+    def __init__(self, c0, nv0, cands0=None):
+        self.c0, self.nv0, self.cands0 = c0, nv0, cands0
 
     def start_all_gather_equal(self, out, t):
         from syzkaller_amd.shard import _Done
@@ -61,6 +66,17 @@ class _RankOneOfTwo:
         out[:w].copy_(self.c0)
         out[w:2 * w].copy_(t)
         return _Done()
+
+    def all_gather_equal(self, out, t):
+        w = t.numel()
+        if t.dtype == torch.int64:  # the counts
+            n0 = self.nv0 if self.cands0 is None else self.cands0.numel()
+            out[:2].copy_(torch.tensor([n0, self.nv0], dtype=torch.int64, device=out.device))
+        else:  # a candidate list, padded to the longest
+            out[:w].zero_()
+            out[: self.cands0.numel()].copy_(self.cands0)
+        out[w:2 * w].copy_(t)
+        return out
 
 
 @pytest.mark.timeout(900)
@@ -107,16 +123,27 @@ def test_c3_rank_slice_prefix_and_pairs_vs_oracle(ctx):
     st.add(s_m0, m0_dev, m0.size)
     c0 = all0 & ~m0w
     assert int(torch.count_nonzero(c0)) > 0  # a non-empty prefix
-    ms, ns = st.new_set(), st.new_set()
-    st.add(ms, m0_dev, m0.size)
-    tri = PrefixTriage(st, _RankOneOfTwo(c0), gather=True)
-    rec_new = torch.zeros(nrec1, dtype=torch.uint8, device="cuda")
-    assert tri.step(ms, ns, sig1, off1, nv1, nrec1, nrec0, rec_new, nrec_total=nrec0 + nrec1) == nrec0 + nrec1
-    torch.cuda.synchronize()
-    assert np.array_equal(rec_new.cpu().numpy(), ef1)
-    assert np.array_equal(ms.export(), em)
-    assert np.array_equal(ns.export(), en)
-    del tri, rec_new, c0, all0, m0w, s_all0, s_m0, ms, ns
+    # rank 0's candidate list (its signal not in M0, once each) for the sparse exchange
+    sv = sig0.to(torch.int64) & 0xFFFFFFFF
+    pos = ((sv & 0x00FFFF00) << 8) | ((sv >> 16) & 0xFF00) | (sv & 0xFF)  # sgd::set_pos
+    inm0 = (m0w.to(torch.int64)[pos >> 5] >> (sv & 31)) & 1
+    cands0 = torch.unique(sv[inm0 == 0]).to(torch.int32)
+    del sv, pos, inm0
+    assert 0 < cands0.numel() < nv0 // 20  # the steady state's few candidates
+    for exchange in ("dense", "sparse"):  # bitmaps (C_0 gathered), then candidate lists
+        ms, ns = st.new_set(), st.new_set()
+        st.add(ms, m0_dev, m0.size)
+        comm = _RankOneOfTwo(c0, nv0, cands0 if exchange == "sparse" else None)
+        tri = PrefixTriage(st, comm, gather=True, exchange=exchange)
+        rec_new = torch.zeros(nrec1, dtype=torch.uint8, device="cuda")
+        assert tri.step(ms, ns, sig1, off1, nv1, nrec1, nrec0, rec_new, nrec_total=nrec0 + nrec1) == nrec0 + nrec1
+        torch.cuda.synchronize()
+        assert tri.last["exchange"] == exchange
+        assert np.array_equal(rec_new.cpu().numpy(), ef1), exchange
+        assert np.array_equal(ms.export(), em), exchange
+        assert np.array_equal(ns.export(), en), exchange
+        del tri, rec_new, ms, ns
+    del c0, all0, m0w, s_all0, s_m0, cands0
     torch.cuda.empty_cache()
 
     # --- the pair protocol's stages over the two slices, G = 2 --------------

@@ -89,6 +89,28 @@ class NumpyPrefixStages:
             newset.w |= w & ~s.w
         s.w |= w
 
+    def add(self, sset, vals, n):
+        if n:
+            sset.add(vals[:n].numpy().view(np.uint32))
+
+    def add_new(self, newset, sset, vals, n):
+        """sset |= vals[:n]; newset gains those sset lacked (sg_set_add_new_dev)."""
+        if n:
+            v = vals[:n].numpy().view(np.uint32)
+            if newset is not None:
+                newset.add(v[~sset.has(v)])
+            sset.add(v)
+
+    def delete(self, sset, vals, n):
+        if n:
+            v = vals[:n].numpy().view(np.uint32).astype(np.uint64)
+            np.bitwise_and.at(sset.w, v >> np.uint64(5), ~(np.uint32(1) << (v & np.uint64(31)).astype(np.uint32)))
+
+    def prefix_cands(self, out, cap, slot=0):
+        """The slot's batch signal not in base, once each (sg_prefix_cands_dev)."""
+        m = np.array(self.kept[slot][4].export(), np.uint32)[:cap]
+        out.numpy().view(np.uint32)[: m.size] = m
+
     def prefix_begin(self, base, marks, vals, off, nvals, nrec, slot=0, form=None, ncand=None):
         v = vals[:nvals].numpy().view(np.uint32)
         marks.w[:] = 0  # (marks = the batch's signal not in base)
@@ -145,14 +167,17 @@ M0 = np.arange(0, 3000, 5, dtype=np.uint32)
 BATCHES = [(21, 700), (22, 1), (23, 900), (24, 0), (25, 600)]
 
 
-def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.05):
+def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.05, exchange="auto", sparse_below=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from syzkaller_amd.shard import Comm, PrefixTriage
 
         stages = NumpyPrefixStages()
-        tri = PrefixTriage(stages, Comm(), device="cpu", gather=gather, pairs_below=pairs_below)
+        tri = PrefixTriage(stages, Comm(), device="cpu", gather=gather, pairs_below=pairs_below, exchange=exchange,
+                           sparse_below=sparse_below)
+        xforms = []  # each started batch's exchange form
+        xbytes = []
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
@@ -160,6 +185,8 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
         pend = None
 
         def finish(pd):
+            xforms.append(pd[0]["last"]["exchange"])
+            xbytes.append(pd[0]["last"]["exchange_bytes"])
             assert tri.finish(pd[0]) == pd[1]
             if drain:
                 drained.append(ns.export())
@@ -175,6 +202,8 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
             out.append((r0, r1, rec_new))
             if not pipelined:
                 assert tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new) == nrec
+                xforms.append(tri.last["exchange"])
+                xbytes.append(tri.last["exchange_bytes"])
                 continue
             # the next batch started (marked against the maxSignal that still
             # lacks this batch's total) before the previous one is finished
@@ -185,7 +214,7 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
         if pend is not None:
             finish(pend)
         q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(),
-               drained if drain else ns.export(), stages.forms))
+               drained if drain else ns.export(), stages.forms, xforms, xbytes))
     finally:
         dist.destroy_process_group()
 
@@ -199,6 +228,10 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
                           (2, False, False, False, 2.0), (4, True, False, True, 2.0),
                           (2, True, True, False, -1.0)])
 def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain, pairs_below):
+    _run_and_check(world, pipelined, gather, drain, pairs_below, "auto", None, None)
+
+
+def _run_and_check(world, pipelined, gather, drain, pairs_below, exchange, sparse_below, expect_x):
     """drain: newSignal is read and cleared after every finish() while the next
     batch is already started -- each drained set must be exactly that batch's
     new signal (fuzzer.go:674: only what maxSignal lacked), not a re-report of
@@ -208,26 +241,40 @@ def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain, p
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather, drain, pairs_below))
-             for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, gather, drain, pairs_below, exchange,
+                                               sparse_below)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
+    xall = []
     for _ in range(world):
-        r, out, m, n, forms = q.get(timeout=240)
+        r, out, m, n, forms, xforms, xbytes = q.get(timeout=240)
+        if expect_x is None:  # (the default sparse_below, 0.05, is below the novelty here)
+            assert set(xforms) == {"dense"}, xforms
+        else:
+            if expect_x == "any":
+                xall.append(xforms)
+            else:
+                assert xforms == expect_x, xforms
+            for f, b in zip(xforms, xbytes):  # a list of candidates against whole bitmaps
+                assert (b < 4 * (1 << 20)) if f == "sparse" else (b >= (1 << 15)), (f, b)
         res[r] = (out, m, n)
         # the form of each batch from the novelty of the last counted one: kept
         # first (no count yet); pairs_below 2.0 (above any novelty): pairs after
-        assert forms[0] == 0, forms
-        if pairs_below > 1.0:  # kept until a non-empty batch has been counted, pairs after
+        if expect_x is not None:  # the sparse exchange takes the pairs form
+            assert all(f == 1 for f, x in zip(forms, expect_x) if x == "sparse"), forms
+        elif pairs_below > 1.0:  # kept until a non-empty batch has been counted, pairs after
             assert forms[-1] == 1 and forms == sorted(forms), forms
         elif pairs_below < 0:
             assert set(forms) == {0}, forms
+        if expect_x is None or expect_x[0] == "dense":
+            assert forms[0] == 0, forms
         else:  # by each rank's novelty (later batches overlap the earlier ones' signal)
             assert set(forms) <= {0, 1}, forms
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert all(x == xall[0] for x in xall), xall  # every rank took the same forms
     om, on = O.OSet(M0), O.OSet()
     per_batch_new = []
     for b, (seed, nrec) in enumerate(BATCHES):
@@ -249,3 +296,23 @@ def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain, p
             assert res[r][2] == per_batch_new
         else:
             assert res[r][2] == on.export().tolist()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,pipelined,gather,drain,exchange,sparse_below,expect",
+                         [(2, False, True, False, "auto", 2.0, ["dense", "dense", "sparse", "sparse", "sparse"]),
+                          (4, True, False, True, "auto", 2.0, ["dense", "dense", "sparse", "sparse", "sparse"]),
+                          (4, False, False, False, "sparse", None, ["sparse"] * 5),
+                          (2, True, True, True, "sparse", None, ["sparse"] * 5),
+                          (4, True, True, False, "auto", 0.2, None)])
+def test_prefix_sparse_exchange_equals_sequential_loop(world, pipelined, gather, drain, exchange, sparse_below, expect):
+    """The candidate-list exchange: forced from the first
+    batch, and mixed with the bitmap exchange within one run (the form agreed
+    from the counts two batches back; sparse_below 2.0 is above any novelty,
+    0.2 lets the batches decide), pipelined or not, in gather and all-to-all
+    mode, with newSignal drained between batches.  Flags and both sets equal
+    the sequential loop's; the sparse steps move a few KB per rank."""
+    if expect is None:  # the forms depend on the batches: any mix, the same on every rank
+        _run_and_check(world, pipelined, gather, drain, 0.05, exchange, sparse_below, "any")
+    else:
+        _run_and_check(world, pipelined, gather, drain, 0.05, exchange, sparse_below, expect)

@@ -24,6 +24,23 @@ def test_uvarint_matches_go_encoding():
             O.delta_decode(bad)
 
 
+def test_delta_encode_batch_matches_per_list_oracle():
+    """The vectorised batch encoder (the f4 row's full-payload check) gives the
+    per-list oracle's bytes: empty lists, value 0 and 0xFFFFFFFF, repeats
+    (delta 0), deltas at every varint length boundary."""
+    rng = np.random.default_rng(43)
+    lists = [np.zeros(0, np.uint32), np.array([0], np.uint32), np.array([0xFFFFFFFF], np.uint32),
+             np.array([5, 5, 5], np.uint32), np.cumsum([127, 1, 16383, 1, 2097151, 1, 268435455, 1]).astype(np.uint32)]
+    for _ in range(300):
+        v = np.sort(rng.integers(0, 1 << 32, size=int(rng.integers(0, 60)), dtype=np.uint64)).astype(np.uint32)
+        lists.append(v if rng.random() < 0.5 else np.unique(v))
+    vals = np.concatenate(lists).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum([x.size for x in lists])]).astype(np.uint64)
+    b, bo = O.delta_encode_batch(vals, off)
+    for k, x in enumerate(lists):
+        assert b[int(bo[k]):int(bo[k + 1])].tobytes() == O.delta_encode(x), k
+
+
 def test_sancov_layout():
     b = O.sancov([0x81000010, 5])
     assert b[:8] == bytes.fromhex("64ffffffffffbfc0")

@@ -215,6 +215,9 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=
 
     ctx = C.Context(ctx_dev)
     side_ctx = None
+    exchange = "auto"
+    if proto.endswith("_sparse"):  # the candidate-list exchange from the first batch on
+        proto, exchange = proto[: -len("_sparse")], "sparse"
     if proto == "prefix_pipelined":
         # the PrefixTriage the bench runs at N > 1: batches overlapped through
         # the two slots, the prefix-OR on a side stream (here also at one rank;
@@ -224,9 +227,10 @@ def _run_protocol(ctx_dev, world, rank, batches, m0, proto="pairs", collectives=
         with torch.cuda.stream(side):
             side_st = HipStages(side_ctx)
         tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=True, side_stages=side_st,
-                           side_stream=side, gather=False, form=form)
+                           side_stream=side, gather=False, form=form, exchange=exchange)
     elif proto == "prefix":
-        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives), two_phase_at_one=collectives, form=form)
+        tri = PrefixTriage(HipStages(ctx), Comm(collectives=collectives),
+                           two_phase_at_one=collectives or exchange == "sparse", form=form, exchange=exchange)
     else:
         tri = ShardedTriage(HipStages(ctx), Comm(collectives=collectives))
     ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
@@ -273,7 +277,8 @@ def _expected():
 
 
 @pytest.mark.parametrize("proto,form", [("pairs", "auto"), ("prefix", "auto"), ("prefix_pipelined", "auto"),
-                                        ("prefix_pipelined", "pairs"), ("prefix_pipelined", "kept")])
+                                        ("prefix_pipelined", "pairs"), ("prefix_pipelined", "kept"),
+                                        ("prefix_sparse", "auto"), ("prefix_pipelined_sparse", "auto")])
 def test_sharded_protocol_one_rank_vs_oracle(ctx, proto, form):
     """form: PrefixTriage's per-batch step-1 form (auto by the last counted
     batch's novelty, or forced) -- the same flags and sets whichever runs."""
@@ -310,7 +315,7 @@ def _worker(rank, world, port, q, proto, backend="gloo"):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
+@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined", "prefix_sparse", "prefix_pipelined_sparse"])
 def test_sharded_protocol_two_ranks_one_gpu(proto):
     import torch.multiprocessing as mp
 
@@ -340,7 +345,7 @@ def test_sharded_protocol_two_ranks_one_gpu(proto):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined"])
+@pytest.mark.parametrize("proto", ["pairs", "prefix", "prefix_pipelined", "prefix_sparse"])
 def test_sharded_protocol_rccl_one_rank(proto):
     """The RCCL branch of Comm (syzkaller_amd/shard.py): a one-rank "nccl"
     group with the collectives forced on, so the device-tensor
