@@ -126,7 +126,8 @@ POP_SEED = 0x9091A7E5
 
 # kernels of one partitioned triage step (sg_bucket.hip), for the per-kernel table
 STEP_KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan"]
-OTHER_KERNELS = ["triage_claim", "triage_resolve", "emit", "shard_local", "shard_route", "shard_owner",
+ORDERED_KERNELS = ["owned_sort", "owned_sweep", "emit"]
+OTHER_KERNELS = ["emit", "shard_local", "shard_route", "shard_owner",
                  "shard_resolve", "shard_flags", "set_add"]
 
 
@@ -183,7 +184,7 @@ class Gen:
 def triage(ctx, maxsig, newsig, b, rec_new, diff_vals=None, diff_off=None, rec0=0, rec1=None, e0=0, e1=None):
     """fuzzer.go:645-693 over one batch (or records [rec0, rec1) of it).
     Without diff buffers: the partitioned path (flags + set updates); with:
-    the claim/resolve path, which also emits the ordered diff lists."""
+    the ordered-output path, which also emits the diff lists (fuzzer.go:669)."""
     if rec1 is None:
         rec1, e1 = b.nrec, b.nvals
         vals, off = b.vals, b.off
@@ -382,7 +383,7 @@ def cpu_baseline(m0_values, batch, calls, gpu_flags, budget_s, threads, threads_
 
 def account(ctx, maxsig, m0set, newsig, batches, calls, rec_new, diff_vals, diff_off):
     """Outside the timed region: replay the timed steps from the same state,
-    on the claim/resolve path (so the diff element count is known), with the
+    on the ordered-output path (so the diff element count is known), with the
     candidate and program-distinct counts measured."""
     tot = dict(n_in=0, n_uniq=0, n_cand=0, n_diff=0, n_rec=0, n_new_signal=0, n_queued=0)
     flags_eq = True
@@ -408,7 +409,7 @@ def account(ctx, maxsig, m0set, newsig, batches, calls, rec_new, diff_vals, diff
     L = len(batches)
     per = {k: v / L for k, v in tot.items()}
     per["queued_frac"] = tot["n_queued"] / tot["n_rec"] if tot["n_rec"] else None
-    per["paths_agree"] = flags_eq  # partitioned flags == claim/resolve flags on every timed batch
+    per["paths_agree"] = flags_eq  # flags-only path == ordered-output path's flags on every timed batch
     return per
 
 
@@ -489,6 +490,42 @@ def timed_steps_pipelined(ctx, m0set, newsig, batches, flags0):
             "state_sizes_after": sorted(counts)}
 
 
+def timed_ordered(ctx, maxsig, m0set, newsig, batches, rec_new, diff_vals, diff_off, flags_ms):
+    """The C2 step with the ordered outputs (the per-record diff CSR of
+    fuzzer.go:669 besides flags and set updates, sg_triage.hip
+    owned_outputs), timed like timed_steps over the same batches from the
+    same state, one untimed step first (its workspace)."""
+    call("sg_set_copy", maxsig.h, m0set.h)
+    triage(ctx, maxsig, newsig, batches[0], rec_new, diff_vals, diff_off)
+    states = [maxsig] + [SignalSet(ctx) for _ in batches[1:]]
+    for st in states:
+        call("sg_set_copy", st.h, m0set.h)
+    torch.cuda.synchronize()
+    ctx.timing(True)
+    tm = StepTimer()
+    call("sg_ctx_marker", ctx.h, 0, 6)
+    t0 = time.perf_counter()
+    for st, b in zip(states, batches):
+        tm.mark()
+        triage(ctx, st, newsig, b, rec_new, diff_vals, diff_off)
+        tm.mark()
+    call("sg_ctx_marker", ctx.h, 1, 6)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernels = kernel_table(ctx, STEP_KERNELS + ORDERED_KERNELS, len(batches))
+    ctx.timing(False)
+    tri = [tm.ev[i].elapsed_time(tm.ev[i + 1]) for i in range(0, len(tm.ev), 2)]
+    for st in states[1:]:
+        st.close()
+    ms = float(np.mean(tri))
+    return {"ms_per_step": round(ms, 4), "wall_ms_per_step": round(wall * 1e3 / len(batches), 4),
+            "over_flags": round(ms / flags_ms, 3), "diff_elements_last_step": int(diff_off[batches[-1].nrec].item()),
+            "kernels": kernels,
+            "how": "sg_triage_batch_dev with diff_vals/diff_off: partition + update-emitting bucket stage (each new "
+                   "signal with its first record), pairs radix-sorted by record, one wave per record sweeping S_r "
+                   "against its owned signals into ballot masks, ordered compaction"}
+
+
 def kernel_table(ctx, names, steps):
     out = {}
     for name in names:
@@ -546,6 +583,9 @@ def run_c2(ctx, args, cfg, rank):
         diff_vals = torch.empty(maxnvals, dtype=torch.int32, device="cuda")
         diff_off = torch.empty(maxnrec + 1, dtype=torch.int64, device="cuda")
         res["acct"] = account(ctx, maxsig, m0set, newsig, timed, calls, rec_new, diff_vals, diff_off)
+        if args.ordered:
+            res["ordered"] = timed_ordered(ctx, maxsig, m0set, newsig, timed, rec_new, diff_vals, diff_off,
+                                           float(np.mean(tri)))
         del diff_vals, diff_off
     if not args.no_cpu:
         m0_values = m0set.export()
@@ -869,6 +909,8 @@ def main():
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host entry point leg (C2 batch from pageable host memory)")
     ap.add_argument("--no-account", action="store_true", help="skip the byte-accounting replay")
+    ap.add_argument("--no-ordered", dest="ordered", action="store_false",
+                    help="skip the timed C2 step with the ordered diff outputs (needs the accounting replay)")
     ap.add_argument("--pipeline", action="store_true",
                     help="C2: also time the two-stage pipelined loop (syzkaller_amd/pipeline.py)")
     args = ap.parse_args()
@@ -942,6 +984,7 @@ def main():
                        "wall_ms_per_step": ms_step},
             "kernels": r["kernels"],
             "accounting": acct,
+            "ordered_outputs": r.get("ordered"),
             "steady_state": r.get("steady"),
             "from_traces": r.get("from_traces"),
             "host_api": r.get("host_api"),

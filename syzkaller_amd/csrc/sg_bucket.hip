@@ -900,7 +900,10 @@ struct BucketArgs {
   uint32_t rec_base;
   uint32_t nshards;         // pairs are counted per owning shard (shard_of) ...
   unsigned long long* shard_cnt;  // ... when this is given
-};
+  uint32_t update;          // emitting form that also updates mwords / nwords (the ordered outputs) ...
+  unsigned long long* gcur; // ... with the pairs group-major: pairs of group g's records appended at
+  const uint64_t* goff;     //     goff[g << 16] + gcur[g] (goff: the launch's record offsets; a group's
+};                          //     pairs never outnumber its entries)
 
 // Owning shard of a signal in the hash-sharded multi-GPU triage: the murmur3
 // finaliser of s, scaled to [0, nshards).
@@ -955,6 +958,36 @@ __device__ __forceinline__ void emit_pairs(const BucketArgs& a, const uint32_t (
       if (a.shard_cnt) atomicAdd(&shcnt[shard_of(sig[k], a.nshards)], 1u);
     }
   __syncthreads();  // ewc / ebase are rewritten by the next call
+}
+
+// Group-major append (the ordered outputs): up to kPer pairs per thread
+// (valid where rec != kEmpty), counted per record group in LDS, one global
+// cursor atomic per group and call, then placed.  Order within a group is
+// free: the pairs are sorted by record afterwards.  lcnt (LDS, kMaxGroups
+// words) is zero on entry and on exit.  Called by every thread.
+template <int kPer>
+__device__ __forceinline__ void emit_grouped(const BucketArgs& a, const uint32_t (&sig)[kPer], const uint32_t (&rec)[kPer],
+                                             uint32_t* lcnt, unsigned long long* lbase) {
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (rec[k] != kNone) atomicAdd(&lcnt[rec[k] >> kGroupBits], 1u);
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < a.NG; g += blockDim.x) {
+    const uint32_t c = lcnt[g];
+    lbase[g] = c ? a.goff[(uint64_t)g << kGroupBits] + atomicAdd(&a.gcur[g], (unsigned long long)c) : 0ull;
+    lcnt[g] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (rec[k] != kNone) {
+      const uint32_t g = rec[k] >> kGroupBits;
+      a.pairs[lbase[g] + atomicAdd(&lcnt[g], 1u)] = make_uint2(sig[k], rec[k]);
+    }
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < a.NG; g += blockDim.x) lcnt[g] = 0;
+  __syncthreads();
 }
 
 __device__ __forceinline__ void flush_shard_counts(const BucketArgs& a, const uint32_t* shcnt) {
@@ -1164,9 +1197,13 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
   __shared__ uint32_t sh_b[2];
   __shared__ uint4 sh_q[2];
   __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];  // emitted pairs per owning shard
+  __shared__ uint32_t lcnt[kEmit ? kMaxGroups : 1];   // group-major emission: pairs per record group ...
+  __shared__ unsigned long long lbase[kEmit ? kMaxGroups : 1];  // ... and where they go
   const int tid = threadIdx.x;
-  if (kEmit)
+  if (kEmit) {
     for (uint32_t i = tid; i < kMaxShards; i += kBThreads) shcnt[i] = 0;
+    for (uint32_t i = tid; i < kMaxGroups; i += kBThreads) lcnt[i] = 0;
+  }
   const uint32_t NG = a.NG;
   constexpr uint32_t kRound = kBThreads * kBU;
   // diagnostics (kDbg): block span, buckets, rounds, cycles per phase as wave 0 sees them
@@ -1392,6 +1429,35 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
+    } else if (kEmit && a.gcur) {
+      // the ordered outputs: every new signal with its first record, group-major
+      constexpr int kOwn = kHash / kBThreads;
+      uint32_t sg[kOwn], rc[kOwn];
+#pragma unroll
+      for (int k = 0; k < kOwn; k++) {
+        const uint32_t i = k * kBThreads + tid;
+        const uint32_t v = ht[i];
+        rc[k] = kEmpty;
+        sg[k] = 0;
+        if (v != kEmpty) {
+          const uint32_t sl = map_signal(i, v);
+          sg[k] = part_sig((b << 16) | sl);
+          rc[k] = v & kRecMask;
+          atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+          ht[i] = kEmpty;
+        }
+      }
+      emit_grouped(a, sg, rc, lcnt, lbase);  // (its barriers also complete nbits)
+      const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
+      const wvec mw = reinterpret_cast<const wvec*>(mslice)[tid];
+      const uint64_t w0 = bucket_word(b, kWPT * tid);
+#pragma unroll
+      for (int j = 0; j < kWPT; j++)
+        if (nb[j]) {
+          a.mwords[w0 + j] = mw[j] | nb[j];
+          if (a.nwords) a.nwords[w0 + j] = ns[j] | nb[j];
+        }
+      reinterpret_cast<wvec*>(nbits)[tid] = wvec{};
     } else if (kEmit) {
       // every distinct candidate of the bucket with its first record: the
       // thread's occupied slots counted, one block scan and one global
@@ -1430,13 +1496,23 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
             const uint32_t sg = part_sig((b << 16) | sl);
             a.pairs[pos++] = make_uint2(sg, a.rec_base + (v & kRecMask));
             if (a.shard_cnt) atomicAdd(&shcnt[shard_of(sg, a.nshards)], 1u);
-            if (a.nwords) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+            if (a.nwords || a.update) atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
             ht[i] = kEmpty;
           }
         }
       }
       __syncthreads();  // nbits complete; ewc / ebase free for the next bucket
-      if (a.nwords) {  // the candidates' bits: words kWPT tid .., written by this block alone
+      if (a.update) {  // the candidates are the new signals: words kWPT tid .., this block their only writer
+        const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
+        const wvec mw = reinterpret_cast<const wvec*>(mslice)[tid];
+        const uint64_t w0 = bucket_word(b, kWPT * tid);
+#pragma unroll
+        for (int j = 0; j < kWPT; j++)
+          if (nb[j]) {
+            a.mwords[w0 + j] = mw[j] | nb[j];
+            if (a.nwords) a.nwords[w0 + j] = ns[j] | nb[j];
+          }
+      } else if (a.nwords) {  // the candidates' bits: words kWPT tid .., written by this block alone
         const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
         uint32_t* ng = a.nwords + bucket_word(b, kWPT * tid);
 #pragma unroll
@@ -1533,10 +1609,13 @@ __global__ __launch_bounds__(kDThreads) void k_bucket_direct(BucketArgs a) {
   __shared__ uint32_t nbits[kQW];
   __shared__ uint32_t gb[kMaxGroups];
   __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];
+  __shared__ uint32_t lcnt[kEmit ? kMaxGroups : 1];
+  __shared__ unsigned long long lbase[kEmit ? kMaxGroups : 1];
   const int tid = threadIdx.x;
   const uint32_t nsp = *a.nspill, NG = a.NG;
   if (kEmit) {
     for (uint32_t i = tid; i < kMaxShards; i += kDThreads) shcnt[i] = 0;
+    for (uint32_t i = tid; i < kMaxGroups; i += kDThreads) lcnt[i] = 0;
     __syncthreads();
   }
   for (uint32_t job = blockIdx.x; job < nsp * kNQ; job += gridDim.x) {
@@ -1567,10 +1646,17 @@ __global__ __launch_bounds__(kDThreads) void k_bucket_direct(BucketArgs a) {
         sig[k] = part_sig((b << 16) | (qq * kQ + i));
         rec[k] = owner[i];
       }
-      emit_pairs(a, sig, rec, shcnt);
-      if (a.nwords)
-        for (uint32_t i = tid; i < kQW; i += kDThreads)
-          if (nbits[i]) a.nwords[bucket_word(b, qq * kQW + i)] |= nbits[i];
+      if (a.gcur)
+        emit_grouped(a, sig, rec, lcnt, lbase);
+      else
+        emit_pairs(a, sig, rec, shcnt);
+      for (uint32_t i = tid; i < kQW; i += kDThreads) {
+        const uint32_t nb = nbits[i];
+        if (!nb) continue;
+        const uint64_t w = bucket_word(b, qq * kQW + i);
+        if (a.update) a.mwords[w] = mpart[i] | nb;
+        if (a.nwords) a.nwords[w] |= nb;
+      }
     } else {
       for (uint32_t i = tid; i < kQ; i += kDThreads)
         if (owner[i] != kEmpty) a.rec_new[owner[i]] = 1;
@@ -1791,7 +1877,7 @@ static_assert(kMaxLaunchRecords == (uint64_t)kMaxGroups * kGroupRecs, "records p
 
 // Grid of a persistent kernel: every block resident at once (CUs x blocks
 // per CU from the occupancy query), cached per kernel.
-static uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
+uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
   static std::mutex mu;
   static std::map<std::pair<int, const void*>, uint32_t> cache;
   std::lock_guard<std::mutex> lock(mu);
@@ -1969,6 +2055,9 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
     ba.rec_base = emit->rec_base;
     ba.nshards = emit->nshards;
     ba.shard_cnt = emit->shard_cnt;
+    ba.update = emit->update ? 1u : 0u;
+    ba.gcur = emit->gcur;
+    ba.goff = emit->goff;
   }
   uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, false>, kBThreads);
   // diagnostics: SG_BUCKET_BLOCKS caps the persistent grid (leaves CUs to
@@ -2191,6 +2280,12 @@ __global__ void k_rebase(const uint64_t* __restrict__ off, uint64_t n, uint64_t 
   if (i < n) out[i] = off[i] - base;
 }
 
+int rebase_offsets(sg_ctx* ctx, const uint64_t* d_off, uint64_t n, uint64_t base, uint64_t* d_out) {
+  hipLaunchKernelGGL(k_rebase, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_off, n, base, d_out);
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
 // Flags-only triage of a device-resident batch (ctx lock held).  Batches of
 // more than ctx->max_launch_recs records run as consecutive record slices:
 // the sequential loop (fuzzer.go:665) cut between two records sees the same
@@ -2346,7 +2441,8 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     uint64_t* roff = ctx->slice_off + at;
     at += nr + 1;
     if (x.e1 == x.e0) continue;  // records without entries (flags cleared above)
-    hipLaunchKernelGGL(k_rebase, dim3(div_up(nr + 1, 256)), dim3(256), 0, ctx->stream, d_off + x.r0, nr + 1, x.e0, roff);
+    rc = rebase_offsets(ctx, d_off + x.r0, nr + 1, x.e0, roff);
+    if (rc) return rc;
     rc = bucket_triage_one(ctx, mwords, nwords, d_vals + x.e0, roff, x.e1 - x.e0, nr, d_rec_new + x.r0, nullptr, 0,
                            trace);
     if (rc) return rc;
@@ -2631,6 +2727,20 @@ int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, con
   }
   return bucket_triage_one(ctx, const_cast<uint32_t*>(mwords), nullptr, d_vals, d_off, n, nrec, nullptr, &emit,
                            ws_base);
+}
+
+int bucket_emit_update(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                       uint64_t n, uint64_t nrec, uint2* pairs, unsigned long long* gcur, size_t ws_base) {
+  if (nrec > kMaxLaunchRecords || n >= 0xFFFFFFFFull - 2 * kPT) {
+    set_error("bucket emit: a launch holds <= 2^24 records and < 2^32 - 2^15 entries");
+    return SG_EINVAL;
+  }
+  EmitArgs e{};
+  e.pairs = pairs;
+  e.update = true;
+  e.gcur = gcur;
+  e.goff = d_off;
+  return bucket_triage_one(ctx, mwords, nwords, d_vals, d_off, n, nrec, nullptr, &e, ws_base);
 }
 
 }  // namespace sg

@@ -31,9 +31,6 @@ namespace sg {
 int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint32_t* dout, const uint64_t* a_beg,
               const uint64_t* a_len, const uint64_t* b_beg, const uint64_t* b_len, const uint64_t* out_beg,
               size_t npair, uint64_t* out_len);
-size_t radix_sort_ws(uint64_t n);
-int radix_sort_u64(sg_ctx* ctx, uint64_t* a, uint64_t* b, uint64_t n, size_t ws_used, uint64_t** sorted,
-                   uint64_t vary = 0);
 
 namespace {
 

@@ -182,18 +182,6 @@ int set_export_dev(sg_set* set, uint32_t* d_out, uint64_t cap, uint64_t* total);
 // SignalAdd of device-resident values (sg_ctx.hip; ctx lock held, stream-ordered).
 int set_add_dev_locked(sg_set* set, const uint32_t* d_vals, uint64_t n);
 
-// Shared first-owner pipeline (sg_triage.hip).
-struct OwnerJob {
-  const uint32_t* vals;   // device
-  const uint64_t* off;    // device, nseg+1 (nullptr: every element is its own segment)
-  uint64_t nvals;
-  uint64_t nseg;
-  const uint32_t* filter; // set words consulted before claiming (nullptr: none)
-  const uint32_t* order_rank;  // device rank of each segment (nullptr: rank = segment index)
-};
-int owner_claim_resolve(sg_ctx* ctx, const OwnerJob& job, uint32_t key_lo, uint64_t* d_cmask, uint64_t* d_dmask,
-                        uint32_t* d_tile_rec, uint8_t* d_seg_flag, uint32_t* set_a, uint32_t* set_b);
-
 // A batch in host memory through pinned double-buffered staging, record
 // slice by record slice, each slice's copies overlapping the previous one's
 // partitioned triage (sg_host.hip); takes the ctx lock.
@@ -213,7 +201,14 @@ struct EmitArgs {
   uint32_t rec_base;
   uint32_t nshards;
   unsigned long long* shard_cnt;
+  bool update;  // also update the sets (their new bits = the emitted signals); no record flags
+  unsigned long long* gcur;  // update form: pairs group-major, group g's at goff[g << 16] + gcur[g]++
+  const uint64_t* goff;      //   (goff: the launch's record offsets)
 };
+// Workgroups of `kernel` resident on the whole device at once (cached per device).
+uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads);
+// d_out[i] = d_off[i] - base, i < n (a record slice's offsets rebased).
+int rebase_offsets(sg_ctx* ctx, const uint64_t* d_off, uint64_t n, uint64_t base, uint64_t* d_out);
 // Workspace bytes of one partitioned launch over n entries / nrec records.
 size_t bucket_plan_bytes(uint64_t n, uint64_t nrec);
 // A batch's record slices (<= max_launch_recs records, <= lim entries unless
@@ -234,6 +229,19 @@ int prefix_end(sg_ctx* ctx, uint32_t slot, uint32_t* mwords, const uint32_t* owo
 // at ws_base (reserved by the caller).
 int bucket_emit(sg_ctx* ctx, const uint32_t* mwords, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n,
                 uint64_t nrec, const EmitArgs& emit, size_t ws_base);
+// The ordered outputs' bucket stage (one launch, limits as bucket_emit):
+// mwords / nwords (nullable) gain the batch's new signals, and each new
+// signal is written once as {s, its first record} (records launch-relative),
+// group-major: the pairs of record group g (records g << 16 ..) at
+// pairs[d_off[g << 16] + i], i < gcur[g] (device, zeroed by the caller; a
+// group's new signals never outnumber its entries); no record flags.
+int bucket_emit_update(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals, const uint64_t* d_off,
+                       uint64_t n, uint64_t nrec, uint2* pairs, unsigned long long* gcur, size_t ws_base);
+constexpr uint32_t kRecGroupBits = 16;  // records per group of the partitioned path: 2^16
+// Workspace bytes beyond two key buffers of radix_sort_u64 (sg_sort.hip).
+size_t radix_sort_ws(uint64_t n);
+int radix_sort_u64(sg_ctx* ctx, uint64_t* a, uint64_t* b, uint64_t n, size_t ws_used, uint64_t** sorted,
+                   uint64_t vary = 0);
 
 }  // namespace sg
 

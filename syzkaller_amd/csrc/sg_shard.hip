@@ -316,17 +316,6 @@ __global__ __launch_bounds__(256) void k_prefix_or_rank4(const uint4* __restrict
   }
 }
 
-__global__ void k_rebase_off(const uint64_t* __restrict__ off, uint64_t n, uint64_t base, uint64_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = off[i] - base;
-}
-
-static int read_u64(sg_ctx* ctx, const uint64_t* d, uint64_t* h) {
-  SG_HIP(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  return SG_OK;
-}
-
 }  // namespace sg
 
 using namespace sg;
@@ -398,8 +387,8 @@ int sg_shard_candidates_dev(sg_ctx* ctx, sg_set* snapshot, const uint32_t* d_val
       uint64_t* roff = ctx->slice_off + at;
       at += r1 - r0 + 1;
       if (e1 == e0) continue;
-      hipLaunchKernelGGL(k_rebase_off, dim3(div_up(r1 - r0 + 1, 256)), dim3(256), 0, ctx->stream, d_rec_off + r0,
-                         r1 - r0 + 1, e0, roff);
+      rc = rebase_offsets(ctx, d_rec_off + r0, r1 - r0 + 1, e0, roff);
+      if (rc) return rc;
       EmitArgs e{tmp, npairs, (uint32_t)(rec_base + r0), nshards, cnt};
       rc = bucket_emit(ctx, snapshot->words, d_vals + e0, roff, e1 - e0, r1 - r0, e, o_plan);
       if (rc) return rc;

@@ -13,15 +13,12 @@
 //
 // Parallel form: owner(s) = min{key(item) : s ∈ item, s ∉ S0}.  Item k is
 // "new" iff some element s ∉ S0 has owner(s) == key(k); its diff is exactly
-// those elements, in item order with duplicates.  Two streaming kernels:
-//   claim   : probe the S0 bitmap per element; for s ∉ S0 atomicMin its key
-//             into the direct-indexed owner table (2^32 x u32, 16 GiB);
-//             record the candidates as per-chunk ballot masks.
-//   resolve : for candidates only, owner[s] == own key -> diff element; set
-//             the bits of the running sets, flag the item, ballot-mask it.
-// The ordered diff output is a stream compaction of the resolve masks.
-// Owner keys decrease from batch to batch (sg::owner_keys), so the table
-// never needs resetting between batches.
+// those elements, in item order with duplicates.  The triage-shaped loops
+// (A8 with its diff lists, A11, A12) take the owners from the partitioned
+// path's bucket stage (sg_bucket.hip) and emit the ordered lists from them
+// here (owned_outputs); Minimize keeps a direct-indexed owner table (2^32 x
+// u32, 16 GiB) whose keys decrease from call to call (sg::owner_keys), so it
+// never needs resetting.
 #include "sg_internal.h"
 
 #include <algorithm>
@@ -29,25 +26,6 @@
 #include <cstring>
 
 namespace sg {
-
-struct PipeArgs {
-  const uint32_t* vals;
-  uint64_t n;
-  const uint64_t* off;      // nseg+1 (null: element-level items)
-  uint64_t nseg;
-  const uint32_t* filter;   // S0 words (null: S0 = ∅)
-  const uint32_t* rank;     // rank of item (null: identity)
-  const uint32_t* tile_rec; // ntiles+1: item of the first element of each tile
-  uint32_t* owner;
-  uint32_t key_lo;
-  uint64_t* cmask;          // nchunks*4 candidate ballots
-  uint64_t* dmask;          // nchunks*4 diff ballots
-  uint32_t* dcnt;           // nchunks diff counts
-  uint8_t* seg_flag;        // nseg (nullable)
-  uint32_t* set_a;          // running sets updated with diff elements (nullable)
-  uint32_t* set_b;
-  int aligned;              // vals is 16-B aligned
-};
 
 __device__ __forceinline__ void load4(const uint32_t* __restrict__ v, uint64_t n, uint64_t e0, int aligned,
                                       uint32_t (&x)[4], uint32_t& okbits) {
@@ -69,30 +47,6 @@ __device__ __forceinline__ void load4(const uint32_t* __restrict__ v, uint64_t n
   }
 }
 
-// chunk c of tile t handled by wave w at step j (interleaved so the block's
-// loads at one step cover 4 KiB contiguously).
-__device__ __forceinline__ uint64_t chunk_of(uint64_t tile, int j, int wave) {
-  return tile * kChunksPerTile + (uint64_t)(j * 4 + wave);
-}
-
-// Item window of one tile kept in LDS.
-struct Win {
-  uint64_t r_a, r_b, wn;
-};
-
-__device__ __forceinline__ void win_setup(const PipeArgs& a, uint64_t tile, uint64_t* win, Win& w) {
-  w.r_a = a.tile_rec[tile];
-  w.r_b = a.tile_rec[tile + 1];
-  w.wn = w.r_b - w.r_a + 1;
-  if (w.wn <= (uint64_t)kWin)
-    for (uint64_t k = threadIdx.x; k < w.wn; k += blockDim.x) win[k] = a.off[w.r_a + k];
-}
-
-__device__ __forceinline__ uint64_t win_lookup(const PipeArgs& a, const uint64_t* win, const Win& w, uint64_t e) {
-  if (w.wn <= (uint64_t)kWin) return w.r_a + sgd::seg_search(win, 0, w.wn - 1, e);
-  return sgd::seg_search(a.off, w.r_a, w.r_b, e);
-}
-
 __device__ __forceinline__ void store_ballots(uint64_t* mask, uint64_t c, int lane, uint32_t bits4) {
   uint64_t b0 = __ballot(bits4 & 1u);
   uint64_t b1 = __ballot(bits4 & 2u);
@@ -102,110 +56,367 @@ __device__ __forceinline__ void store_ballots(uint64_t* mask, uint64_t c, int la
   if (lane < 4) mask[c * 4 + lane] = mine;
 }
 
-__global__ void k_tile_rec(const uint64_t* __restrict__ off, uint64_t nseg, uint64_t n, uint64_t ntiles,
-                           uint32_t* __restrict__ tile_rec) {
-  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > ntiles) return;
-  uint64_t e = t * kTile;
-  if (e >= n) e = n - 1;
-  tile_rec[t] = (uint32_t)sgd::seg_search(off, 0, nseg - 1, e);
+// ---- ordered outputs from the partitioned path ------------------------------
+// The bucket stage in its update-emitting form (sg_bucket.hip) writes every
+// new signal s of a record slice once, with its first record r, as the key
+// r << 32 | s; sorted by record (a stable LSD radix over the record bits),
+// record r's keys are O_r, the signals it owns.  Its diff is S_r's elements
+// that lie in O_r, in S_r order with duplicates (cover.go:169-176), or with
+// `dedup` only the first occurrence of each (the Poll merge's element loop,
+// manager.go:949-956).  One wave per record holds O_r as an LDS hash set and
+// sweeps S_r by 256-element chunks, lane l testing elements 4l .. 4l + 3, so
+// its four ballots are the chunk's words of the batch's diff mask; the ordered
+// compaction below (k_scatter, k_seg_offsets) turns the mask into the CSR.  A
+// record owning more than kOwnWave signals is listed for k_own_big (a
+// workgroup per record, O_r in pieces of kOwnBigCap).
+constexpr int kOwnWaves = 4;
+constexpr uint32_t kOwnSlots = 2048;          // hash slots per wave: 512 buckets of 4
+constexpr uint32_t kOwnWave = kOwnSlots / 4;  // the largest O_r of the wave path (load <= 1/4)
+constexpr int kOwnBigT = 1024;
+constexpr uint32_t kOwnBigSlots = 16384;
+constexpr uint32_t kOwnBigCap = kOwnBigSlots / 4;
+constexpr uint32_t kOwnEmpty = 0xFFFFFFFFu;  // an empty slot (the signal 0xFFFFFFFF is held by a flag)
+
+struct OwnArgs {
+  const uint32_t* vals;  // the batch (element e at vals[e])
+  const uint64_t* roff;  // the slice's record offsets, rebased: record r = elements e0 + roff[r] ..
+  uint64_t e0;
+  uint32_t nrec;         // records in the slice
+  const uint64_t* keys;  // r << 32 | s, sorted by record within each record group
+  const uint2* po;       // record r's keys are [po[r].x, po[r].y)
+  uint8_t* rec_new;      // the slice's record flags (nullable)
+  uint64_t* mask;        // the batch's diff ballots, zeroed: 4 words per chunk
+  uint32_t* big;         // [0]: count, then the records left for k_own_big
+  uint64_t n;            // elements in the batch (vals[0 .. n) readable)
+};
+
+// The set: 1 << bb buckets of four slots, a key in the first bucket from its
+// home with a free slot (a bucket's slots fill in order, so a lookup reads one
+// 16-B bucket and stops at the first one not full; at load <= 1/4 nearly
+// every lookup is that one read).
+__device__ __forceinline__ uint32_t own_home(uint32_t s, uint32_t bb) { return (s * 0x9E3779B1u) >> (32 - bb); }
+
+__device__ __forceinline__ void own_insert(uint32_t* ht, uint32_t bb, uint32_t s) {
+  const uint32_t m = (1u << bb) - 1;
+  for (uint32_t b = own_home(s, bb);; b = (b + 1) & m)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (atomicCAS(&ht[4 * b + j], kOwnEmpty, s) == kOwnEmpty) return;
 }
 
-template <bool kSeg>
-__global__ __launch_bounds__(kBlock) void k_claim(PipeArgs a) {
-  __shared__ uint64_t win[kWin];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t tile = blockIdx.x;
-  uint32_t x[4][4];
-  uint32_t cand = 0;  // bit 4j+k
+__device__ __forceinline__ uint32_t own_eq_slot(const uint4& v, uint32_t s, uint32_t b, bool& any) {
+  const bool e0 = v.x == s, e1 = v.y == s, e2 = v.z == s, e3 = v.w == s;
+  any = e0 | e1 | e2 | e3;
+  return 4 * b + (e0 ? 0u : e1 ? 1u : e2 ? 2u : 3u);
+}
+
+// Membership of the lane's four values: the four home buckets read together,
+// straight-line; the rare value whose home bucket is full and does not hold
+// it probes on in a loop the wave enters only then.  kSlot: also each hit's
+// slot (4 << bb for the 0xFFFFFFFF signal, held by has_ff).
+template <bool kSlot>
+__device__ __forceinline__ uint32_t own_probe(const uint32_t* ht, uint32_t bb, bool has_ff, const uint32_t (&x)[4],
+                                              uint32_t (&slot)[4]) {
+  const uint32_t m = (1u << bb) - 1;
+  uint32_t h[4];
+  uint4 v[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    uint64_t c = chunk_of(tile, j, wave);
-    uint32_t ok;
-    load4(a.vals, a.n, c * kChunk + lane * 4, a.aligned, x[j], ok);
+  for (int k = 0; k < 4; k++) {
+    h[k] = own_home(x[k], bb);
+    v[k] = reinterpret_cast<const uint4*>(ht)[h[k]];
+  }
+  uint32_t hit = 0, more = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    bool any;
+    const uint32_t sl = own_eq_slot(v[k], x[k], h[k], any);
+    const bool ff = x[k] == kOwnEmpty;  // (equal to every empty slot: never stored)
+    if (kSlot) slot[k] = ff ? (4u << bb) : sl;
+    hit |= ((ff ? has_ff : any) ? 1u : 0u) << k;
+    more |= (!ff && !any && v[k].w != kOwnEmpty ? 1u : 0u) << k;
+  }
+  if (__builtin_expect(__ballot(more != 0) != 0, 0)) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if ((more >> k) & 1u)
+        for (uint32_t b = (h[k] + 1) & m;; b = (b + 1) & m) {
+          const uint4 w = reinterpret_cast<const uint4*>(ht)[b];
+          bool any;
+          const uint32_t sl = own_eq_slot(w, x[k], b, any);
+          if (any) {
+            hit |= 1u << k;
+            if (kSlot) slot[k] = sl;
+            break;
+          }
+          if (w.w == kOwnEmpty) break;
+        }
+  }
+  return hit;
+}
+
+// The lane's four values of chunk c (a chunk inside the batch is loaded whole
+// whatever the record bounds: one 16-B load, or four 4-B loads when vals is
+// not 16-B aligned; only the batch's last, partial chunk takes guarded loads).
+template <bool kAligned>
+__device__ __forceinline__ void own_load(const OwnArgs& a, uint64_t c, int lane, uint32_t (&x)[4]) {
+  const uint64_t p = c * kChunk + 4 * (uint64_t)lane;
+  if ((c + 1) * kChunk <= a.n) {
+    if (kAligned) {
+      const uint4 q = *reinterpret_cast<const uint4*>(a.vals + p);
+      x[0] = q.x;
+      x[1] = q.y;
+      x[2] = q.z;
+      x[3] = q.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = a.vals[p + k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = p + k < a.n ? a.vals[p + k] : 0u;
+  }
+}
+
+// the chunk's four ballots into the mask: stored where the chunk lies inside
+// one record (this wave its only writer), OR-ed where it is shared
+__device__ __forceinline__ void own_store(uint64_t* mask, uint64_t c, int lane, uint32_t bits4, bool shared) {
+  const uint64_t b0 = __ballot(bits4 & 1u), b1 = __ballot(bits4 & 2u), b2 = __ballot(bits4 & 4u),
+                 b3 = __ballot(bits4 & 8u);
+  const uint64_t mine = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+  if (lane < 4 && mine) {
+    if (shared)
+      atomicOr(reinterpret_cast<unsigned long long*>(mask + c * 4 + lane), (unsigned long long)mine);
+    else
+      mask[c * 4 + lane] = mine;
+  }
+}
+
+// One chunk of record [lo, hi) (wave-uniform).  pass 0 (dedup): each
+// member's first position per slot; pass 1: the ballots (always OR-ed with
+// kOr: a record swept once per piece of O_r).
+template <bool kDedup, int kPass, bool kOr>
+__device__ __forceinline__ void own_chunk(const OwnArgs& a, const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff,
+                                          int lane, uint64_t lo, uint64_t hi, uint64_t c, const uint32_t (&x)[4]) {
+  const uint64_t cs = c * kChunk;
+  const bool inner = cs >= lo && cs + kChunk <= hi;
+  uint32_t ok = 0xFu;
+  if (!inner) {
+    const int32_t l = lo > cs ? (int32_t)(lo - cs) : 0, h = hi - cs < (uint64_t)kChunk ? (int32_t)(hi - cs) : kChunk;
+    ok = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      bool cnd = (ok >> k) & 1u;
-      if (a.filter) cnd = cnd && !sgd::test_bit(a.filter, x[j][k]);
-      cand |= (cnd ? 1u : 0u) << (4 * j + k);
+      const int32_t qv = 4 * lane + k;
+      ok |= (qv >= l && qv < h ? 1u : 0u) << k;
     }
   }
-  int any = __syncthreads_or(cand != 0);
-  if (any) {
-    Win w;
-    if (kSeg) {
-      win_setup(a, tile, win, w);
-      __syncthreads();
-    }
+  uint32_t slot[4];
+  uint32_t hit = own_probe<kDedup>(ht, bb, has_ff, x, slot) & ok;
+  if (kDedup) {
+    const uint32_t cr = (uint32_t)(cs - lo);  // (record positions fit 32 bits; wraps before the record)
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {  // static indices keep x[][] in registers
-        if (!((cand >> (4 * j + k)) & 1u)) continue;
-        uint64_t e = chunk_of(tile, j, wave) * kChunk + lane * 4 + k;
-        uint64_t r = kSeg ? win_lookup(a, win, w, e) : e;
-        uint32_t rk = a.rank ? a.rank[r] : (uint32_t)r;
-        uint32_t key = a.key_lo + rk;
-        uint32_t* p = a.owner + x[j][k];
-        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > key) atomicMin(p, key);
+    for (int k = 0; k < 4; k++)
+      if ((hit >> k) & 1u) {
+        const uint32_t pos = cr + 4 * lane + k;
+        if (kPass == 0)
+          atomicMin(&pm[slot[k]], pos);
+        else if (pm[slot[k]] != pos)
+          hit &= ~(1u << k);
       }
-    }
   }
-#pragma unroll
-  for (int j = 0; j < 4; j++) store_ballots(a.cmask, chunk_of(tile, j, wave), lane, (cand >> (4 * j)) & 0xFu);
+  if (kPass == 1) own_store(a.mask, c, lane, hit, kOr || !inner);
 }
 
-template <bool kSeg>
-__global__ __launch_bounds__(kBlock) void k_resolve(PipeArgs a) {
-  __shared__ uint64_t win[kWin];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t tile = blockIdx.x;
-  uint32_t cand = 0;
+// A wave's LDS operations take effect in order; this only keeps the compiler
+// from moving them across (a fence would also wait for the wave's global
+// loads and stores in flight).
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+constexpr int kOwnKB = 8;  // keys per lane loaded together
+constexpr int kOwnCB = 4;  // chunks loaded together
+
+template <bool kAligned, bool kDedup, int kPass, bool kOr = false>
+__device__ __forceinline__ void own_sweep(const OwnArgs& a, const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff,
+                                          int lane, uint64_t lo, uint64_t hi, uint64_t c0, uint64_t c1) {
+  for (uint64_t cb = c0; cb <= c1; cb += kOwnCB) {
+    uint32_t x[kOwnCB][4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    uint64_t c = chunk_of(tile, j, wave);
-    const uint64_t* m = a.cmask + c * 4;
+    for (int j = 0; j < kOwnCB; j++)
+      if (cb + j <= c1) own_load<kAligned>(a, cb + j, lane, x[j]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) cand |= (uint32_t)((m[k] >> lane) & 1ull) << (4 * j + k);
+    for (int j = 0; j < kOwnCB; j++)
+      if (cb + j <= c1) own_chunk<kDedup, kPass, kOr>(a, ht, pm, bb, has_ff, lane, lo, hi, cb + j, x[j]);
   }
-  uint32_t diff = 0;
-  int any = __syncthreads_or(cand != 0);
-  if (any) {
-    Win w;
-    if (kSeg) {
-      win_setup(a, tile, win, w);
+}
+
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+template <bool kAligned, bool kDedup>
+__global__ __launch_bounds__(kOwnWaves * 64) void k_own_wave(OwnArgs a) {
+  __shared__ alignas(16) uint32_t hts[kOwnWaves][kOwnSlots];
+  __shared__ uint32_t pms[kDedup ? kOwnWaves : 1][kDedup ? kOwnSlots + 1 : 1];  // first position per slot
+  static_assert(kOwnWave <= 64 * kOwnKB, "a wave-path record's keys: one batch");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t* ht = hts[w];
+  uint32_t* pm = pms[kDedup ? w : 0];
+  const uint32_t stride = gridDim.x * kOwnWaves;
+  uint32_t r = blockIdx.x * kOwnWaves + w;
+  // the next record's keys range and element range, loaded a record ahead
+  uint2 q = make_uint2(0, 0);
+  uint64_t lo = 0, hi = 0;
+  if (r < a.nrec) {
+    q = a.po[r];
+    lo = a.roff[r];
+    hi = a.roff[r + 1];
+  }
+  for (; r < a.nrec; r += stride) {
+    // (wave-uniform: in scalar registers, so every branch on them is a scalar one)
+    const uint32_t p0 = uni32(q.x), np = uni32(q.y) - p0;
+    const uint64_t elo = a.e0 + uni64(lo), ehi = a.e0 + uni64(hi);
+    if (r + stride < a.nrec) {
+      q = a.po[r + stride];
+      lo = a.roff[r + stride];
+      hi = a.roff[r + stride + 1];
+    }
+    if (a.rec_new && lane == 0) a.rec_new[r] = np ? 1 : 0;  // queued iff it owns a signal (fuzzer.go:678-690)
+    if (!np) continue;
+    if (np > kOwnWave) {
+      if (lane == 0) a.big[1 + atomicAdd(a.big, 1u)] = r;
+      continue;
+    }
+    // the keys and the first chunks in flight together, the set cleared meanwhile
+    uint32_t kv[kOwnKB];
+#pragma unroll
+    for (int j = 0; j < kOwnKB; j++) {
+      const uint32_t i = j * 64 + lane;
+      if (j * 64 < np) kv[j] = i < np ? (uint32_t)a.keys[p0 + i] : 0u;
+    }
+    const uint64_t c0 = elo / kChunk, c1 = (ehi - 1) / kChunk;  // (a record owning a signal has elements)
+    uint32_t x[kOwnCB][4];
+    if (!kDedup) {
+#pragma unroll
+      for (int j = 0; j < kOwnCB; j++)
+        if (c0 + j <= c1) own_load<kAligned>(a, c0 + j, lane, x[j]);
+    }
+    uint32_t bb = 4;  // buckets: >= np (load <= 1/4)
+    while ((1u << bb) < np) bb++;
+    const uint32_t size = 4u << bb;
+    for (uint32_t i = 4 * lane; i < size; i += 256)
+      *reinterpret_cast<uint4*>(ht + i) = make_uint4(kOwnEmpty, kOwnEmpty, kOwnEmpty, kOwnEmpty);
+    if (kDedup)
+      for (uint32_t i = lane; i <= size; i += 64) pm[i] = kOwnEmpty;
+    wave_sync();
+    bool ff = false;
+#pragma unroll
+    for (int j = 0; j < kOwnKB; j++) {
+      if (j * 64 >= np) break;
+      if (j * 64 + lane >= np) continue;
+      if (kv[j] == kOwnEmpty)
+        ff = true;
+      else
+        own_insert(ht, bb, kv[j]);
+    }
+    const bool has_ff = __ballot(ff) != 0;
+    wave_sync();
+    if (kDedup) {
+      own_sweep<kAligned, true, 0>(a, ht, pm, bb, has_ff, lane, elo, ehi, c0, c1);
+      wave_sync();
+      own_sweep<kAligned, true, 1>(a, ht, pm, bb, has_ff, lane, elo, ehi, c0, c1);
+    } else {  // the first batch was loaded with the keys
+#pragma unroll
+      for (int j = 0; j < kOwnCB; j++)
+        if (c0 + j <= c1) own_chunk<false, 1, false>(a, ht, pm, bb, has_ff, lane, elo, ehi, c0 + j, x[j]);
+      if (c0 + kOwnCB <= c1) own_sweep<kAligned, false, 1>(a, ht, pm, bb, has_ff, lane, elo, ehi, c0 + kOwnCB, c1);
+    }
+    wave_sync();  // (the set is cleared for the next record)
+  }
+}
+
+// Records owning more than kOwnWave signals: a workgroup each, O_r in pieces
+// of kOwnBigCap signals, each piece a sweep of S_r (two with dedup) whose
+// ballots are OR-ed into the mask.
+template <bool kAligned, bool kDedup>
+__global__ __launch_bounds__(kOwnBigT) void k_own_big(OwnArgs a) {
+  __shared__ alignas(16) uint32_t ht[kOwnBigSlots];
+  __shared__ uint32_t pm[kDedup ? kOwnBigSlots + 1 : 1];
+  __shared__ uint32_t sh_ff;
+  constexpr int kW = kOwnBigT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t nbig = a.big[0];
+  for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {
+    const uint32_t r = uni32(a.big[1 + j]);
+    const uint2 q = make_uint2(uni32(a.po[r].x), uni32(a.po[r].y));
+    const uint64_t lo = a.e0 + uni64(a.roff[r]), hi = a.e0 + uni64(a.roff[r + 1]);
+    const uint64_t c0 = lo / kChunk, c1 = (hi - 1) / kChunk;
+    for (uint32_t q0 = q.x; q0 < q.y; q0 += kOwnBigCap) {
+      const uint32_t q1 = min(q.y, q0 + kOwnBigCap);
+      uint32_t bb = 4;  // buckets: >= the piece's keys
+      while ((1u << bb) < q1 - q0) bb++;
+      const uint32_t size = 4u << bb;
+      for (uint32_t i = tid; i < size; i += kOwnBigT) ht[i] = kOwnEmpty;
+      if (kDedup)
+        for (uint32_t i = tid; i <= size; i += kOwnBigT) pm[i] = kOwnEmpty;
+      if (tid == 0) sh_ff = 0;
+      __syncthreads();
+      for (uint32_t i = q0 + tid; i < q1; i += kOwnBigT) {
+        const uint32_t sv = (uint32_t)a.keys[i];
+        if (sv == kOwnEmpty)
+          sh_ff = 1;
+        else
+          own_insert(ht, bb, sv);
+      }
+      __syncthreads();
+      const bool has_ff = sh_ff != 0;
+      // the waves take chunk batches kW apart: wave w's chunks c0 + kOwnCB (w + kW i) ..
+      for (uint64_t cb = c0 + (uint64_t)w * kOwnCB; kDedup && cb <= c1; cb += (uint64_t)kW * kOwnCB)
+        own_sweep<kAligned, true, 0>(a, ht, pm, bb, has_ff, lane, lo, hi, cb, min(c1, cb + kOwnCB - 1));
+      if (kDedup) __syncthreads();
+      for (uint64_t cb = c0 + (uint64_t)w * kOwnCB; cb <= c1; cb += (uint64_t)kW * kOwnCB)
+        own_sweep<kAligned, kDedup, 1, true>(a, ht, pm, bb, has_ff, lane, lo, hi, cb, min(c1, cb + kOwnCB - 1));
       __syncthreads();
     }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      uint32_t cj = (cand >> (4 * j)) & 0xFu;
-      if (!cj) continue;
-      uint64_t e0 = chunk_of(tile, j, wave) * kChunk + lane * 4;
-      uint32_t x[4], ok;
-      load4(a.vals, a.n, e0, a.aligned, x, ok);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (!((cj >> k) & 1u)) continue;
-        uint64_t e = e0 + k;
-        uint64_t r = kSeg ? win_lookup(a, win, w, e) : e;
-        uint32_t rk = a.rank ? a.rank[r] : (uint32_t)r;
-        if (a.owner[x[k]] != a.key_lo + rk) continue;
-        diff |= 1u << (4 * j + k);
-        if (a.set_a) sgd::set_bit(a.set_a, x[k]);
-        if (a.set_b) sgd::set_bit(a.set_b, x[k]);
-        if (a.seg_flag) a.seg_flag[r] = 1;
-      }
-    }
   }
+}
+
+// [po[r].x, po[r].y): record r's keys (po zeroed: records without keys stay
+// empty), from the run boundaries of each group's sorted keys, kBoundPer
+// consecutive keys per thread
+constexpr int kBoundPer = 8;
+__global__ void k_own_bounds(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ gs,
+                             const unsigned long long* __restrict__ gcnt, uint32_t ng, uint2* __restrict__ po) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t n = gcnt[g], i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kBoundPer;
+  if (g >= ng || i0 >= n) return;
+  const uint64_t* k = keys + gs[g];
+  uint32_t prev = i0 ? (uint32_t)(k[i0 - 1] >> 32) : 0xFFFFFFFFu;
+  uint32_t cur = (uint32_t)(k[i0] >> 32);
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    uint64_t c = chunk_of(tile, j, wave);
-    uint32_t dj = (diff >> (4 * j)) & 0xFu;
-    store_ballots(a.dmask, c, lane, dj);
-    uint32_t cntj = __popcll(__ballot(dj & 1u)) + __popcll(__ballot(dj & 2u)) + __popcll(__ballot(dj & 4u)) +
-                    __popcll(__ballot(dj & 8u));
-    if (lane == 0) a.dcnt[c] = cntj;
+  for (int j = 0; j < kBoundPer; j++) {
+    const uint64_t i = i0 + j;
+    if (i >= n) break;
+    const uint32_t next = i + 1 < n ? (uint32_t)(k[i + 1] >> 32) : 0xFFFFFFFFu;
+    if (cur != prev) po[cur].x = (uint32_t)(gs[g] + i);
+    if (cur != next) po[cur].y = (uint32_t)(gs[g] + i + 1);
+    prev = cur;
+    cur = next;
   }
+}
+
+// gs[g] = roff[g << 16] (g < ng): where group g's pairs start
+__global__ void k_group_starts(const uint64_t* __restrict__ roff, uint32_t ng, uint64_t* __restrict__ gs) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ng) gs[g] = roff[(uint64_t)g << kRecGroupBits];
+}
+
+// diff elements per chunk, from its ballots
+__global__ void k_mask_count(const uint64_t* __restrict__ mask, uint64_t nchunks, uint32_t* __restrict__ cnt) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const ulonglong2 u = reinterpret_cast<const ulonglong2*>(mask)[2 * c];
+  const ulonglong2 v = reinterpret_cast<const ulonglong2*>(mask)[2 * c + 1];
+  cnt[c] = __popcll(u.x) + __popcll(u.y) + __popcll(v.x) + __popcll(v.y);
 }
 
 // ---- ordered compaction by ballot masks --------------------------------------
@@ -567,38 +778,6 @@ static Scratch scratch_bind(sg_ctx* ctx, uint64_t n, const size_t o[5]) {
   return s;
 }
 
-// claim + resolve over a batch already on the device.
-static int run_pipe(sg_ctx* ctx, PipeArgs a, const Scratch& s) {
-  if (a.n == 0) return SG_OK;
-  a.cmask = s.cmask;
-  a.dmask = s.dmask;
-  a.dcnt = s.dcnt;
-  a.tile_rec = s.tile_rec;
-  a.owner = ctx->owner;
-  a.aligned = ((uintptr_t)a.vals & 15) == 0;
-  if (a.off) {
-    ScopedTimer tm(ctx, "tile_rec");
-    hipLaunchKernelGGL(k_tile_rec, dim3(div_up(s.ntiles + 1, 256)), dim3(256), 0, ctx->stream, a.off, a.nseg, a.n,
-                       s.ntiles, s.tile_rec);
-  }
-  {
-    ScopedTimer tm(ctx, "triage_claim");
-    if (a.off)
-      hipLaunchKernelGGL(k_claim<true>, dim3((uint32_t)s.ntiles), dim3(kBlock), 0, ctx->stream, a);
-    else
-      hipLaunchKernelGGL(k_claim<false>, dim3((uint32_t)s.ntiles), dim3(kBlock), 0, ctx->stream, a);
-  }
-  {
-    ScopedTimer tm(ctx, "triage_resolve");
-    if (a.off)
-      hipLaunchKernelGGL(k_resolve<true>, dim3((uint32_t)s.ntiles), dim3(kBlock), 0, ctx->stream, a);
-    else
-      hipLaunchKernelGGL(k_resolve<false>, dim3((uint32_t)s.ntiles), dim3(kBlock), 0, ctx->stream, a);
-  }
-  SG_HIP(hipGetLastError());
-  return SG_OK;
-}
-
 // ordered emission of the masked values (+ per-segment offsets)
 static int run_emit(sg_ctx* ctx, const uint32_t* vals, uint64_t n, const uint64_t* mask, const uint32_t* cnt,
                     const Scratch& s, size_t scan_ws_off, const uint64_t* off, uint64_t nseg, uint32_t* out_vals,
@@ -615,6 +794,134 @@ static int run_emit(sg_ctx* ctx, const uint32_t* vals, uint64_t n, const uint64_
                        s.base, s.nchunks, out_off);
   SG_HIP(hipGetLastError());
   return SG_OK;
+}
+
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// the per-record sweeps of one slice: the wave kernel over the resident grid
+// (each wave takes every grid-th record), then the listed large records
+template <bool kAligned>
+static int launch_own(sg_ctx* ctx, const OwnArgs& oa, uint64_t nr, bool dedup) {
+  const void* kw = dedup ? (const void*)k_own_wave<kAligned, true> : (const void*)k_own_wave<kAligned, false>;
+  const uint32_t wg = std::min<uint32_t>(div_up(nr, kOwnWaves), persistent_grid(ctx, kw, kOwnWaves * 64));
+  if (dedup) {
+    hipLaunchKernelGGL((k_own_wave<kAligned, true>), dim3(wg), dim3(kOwnWaves * 64), 0, ctx->stream, oa);
+    hipLaunchKernelGGL((k_own_big<kAligned, true>), dim3(512), dim3(kOwnBigT), 0, ctx->stream, oa);
+  } else {
+    hipLaunchKernelGGL((k_own_wave<kAligned, false>), dim3(wg), dim3(kOwnWaves * 64), 0, ctx->stream, oa);
+    hipLaunchKernelGGL((k_own_big<kAligned, false>), dim3(512), dim3(kOwnBigT), 0, ctx->stream, oa);
+  }
+  SG_HIP(hipGetLastError());
+  return SG_OK;
+}
+
+// Ordered outputs of a first-owner loop over records (ctx lock held): flags
+// (nullable), mwords / nwords (nullable) updated, the diff CSR (out_vals,
+// out_off; either nullable).  Record slices as the flags path cuts them; per
+// slice: partition + the update-emitting bucket stage, the pairs sorted by
+// record, the per-record sweeps into the batch's diff mask; then one ordered
+// compaction.  Workspace: the batch's masks, then one slice's region -- the
+// partition's scratch, which the radix sort reuses as its second key buffer
+// once the bucket stage is done, the pairs, the sort's counts and the
+// per-record tables.
+static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
+                         const uint64_t* d_off, uint64_t nvals, uint64_t nrec, uint8_t* d_rec_new, uint32_t* d_out_vals,
+                         uint64_t* d_out_off, bool dedup) {
+  if (nrec >= 0xFFFFFFFFull || nvals >= 0xFFFFFFFFull - (1ull << 16)) {
+    set_error("ordered triage: a batch holds < 2^32 signal entries and < 2^32 - 1 records");
+    return SG_EINVAL;
+  }
+  if (nrec && d_rec_new) SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
+  if (nvals == 0) {
+    if (d_out_off) SG_HIP(hipMemsetAsync(d_out_off, 0, (nrec + 1) * 8, ctx->stream));
+    return SG_OK;
+  }
+  if (nrec == 0) {
+    set_error("ordered triage: signal entries without records");
+    return SG_EINVAL;
+  }
+  std::vector<uint64_t> cuts;
+  int rc = record_slice_cuts(ctx, d_off, nrec, 1ull << 30, cuts);
+  if (rc) return rc;
+  WsPlan p;
+  size_t o[5];
+  const size_t scan_b = scratch_plan(p, nvals, o);
+  const size_t scan_off = p.total;
+  const size_t S0 = al256(p.total + scan_b);
+  size_t part = 0, tail = 0;
+  for (size_t j = 0; j + 3 < cuts.size(); j += 4) {
+    const uint64_t nr = cuts[j + 1] - cuts[j], ns = cuts[j + 3] - cuts[j + 2];
+    if (!ns) continue;
+    part = std::max(part, al256(std::max<size_t>(bucket_plan_bytes(ns, nr), ns * 8)));
+    tail = std::max(tail, al256(ns * 8) + al256(radix_sort_ws(ns)) + al256(nr * 8) + al256((nr + 2) * 4) +
+                               al256((nr + 1) * 8) + al256(((nr >> kRecGroupBits) + 1) * 16));
+  }
+  rc = ws_reserve(ctx, S0 + part + tail);
+  if (rc) return rc;
+  Scratch s = scratch_bind(ctx, nvals, o);
+  SG_HIP(hipMemsetAsync(s.dmask, 0, s.nchunks * 32, ctx->stream));
+  const int aligned = ((uintptr_t)d_vals & 15) == 0;
+  for (size_t j = 0; j + 3 < cuts.size(); j += 4) {
+    const uint64_t r0 = cuts[j], nr = cuts[j + 1] - r0, e0 = cuts[j + 2], ns = cuts[j + 3] - e0;
+    if (!ns) continue;  // (flags cleared above)
+    uint64_t* keys_b = (uint64_t*)ws_at(ctx, S0);
+    size_t at = S0 + part;
+    uint64_t* keys_a = (uint64_t*)ws_at(ctx, at);
+    at += al256(ns * 8);
+    const size_t sort_at = at;
+    at += al256(radix_sort_ws(ns));
+    uint2* po = (uint2*)ws_at(ctx, at);
+    at += al256(nr * 8);
+    uint32_t* big = (uint32_t*)ws_at(ctx, at);
+    at += al256((nr + 2) * 4);
+    uint64_t* roff = (uint64_t*)ws_at(ctx, at);
+    at += al256((nr + 1) * 8);
+    const uint32_t ng = (uint32_t)((nr + (1u << kRecGroupBits) - 1) >> kRecGroupBits);
+    unsigned long long* gcur = (unsigned long long*)ws_at(ctx, at);  // ng cursors, then ng starts
+    uint64_t* gs = (uint64_t*)(gcur + ng);
+    rc = rebase_offsets(ctx, d_off + r0, nr + 1, e0, roff);
+    if (rc) return rc;
+    SG_HIP(hipMemsetAsync(gcur, 0, ng * 8, ctx->stream));
+    SG_HIP(hipMemsetAsync(big, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(k_group_starts, dim3(div_up(ng, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)roff, ng, gs);
+    rc = bucket_emit_update(ctx, mwords, nwords, d_vals + e0, roff, ns, nr, (uint2*)keys_a, gcur, S0);
+    if (rc) return rc;
+    std::vector<uint64_t> gh(2 * (size_t)ng);  // counts, starts
+    SG_HIP(hipMemcpyAsync(gh.data(), gcur, gh.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    {
+      // each group's pairs by record: the record's low 16 bits, two passes
+      // (the group itself is the bucket stage's placement), back in keys_a
+      ScopedTimer tm(ctx, "owned_sort");
+      for (uint32_t g = 0; g < ng; g++) {
+        const uint64_t cnt = gh[g], st = gh[ng + g];
+        if (cnt < 2) continue;
+        uint64_t* sorted = nullptr;
+        rc = radix_sort_u64(ctx, keys_a + st, keys_b + st, cnt, sort_at, &sorted, 0xFFFFull << 32);
+        if (rc) return rc;
+        if (sorted != keys_a + st)
+          SG_HIP(hipMemcpyAsync(keys_a + st, sorted, cnt * 8, hipMemcpyDeviceToDevice, ctx->stream));
+      }
+    }
+    ScopedTimer tm(ctx, "owned_sweep");
+    uint64_t gmax = 0;
+    for (uint32_t g = 0; g < ng; g++) gmax = std::max<uint64_t>(gmax, gh[g]);
+    SG_HIP(hipMemsetAsync(po, 0, nr * 8, ctx->stream));
+    if (gmax)
+      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(gmax, 256 * kBoundPer), ng), dim3(256), 0, ctx->stream,
+                         (const uint64_t*)keys_a, (const uint64_t*)gs, (const unsigned long long*)gcur, ng, po);
+    OwnArgs oa{d_vals, roff, e0, (uint32_t)nr, keys_a, po, d_rec_new ? d_rec_new + r0 : nullptr, s.dmask, big, nvals};
+    if (aligned)
+      rc = launch_own<true>(ctx, oa, nr, dedup);
+    else
+      rc = launch_own<false>(ctx, oa, nr, dedup);
+    if (rc) return rc;
+    SG_HIP(hipGetLastError());
+  }
+  if (!d_out_vals && !d_out_off) return SG_OK;
+  hipLaunchKernelGGL(k_mask_count, dim3(div_up(s.nchunks, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)s.dmask,
+                     s.nchunks, s.dcnt);
+  return run_emit(ctx, d_vals, nvals, s.dmask, s.dcnt, s, scan_off, d_off, nrec, d_out_vals, d_out_off);
 }
 
 static int check_alloc(sg_ctx* ctx) { return ensure_device(ctx); }
@@ -642,38 +949,10 @@ int sg_triage_batch_dev(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint3
   if (!d_diff_vals && !d_diff_off)  // flags + set updates only: partitioned path
     return bucket_triage(ctx, maxsig->words, newsig ? newsig->words : nullptr, d_vals, d_rec_off, nvals, nrec,
                          d_rec_new);
-  WsPlan p;
-  size_t o[5];
-  size_t scan_b = scratch_plan(p, nvals, o);
-  size_t scan_off = p.total;
-  rc = ws_reserve(ctx, p.total + scan_b);
-  if (rc) return rc;
-  Scratch s = scratch_bind(ctx, nvals, o);
-  uint32_t key_lo = 0;
-  if (nrec) {
-    rc = owner_keys(ctx, nrec, &key_lo);
-    if (rc) return rc;
-    SG_HIP(hipMemsetAsync(d_rec_new, 0, nrec, ctx->stream));
-  }
-  if (nvals == 0) {
-    if (d_diff_off) SG_HIP(hipMemsetAsync(d_diff_off, 0, (nrec + 1) * 8, ctx->stream));
-    return SG_OK;
-  }
-  PipeArgs a{};
-  a.vals = d_vals;
-  a.n = nvals;
-  a.off = d_rec_off;
-  a.nseg = nrec;
-  a.filter = maxsig->words;
-  a.key_lo = key_lo;
-  a.seg_flag = d_rec_new;
-  a.set_a = maxsig->words;
-  a.set_b = newsig ? newsig->words : nullptr;
-  rc = run_pipe(ctx, a, s);
-  if (rc) return rc;
-  if (d_diff_vals || d_diff_off)
-    rc = run_emit(ctx, d_vals, nvals, s.dmask, s.dcnt, s, scan_off, d_rec_off, nrec, d_diff_vals, d_diff_off);
-  return rc;
+  // the ordered diff lists (fuzzer.go:669 SignalDiff per record) from the
+  // update-emitting bucket stage's first owners
+  return owned_outputs(ctx, maxsig->words, newsig ? newsig->words : nullptr, d_vals, d_rec_off, nvals, nrec, d_rec_new,
+                       d_diff_vals, d_diff_off, false);
 }
 
 int sg_triage_batch(sg_ctx* ctx, sg_set* maxsig, sg_set* newsig, const uint32_t* vals, const uint64_t* rec_off,
@@ -901,34 +1180,21 @@ int sg_merge_poll(sg_ctx* ctx, sg_set* mgr_max, const uint32_t* a_vals, const ui
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = check_alloc(ctx);
   if (rc) return rc;
-  WsPlan p;
-  size_t o[5];
-  size_t o_in = p.add(nv * 4), o_off = p.add((npoll + 1) * 8), o_out = p.add(nv * 4), o_oo = p.add((npoll + 1) * 8);
-  size_t scan_b = scratch_plan(p, nv, o);
-  size_t scan_off = p.total;
-  rc = ws_reserve(ctx, p.total + scan_b);
+  // the Poll loop (manager.go:949-956) is a first-owner loop over the polls
+  // with mgr.maxSignal as the running set, each poll's new signals in its
+  // order, once each (its first occurrence): the ordered-output path with
+  // dedup.  The batch is staged in dstage (the workspace is the partition's).
+  const size_t b_in = al256(nv * 4), b_off = al256((npoll + 1) * 8);
+  rc = dstage_reserve(ctx, 2 * b_in + 2 * b_off + 256);
   if (rc) return rc;
-  Scratch s = scratch_bind(ctx, nv, o);
-  uint32_t* din = (uint32_t*)ws_at(ctx, o_in);
-  uint64_t* doff = (uint64_t*)ws_at(ctx, o_off);
-  uint32_t* dout = (uint32_t*)ws_at(ctx, o_out);
-  uint64_t* doo = (uint64_t*)ws_at(ctx, o_oo);
+  char* st = (char*)ctx->dstage;
+  uint32_t* din = (uint32_t*)st;
+  uint64_t* doff = (uint64_t*)(st + b_in);
+  uint32_t* dout = (uint32_t*)(st + b_in + b_off);
+  uint64_t* doo = (uint64_t*)(st + 2 * b_in + b_off);
   SG_HIP(hipMemcpyAsync(din, a_vals, nv * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(doff, a_off, (npoll + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-  uint32_t key_lo;
-  rc = owner_keys(ctx, nv, &key_lo);  // one key per element: first occurrence wins
-  if (rc) return rc;
-  PipeArgs a{};
-  a.vals = din;
-  a.n = nv;
-  a.off = nullptr;
-  a.nseg = nv;
-  a.filter = mgr_max->words;
-  a.key_lo = key_lo;
-  a.set_a = mgr_max->words;  // manager.go:953
-  rc = run_pipe(ctx, a, s);
-  if (rc) return rc;
-  rc = run_emit(ctx, din, nv, s.dmask, s.dcnt, s, scan_off, doff, npoll, dout, doo);
+  rc = owned_outputs(ctx, mgr_max->words, nullptr, din, doff, nv, npoll, nullptr, dout, doo, true);
   if (rc) return rc;
   SG_HIP(hipMemcpyAsync(new_off, doo, (npoll + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));

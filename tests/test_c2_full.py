@@ -3,7 +3,10 @@
 (sg_triage_batch_dev, the partitioned kernels the bench times) against the
 oracle's sequential loop (oracle/sigoracle.c, restating
 syz-fuzzer/fuzzer.go:645-693) on the same batch, bit-exact in the per-record
-flags and in both sets afterwards.
+flags and in both sets afterwards -- and the same batch again through the
+ordered-output path (the diff CSR of fuzzer.go:669, sg_triage.hip
+owned_outputs) from the same starting sets, bit-exact in the flags, every
+record's diff list and both sets.
 
 The batch is the fuzzer's steady state (bench.py "steady"): programs drawn
 from a fixed population with flaky coverage, against maxSignal = the
@@ -36,6 +39,35 @@ def _signal(call, ctx, trace, nprog, calls, pcs):
     return sig[:n], off
 
 
+def _diff_path(call, ctx, m0, sig, off, ef, ev, eo, em, en):
+    """The batch through sg_triage_batch_dev with the diff CSR, from maxSignal
+    = m0 and an empty newSignal; everything against the oracle's loop."""
+    from syzkaller_amd.cover import SignalSet
+
+    nvals, nrec = sig.numel(), off.numel() - 1
+    ms, ns = SignalSet(ctx), SignalSet(ctx)
+    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()
+    call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
+    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    dv = torch.empty(nvals, dtype=torch.int32, device="cuda")
+    do = torch.empty(nrec + 1, dtype=torch.int64, device="cuda")
+    call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
+         dv.data_ptr(), do.data_ptr())
+    torch.cuda.synchronize()
+    del dm0
+    assert np.array_equal(rec_new.cpu().numpy(), ef)
+    got_o = do.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got_o, eo)
+    nd = int(got_o[-1])
+    assert nd == ev.size
+    assert np.array_equal(dv[:nd].cpu().numpy().view(np.uint32), ev)
+    del dv, do, rec_new
+    assert np.array_equal(ns.export(), en)
+    assert np.array_equal(ms.export(), em)
+    ns.close()
+    ms.close()
+
+
 @pytest.mark.timeout(600)
 def test_c2_full_batch_steady_state_vs_oracle(ctx):
     from syzkaller_amd._lib import call
@@ -65,14 +97,17 @@ def test_c2_full_batch_steady_state_vs_oracle(ctx):
     got = rec_new.cpu().numpy()
     # the oracle's sequential loop over the same batch
     om, on = O.OSet(m0), O.OSet()
-    exp = O.triage_flags_only(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
+    exp, ev, eo = O.triage_batch(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
     frac = float(exp.mean())
     assert 0.05 < frac < 0.95, frac  # mixed flags: the attribution is really tested
     assert np.array_equal(got, exp)
-    assert np.array_equal(ns.export(), on.export())
-    assert np.array_equal(ms.export(), om.export())
+    em, en = om.export(), on.export()
+    del om, on
+    assert np.array_equal(ns.export(), en)
+    assert np.array_equal(ms.export(), em)
     ns.close()
     ms.close()
+    _diff_path(call, ctx, m0, sig, off, exp, ev, eo, em, en)
     call("sg_ctx_reset_stream", ctx.h)
 
 
@@ -83,7 +118,8 @@ def test_c2_full_fresh_batch_sets_vs_oracle(ctx):
     maxSignal taken from a warm batch's first programs.  Every record is
     queued (each carries a never-seen edge), so the check that matters is the
     ~200M new signals: maxSignal and newSignal after the batch, exported and
-    compared whole with the oracle's sequential loop, plus the flags."""
+    compared whole with the oracle's sequential loop, plus the flags; then
+    the ~208M-element diff CSR of the ordered-output path."""
     from syzkaller_amd._lib import call
     from syzkaller_amd.cover import SignalSet
 
@@ -111,13 +147,16 @@ def test_c2_full_fresh_batch_sets_vs_oracle(ctx):
     torch.cuda.synchronize()
     got = rec_new.cpu().numpy()
     om, on = O.OSet(m0), O.OSet()
-    exp = O.triage_flags_only(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
+    exp, ev, eo = O.triage_batch(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
     assert np.array_equal(got, exp)
-    gn, en = ns.export(), on.export()
+    em, en = om.export(), on.export()
+    del om, on
+    gn = ns.export()
     assert gn.size > 100_000_000 and gn.size == en.size  # ~208M new signals
     assert np.array_equal(gn, en)
-    del gn, en
-    assert np.array_equal(ms.export(), om.export())
+    del gn
+    assert np.array_equal(ms.export(), em)
     ns.close()
     ms.close()
+    _diff_path(call, ctx, m0, sig, off, exp, ev, eo, em, en)
     call("sg_ctx_reset_stream", ctx.h)

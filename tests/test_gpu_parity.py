@@ -325,8 +325,9 @@ def test_signal_set_ops(C):
 
 # ---- the hot path: batched new-signal triage (fuzzer.go:645-693) ----------------
 class TwoPaths:
-    """The same sets kept twice: one pair driven through the diff-emitting
-    claim/resolve path, one through the flags-only partitioned path."""
+    """The same sets kept twice: one pair driven through the ordered-output
+    path (the diff CSR from the bucket stage's first owners, sg_triage.hip
+    owned_outputs), one through the flags-only partitioned path."""
 
     def __init__(self, C, ctx=None):
         self.C = C
@@ -344,7 +345,7 @@ class TwoPaths:
     def triage(self, vals, off):
         flags, dv, do = self.C.triage_batch(self.d[0], self.d[1], vals, off)
         fflags, _, _ = self.C.triage_batch(self.f[0], self.f[1], vals, off, want_diff=False)
-        assert np.array_equal(flags, fflags), "partitioned path disagrees with the claim/resolve path"
+        assert np.array_equal(flags, fflags), "flags-only path disagrees with the ordered-output path"
         return flags, dv, do
 
     def exports(self):
@@ -579,6 +580,12 @@ def test_merge_poll_vs_oracle(C):
                  for _ in range(20)]
         polls = [rng.permutation(p) for p in polls]  # map iteration order
         polls.append(np.array([5, 5, 6, 5], np.uint32))  # duplicates: first occurrence only
+        # a poll owning more than the per-wave set (k_own_big) and one past a
+        # piece of it, both with repeats; the 0xFFFFFFFF signal
+        big = rng.integers(0, 1 << 24, size=30000).astype(np.uint32)
+        polls.append(np.concatenate([big[:3000], big[:1500], big[2000:12000], [0xFFFFFFFF], big[500:9000]]))
+        polls.append(np.concatenate([big[12000:], [0xFFFFFFFF, 0xFFFFFFFF], big[12000:20000]]))
+        polls.append(np.array([0xFFFFFFFF, 9, 0xFFFFFFFF], np.uint32))
         av, ao = C.to_csr(polls)
         nv, no = C.merge_poll(mm, av, ao)
         ev, eo = O.merge_poll(om, av, ao)
@@ -739,12 +746,13 @@ def test_triage_record_slices(C, monkeypatch):
 def test_owner_key_generation_reset(C, monkeypatch):
     """The first-owner table (sg_ctx.hip owner_keys) hands out decreasing keys
     and starts a fresh generation (a full reset of the table) when the key
-    space runs out.  The key space is lowered here so that record-keyed
-    triage, element-keyed Poll merges and rank-keyed Minimize cross several
-    resets; every result still equals the oracle's."""
-    monkeypatch.setenv("SG_OWNER_KEY_SPACE", "6000")
+    space runs out.  The key space is lowered here so that rank-keyed
+    Minimize crosses several resets, between triage batches and Poll merges
+    (which take their owners from the bucket stage, not the table); every
+    result still equals the oracle's."""
+    monkeypatch.setenv("SG_OWNER_KEY_SPACE", "1500")
     ctx = C.Context(0)
-    assert ctx.counter("owner_key_space") == 6000
+    assert ctx.counter("owner_key_space") == 1500
     rng = np.random.default_rng(151)
     ms, ns, mm = C.SignalSet(ctx), C.SignalSet(ctx), C.SignalSet(ctx)
     om, on, omm = O.OSet(), O.OSet(), O.OSet()
@@ -753,13 +761,13 @@ def test_owner_key_generation_reset(C, monkeypatch):
         lens = rng.integers(0, 12, size=nrec)
         vals = rng.integers(0, 1 << 16, size=int(lens.sum())).astype(np.uint32)
         off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
-        flags, dv, do = C.triage_batch(ms, ns, vals, off)  # claim/resolve: record keys
+        flags, dv, do = C.triage_batch(ms, ns, vals, off)  # the ordered outputs
         ef, ev, eo = O.triage_batch(om, on, vals, off)
         assert np.array_equal(flags, ef) and np.array_equal(dv, ev) and np.array_equal(do, eo), it
         polls = [rng.permutation(np.unique(rng.integers(0, 1 << 17, size=int(rng.integers(0, 900)))).astype(np.uint32))
                  for _ in range(4)]
         av, ao = C.to_csr(polls)
-        nv, no = C.merge_poll(mm, av, ao, ctx=ctx)  # element keys
+        nv, no = C.merge_poll(mm, av, ao, ctx=ctx)
         ev2, eo2 = O.merge_poll(omm, av, ao)
         assert np.array_equal(nv, ev2) and np.array_equal(no, eo2), it
         covs = [C.Canonicalize(rng.integers(0, 3000, size=int(rng.integers(0, 40))).astype(np.uint32), ctx=ctx)
