@@ -242,6 +242,11 @@ constexpr uint32_t kRecGroupBits = 16;  // records per group of the partitioned 
 size_t radix_sort_ws(uint64_t n);
 int radix_sort_u64(sg_ctx* ctx, uint64_t* a, uint64_t* b, uint64_t n, size_t ws_used, uint64_t** sorted,
                    uint64_t vary = 0);
+// One stable radix pass over keys in runs of a gapped buffer (run order kept
+// within a digit), written contiguously into dst (sg_sort.hip; syncs).
+int radix_pass_runs(sg_ctx* ctx, const uint64_t* src, const std::vector<uint64_t>& run_start,
+                    const std::vector<uint64_t>& run_cnt, uint32_t shift, uint64_t* dst, size_t ws_used);
+size_t radix_pass_runs_ws(uint64_t n, uint64_t nruns);
 
 }  // namespace sg
 

@@ -19,6 +19,9 @@
 // store.
 #include "sg_internal.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace sg {
 
 constexpr int kRsThreads = 512;
@@ -46,13 +49,33 @@ __global__ void k_rs_andor(const uint64_t* __restrict__ k, uint64_t n, unsigned 
 __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t shift) { return (uint32_t)(k >> shift) & 255u; }
 
 // hist[d * ntiles + t] = number of keys of tile t with digit d
+// Tile t's keys: keys[tile_base(t) ..], n_t of them.  Contiguous tiles of
+// kRsTile, or (tsrc != null) tile t = tsrc[t], tcnt[t] keys: a first pass
+// reading runs scattered over a gapped buffer.
+__device__ __forceinline__ void rs_tile(uint64_t n, const uint64_t* tsrc, const uint32_t* tcnt, uint32_t t,
+                                        uint64_t& base, uint64_t& nt) {
+  if (tsrc) {
+    base = tsrc[t];
+    nt = tcnt[t];
+  } else {
+    base = (uint64_t)t * kRsTile;
+    nt = min<uint64_t>(kRsTile, n - base);
+  }
+}
+
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restrict__ keys, uint64_t n, uint32_t shift,
-                                                        uint32_t ntiles, uint32_t* __restrict__ hist) {
+                                                        uint32_t ntiles, uint32_t* __restrict__ hist,
+                                                        const uint64_t* __restrict__ tsrc,
+                                                        const uint32_t* __restrict__ tcnt) {
   __shared__ uint32_t cnt[kRsWaves][256];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   for (int i = tid; i < kRsWaves * 256; i += kRsThreads) (&cnt[0][0])[i] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kRsTile + (uint64_t)w * (64 * kRsSteps);
+  uint64_t tb, tn;
+  rs_tile(n, tsrc, tcnt, blockIdx.x, tb, tn);
+  keys += tb;
+  n = tn;
+  const uint64_t base = (uint64_t)w * (64 * kRsSteps);
 #pragma unroll 4
   for (int s = 0; s < kRsSteps; s++) {
     const uint64_t e = base + s * 64 + lane;
@@ -80,7 +103,8 @@ __device__ __forceinline__ uint64_t rs_peers(uint32_t d, bool live) {
 
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __restrict__ in, uint64_t n, uint32_t shift,
                                                            uint32_t ntiles, const uint64_t* __restrict__ goff,
-                                                           uint64_t* __restrict__ out) {
+                                                           uint64_t* __restrict__ out, const uint64_t* __restrict__ tsrc,
+                                                           const uint32_t* __restrict__ tcnt) {
   __shared__ uint64_t stage[kRsTile];
   __shared__ uint32_t cnt[kRsWaves][256];  // per-wave running counts, then per-wave offsets in the tile
   __shared__ uint32_t dstart[256];         // digit start in the tile (stage)
@@ -90,7 +114,11 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __res
   const uint32_t t = blockIdx.x;
   for (int i = tid; i < kRsWaves * 256; i += kRsThreads) (&cnt[0][0])[i] = 0;
   if (tid < 256) gb[tid] = goff[(uint64_t)tid * ntiles + t];
-  const uint64_t base = (uint64_t)t * kRsTile + (uint64_t)w * (64 * kRsSteps);
+  uint64_t tb, tn;
+  rs_tile(n, tsrc, tcnt, t, tb, tn);
+  in += tb;
+  n = tn;
+  const uint64_t base = (uint64_t)w * (64 * kRsSteps);
   uint64_t k[kRsSteps];
 #pragma unroll
   for (int s = 0; s < kRsSteps; s++) {
@@ -196,16 +224,64 @@ int radix_sort_u64(sg_ctx* ctx, uint64_t* a, uint64_t* b, uint64_t n, size_t ws_
   for (uint32_t shift = lo; shift < hi; shift += 8) {
     if (((vary >> shift) & 255u) == 0) continue;  // the same digit in every key
     hipLaunchKernelGGL(k_rs_hist, dim3((uint32_t)nt), dim3(kRsThreads), 0, ctx->stream, (const uint64_t*)src, n, shift,
-                       (uint32_t)nt, hist);
+                       (uint32_t)nt, hist, nullptr, nullptr);
     int rc = scan_counts(ctx, hist, goff, 256 * nt, scan_at);
     if (rc) return rc;
     hipLaunchKernelGGL(k_rs_scatter, dim3((uint32_t)nt), dim3(kRsThreads), 0, ctx->stream, (const uint64_t*)src, n,
-                       shift, (uint32_t)nt, (const uint64_t*)goff, dst);
+                       shift, (uint32_t)nt, (const uint64_t*)goff, dst, nullptr, nullptr);
     SG_HIP(hipGetLastError());
     std::swap(src, dst);
   }
   *sorted = src;
   return SG_OK;
+}
+
+// One stable pass (digit at `shift`) over keys held in runs of a gapped
+// buffer: the host's runs (start, count) are cut into tiles of <= kRsTile,
+// and the pass writes the n keys contiguously into dst, ordered by digit,
+// then by run order.  Workspace from ws_used on: radix_sort_ws(n) plus the
+// tile table (runs + n / kRsTile tiles).
+int radix_pass_runs(sg_ctx* ctx, const uint64_t* src, const std::vector<uint64_t>& run_start,
+                    const std::vector<uint64_t>& run_cnt, uint32_t shift, uint64_t* dst, size_t ws_used) {
+  std::vector<uint64_t> ts;
+  std::vector<uint32_t> tc;
+  uint64_t n = 0;
+  for (size_t i = 0; i < run_start.size(); i++)
+    for (uint64_t o = 0; o < run_cnt[i]; o += kRsTile) {
+      ts.push_back(run_start[i] + o);
+      tc.push_back((uint32_t)std::min<uint64_t>(kRsTile, run_cnt[i] - o));
+      n += tc.back();
+    }
+  const uint64_t nt = ts.size();
+  if (!nt) return SG_OK;
+  char* ws = (char*)ws_at(ctx, ws_used);
+  uint32_t* hist = (uint32_t*)ws;
+  const size_t o_goff = (256 * nt * 4 + 255) & ~255ull;
+  uint64_t* goff = (uint64_t*)(ws + o_goff);
+  const size_t o_ts = o_goff + ((((256 * nt + 1) * 8) + 255) & ~255ull);
+  uint64_t* dts = (uint64_t*)(ws + o_ts);
+  const size_t o_tc = o_ts + ((nt * 8 + 255) & ~255ull);
+  uint32_t* dtc = (uint32_t*)(ws + o_tc);
+  const size_t scan_at = ws_used + o_tc + ((nt * 4 + 255) & ~255ull);
+  SG_HIP(hipMemcpyAsync(dts, ts.data(), nt * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dtc, tc.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_rs_hist, dim3((uint32_t)nt), dim3(kRsThreads), 0, ctx->stream, src, n, shift, (uint32_t)nt, hist,
+                     (const uint64_t*)dts, (const uint32_t*)dtc);
+  int rc = scan_counts(ctx, hist, goff, 256 * nt, scan_at);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_rs_scatter, dim3((uint32_t)nt), dim3(kRsThreads), 0, ctx->stream, src, n, shift, (uint32_t)nt,
+                     (const uint64_t*)goff, dst, (const uint64_t*)dts, (const uint32_t*)dtc);
+  SG_HIP(hipGetLastError());
+  // (the host tables must outlive the copies)
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
+
+// Workspace bytes of radix_pass_runs over n keys in nruns runs.
+size_t radix_pass_runs_ws(uint64_t n, uint64_t nruns) {
+  const uint64_t nt = n / kRsTile + nruns + 1;
+  return ((256 * nt * 4 + 255) & ~255ull) + (((256 * nt + 1) * 8 + 255) & ~255ull) + ((nt * 8 + 255) & ~255ull) +
+         ((nt * 4 + 255) & ~255ull) + scan_ws_bytes(256 * nt);
 }
 
 }  // namespace sg

@@ -88,6 +88,8 @@ struct OwnArgs {
   uint64_t* mask;        // the batch's diff ballots, zeroed: 4 words per chunk
   uint32_t* big;         // [0]: count, then the records left for k_own_big
   uint64_t n;            // elements in the batch (vals[0 .. n) readable)
+  uint32_t* ticket;      // k_own_pipe's next block of 64 records (zeroed)
+  uint32_t dbg;          // diagnostics (SG_OWN_DBG, results wrong): 1 no inserts, 2 no lookups, 4 no chunk loads, 8 no key loads
 };
 
 // The set: 1 << bb buckets of four slots, a key in the first bucket from its
@@ -104,16 +106,18 @@ __device__ __forceinline__ void own_insert(uint32_t* ht, uint32_t bb, uint32_t s
       if (atomicCAS(&ht[4 * b + j], kOwnEmpty, s) == kOwnEmpty) return;
 }
 
-__device__ __forceinline__ uint32_t own_eq_slot(const uint4& v, uint32_t s, uint32_t b, bool& any) {
-  const bool e0 = v.x == s, e1 = v.y == s, e2 = v.z == s, e3 = v.w == s;
-  any = e0 | e1 | e2 | e3;
-  return 4 * b + (e0 ? 0u : e1 ? 1u : e2 ? 2u : 3u);
+// Membership of the lane's four values: the four home buckets read together,
+// straight-line (a bucket holds s iff the min of its slots XOR s is 0); the
+// rare value whose home bucket is full and does not hold it probes on in a
+// loop the wave enters only then.  kSlot: also each hit's slot (4 << bb for
+// the 0xFFFFFFFF signal, held by has_ff).
+__device__ __forceinline__ bool own_has(const uint4& v, uint32_t s) {
+  return min(min(v.x ^ s, v.y ^ s), min(v.z ^ s, v.w ^ s)) == 0u;
+}
+__device__ __forceinline__ uint32_t own_slot(const uint4& v, uint32_t s, uint32_t b) {
+  return 4 * b + (v.x == s ? 0u : v.y == s ? 1u : v.z == s ? 2u : 3u);
 }
 
-// Membership of the lane's four values: the four home buckets read together,
-// straight-line; the rare value whose home bucket is full and does not hold
-// it probes on in a loop the wave enters only then.  kSlot: also each hit's
-// slot (4 << bb for the 0xFFFFFFFF signal, held by has_ff).
 template <bool kSlot>
 __device__ __forceinline__ uint32_t own_probe(const uint32_t* ht, uint32_t bb, bool has_ff, const uint32_t (&x)[4],
                                               uint32_t (&slot)[4]) {
@@ -128,10 +132,9 @@ __device__ __forceinline__ uint32_t own_probe(const uint32_t* ht, uint32_t bb, b
   uint32_t hit = 0, more = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    bool any;
-    const uint32_t sl = own_eq_slot(v[k], x[k], h[k], any);
     const bool ff = x[k] == kOwnEmpty;  // (equal to every empty slot: never stored)
-    if (kSlot) slot[k] = ff ? (4u << bb) : sl;
+    const bool any = own_has(v[k], x[k]);
+    if (kSlot) slot[k] = ff ? (4u << bb) : own_slot(v[k], x[k], h[k]);
     hit |= ((ff ? has_ff : any) ? 1u : 0u) << k;
     more |= (!ff && !any && v[k].w != kOwnEmpty ? 1u : 0u) << k;
   }
@@ -141,11 +144,9 @@ __device__ __forceinline__ uint32_t own_probe(const uint32_t* ht, uint32_t bb, b
       if ((more >> k) & 1u)
         for (uint32_t b = (h[k] + 1) & m;; b = (b + 1) & m) {
           const uint4 w = reinterpret_cast<const uint4*>(ht)[b];
-          bool any;
-          const uint32_t sl = own_eq_slot(w, x[k], b, any);
-          if (any) {
+          if (own_has(w, x[k])) {
             hit |= 1u << k;
-            if (kSlot) slot[k] = sl;
+            if (kSlot) slot[k] = own_slot(w, x[k], b);
             break;
           }
           if (w.w == kOwnEmpty) break;
@@ -177,26 +178,33 @@ __device__ __forceinline__ void own_load(const OwnArgs& a, uint64_t c, int lane,
   }
 }
 
-// the chunk's four ballots into the mask: stored where the chunk lies inside
-// one record (this wave its only writer), OR-ed where it is shared
+// the chunk's four ballots into the mask (lane 0 writes all four; none when
+// all are 0): stored where the chunk lies inside one record (this wave its
+// only writer), OR-ed where it is shared
 __device__ __forceinline__ void own_store(uint64_t* mask, uint64_t c, int lane, uint32_t bits4, bool shared) {
   const uint64_t b0 = __ballot(bits4 & 1u), b1 = __ballot(bits4 & 2u), b2 = __ballot(bits4 & 4u),
                  b3 = __ballot(bits4 & 8u);
-  const uint64_t mine = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-  if (lane < 4 && mine) {
-    if (shared)
-      atomicOr(reinterpret_cast<unsigned long long*>(mask + c * 4 + lane), (unsigned long long)mine);
-    else
-      mask[c * 4 + lane] = mine;
+  if ((b0 | b1 | b2 | b3) == 0) return;
+  if (lane == 0) {
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(mask + c * 4);
+    if (shared) {
+      if (b0) atomicOr(p, (unsigned long long)b0);
+      if (b1) atomicOr(p + 1, (unsigned long long)b1);
+      if (b2) atomicOr(p + 2, (unsigned long long)b2);
+      if (b3) atomicOr(p + 3, (unsigned long long)b3);
+    } else {
+      reinterpret_cast<ulonglong2*>(p)[0] = make_ulonglong2(b0, b1);
+      reinterpret_cast<ulonglong2*>(p)[1] = make_ulonglong2(b2, b3);
+    }
   }
 }
 
 // One chunk of record [lo, hi) (wave-uniform).  pass 0 (dedup): each
 // member's first position per slot; pass 1: the ballots (always OR-ed with
 // kOr: a record swept once per piece of O_r).
-template <bool kDedup, int kPass, bool kOr>
-__device__ __forceinline__ void own_chunk(const OwnArgs& a, const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff,
-                                          int lane, uint64_t lo, uint64_t hi, uint64_t c, const uint32_t (&x)[4]) {
+template <bool kDedup, int kPass>
+__device__ __forceinline__ uint32_t own_hits(const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff, int lane,
+                                             uint64_t lo, uint64_t hi, uint64_t c, const uint32_t (&x)[4]) {
   const uint64_t cs = c * kChunk;
   const bool inner = cs >= lo && cs + kChunk <= hi;
   uint32_t ok = 0xFu;
@@ -223,7 +231,21 @@ __device__ __forceinline__ void own_chunk(const OwnArgs& a, const uint32_t* ht, 
           hit &= ~(1u << k);
       }
   }
-  if (kPass == 1) own_store(a.mask, c, lane, hit, kOr || !inner);
+  return hit;
+}
+
+__device__ __forceinline__ bool own_inner(uint64_t lo, uint64_t hi, uint64_t c) {
+  return c * kChunk >= lo && (c + 1) * kChunk <= hi;
+}
+
+// One chunk of record [lo, hi) (wave-uniform).  pass 0 (dedup): each
+// member's first position per slot; pass 1: the ballots (always OR-ed with
+// kOr: a record swept once per piece of O_r).
+template <bool kDedup, int kPass, bool kOr>
+__device__ __forceinline__ void own_chunk(const OwnArgs& a, const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff,
+                                          int lane, uint64_t lo, uint64_t hi, uint64_t c, const uint32_t (&x)[4]) {
+  const uint32_t hit = own_hits<kDedup, kPass>(ht, pm, bb, has_ff, lane, lo, hi, c, x);
+  if (kPass == 1) own_store(a.mask, c, lane, hit, kOr || !own_inner(lo, hi, c));
 }
 
 // A wave's LDS operations take effect in order; this only keeps the compiler
@@ -232,7 +254,7 @@ __device__ __forceinline__ void own_chunk(const OwnArgs& a, const uint32_t* ht, 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
 constexpr int kOwnKB = 8;  // keys per lane loaded together
-constexpr int kOwnCB = 4;  // chunks loaded together
+constexpr int kOwnCB = 5;  // chunks loaded together (a 1024-entry record spans <= 5)
 
 template <bool kAligned, bool kDedup, int kPass, bool kOr = false>
 __device__ __forceinline__ void own_sweep(const OwnArgs& a, const uint32_t* ht, uint32_t* pm, uint32_t bb, bool has_ff,
@@ -334,6 +356,124 @@ __global__ __launch_bounds__(kOwnWaves * 64) void k_own_wave(OwnArgs a) {
   }
 }
 
+// The flags-and-diff sweep (no dedup).  A wave takes 64 consecutive records
+// at a time: their keys ranges and element ranges come in one coalesced load
+// (a lane per record) and are read per record from registers, so a record
+// costs no dependent global load before its data; its flags go out as one
+// 64-byte store.  Per record: the keys and the first kOwnCB chunks loaded
+// together, the set built, the ballots computed, then the mask words stored
+// (OR-ed into a chunk the record shares with a neighbour).
+template <bool kAligned>
+__device__ __forceinline__ uint32_t own_issue(const OwnArgs& a, int lane, uint32_t p0, uint32_t np, uint64_t elo,
+                                              uint64_t ehi, uint32_t (&kv)[kOwnKB], uint32_t (&x)[kOwnCB][4]) {
+  uint32_t pf = 0;  // chunks loaded
+#pragma unroll
+  for (int j = 0; j < kOwnKB; j++) {
+    const uint32_t i = j * 64 + lane;
+    if (j * 64 < np) kv[j] = i < np ? ((a.dbg & 8) ? i * 0x9E3779B1u : (uint32_t)a.keys[p0 + i]) : 0u;
+  }
+  const uint64_t c0 = elo / kChunk, c1 = (ehi - 1) / kChunk;
+#pragma unroll
+  for (int j = 0; j < kOwnCB; j++)
+    if (c0 + j <= c1 && (c0 + j + 1) * kChunk <= a.n) {
+      if (a.dbg & 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[j][k] = (uint32_t)(c0 + j) * 977u + lane * 4 + k;
+      } else {
+        own_load<kAligned>(a, c0 + j, lane, x[j]);
+      }
+      pf |= 1u << j;
+    }
+  return pf;
+}
+
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ uint64_t lane_get(uint64_t v, int i) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), i) << 32) | __builtin_amdgcn_readlane((uint32_t)v, i);
+}
+
+// the four words of chunk c: stored, or OR-ed into what another wave may hold
+__device__ __forceinline__ void own_put(uint64_t* mask, uint64_t c, const uint64_t (&b)[4], bool shared) {
+  unsigned long long* m = reinterpret_cast<unsigned long long*>(mask + c * 4);
+  if (shared) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (b[k]) atomicOr(m + k, (unsigned long long)b[k]);
+  } else if (b[0] | b[1] | b[2] | b[3]) {
+    reinterpret_cast<ulonglong2*>(m)[0] = make_ulonglong2(b[0], b[1]);
+    reinterpret_cast<ulonglong2*>(m)[1] = make_ulonglong2(b[2], b[3]);
+  }
+}
+
+template <bool kAligned>
+__global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
+  __shared__ alignas(16) uint32_t hts[kOwnWaves][kOwnSlots];
+  static_assert(kOwnWave <= 64 * kOwnKB, "a wave-path record's keys: one batch");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t* ht = hts[w];
+  const uint32_t nblk = (a.nrec + 63) / 64;
+  // blocks by ticket (records own very different amounts of work)
+  for (uint32_t blk = uni32(lane == 0 ? atomicAdd(a.ticket, 1u) : 0u); blk < nblk;
+       blk = uni32(lane == 0 ? atomicAdd(a.ticket, 1u) : 0u)) {
+    const uint32_t R0 = blk * 64, nb = min(64u, a.nrec - R0);
+    uint2 gq = make_uint2(0, 0);
+    uint64_t glo = 0, ghi = 0;
+    if ((uint32_t)lane < nb) {
+      gq = a.po[R0 + lane];
+      glo = a.roff[R0 + lane];
+      ghi = a.roff[R0 + lane + 1];
+    }
+    const uint32_t gnp = gq.y - gq.x;
+    if (gnp > kOwnWave) a.big[1 + atomicAdd(a.big, 1u)] = R0 + lane;
+    if ((uint32_t)lane < nb) a.rec_new[R0 + lane] = gnp ? 1 : 0;  // queued iff it owns a signal (fuzzer.go:678-690)
+    for (int i = 0; i < (int)nb; i++) {
+      const uint32_t p0 = lane_get(gq.x, i), np = lane_get(gq.y, i) - p0;
+      if (!np || np > kOwnWave) continue;
+      const uint64_t elo = a.e0 + lane_get(glo, i), ehi = a.e0 + lane_get(ghi, i);
+      uint32_t kv[kOwnKB], x[kOwnCB][4];
+      const uint32_t pf = own_issue<kAligned>(a, lane, p0, np, elo, ehi, kv, x);
+      const uint64_t c0 = elo / kChunk, c1 = (ehi - 1) / kChunk;
+      uint32_t bb = 4;  // buckets: >= np (load <= 1/4)
+      while ((1u << bb) < np) bb++;
+      const uint32_t size = 4u << bb;
+      for (uint32_t t = 4 * lane; t < size; t += 256)
+        *reinterpret_cast<uint4*>(ht + t) = make_uint4(kOwnEmpty, kOwnEmpty, kOwnEmpty, kOwnEmpty);
+      wave_sync();
+      bool ff = false;
+#pragma unroll
+      for (int j = 0; j < kOwnKB; j++) {
+        if (j * 64 >= np) break;
+        if (j * 64 + lane >= np) continue;
+        if (kv[j] == kOwnEmpty)
+          ff = true;
+        else if (!(a.dbg & 1))
+          own_insert(ht, bb, kv[j]);
+      }
+      const bool has_ff = __ballot(ff) != 0;
+      wave_sync();
+#pragma unroll
+      for (int j = 0; j < kOwnCB; j++)
+        if ((pf >> j) & 1u) {
+          const uint64_t c = c0 + j;
+          const uint32_t hit = (a.dbg & 2) ? (x[j][0] & 15u)
+                                           : own_hits<false, 1>(ht, nullptr, bb, has_ff, lane, elo, ehi, c, x[j]);
+          uint64_t b[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) b[k] = __ballot((hit >> k) & 1u);
+          if (lane == 0 && !(a.dbg & 16)) own_put(a.mask, c, b, !own_inner(elo, ehi, c));
+        }
+      // chunks not loaded ahead (past kOwnCB, or the batch's partial last one): OR-ed
+      for (uint64_t c = c0; c <= c1; c++)
+        if (c - c0 >= (uint64_t)kOwnCB || !((pf >> (c - c0)) & 1u)) {
+          uint32_t y[4];
+          own_load<kAligned>(a, c, lane, y);
+          own_chunk<false, 1, true>(a, ht, nullptr, bb, has_ff, lane, elo, ehi, c, y);
+        }
+      wave_sync();  // (the set is cleared for the next record)
+    }
+  }
+}
+
 // Records owning more than kOwnWave signals: a workgroup each, O_r in pieces
 // of kOwnBigCap signals, each piece a sweep of S_r (two with dedup) whose
 // ballots are OR-ed into the mask.
@@ -381,26 +521,21 @@ __global__ __launch_bounds__(kOwnBigT) void k_own_big(OwnArgs a) {
 }
 
 // [po[r].x, po[r].y): record r's keys (po zeroed: records without keys stay
-// empty), from the run boundaries of each group's sorted keys, kBoundPer
-// consecutive keys per thread
-constexpr int kBoundPer = 8;
-__global__ void k_own_bounds(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ gs,
-                             const unsigned long long* __restrict__ gcnt, uint32_t ng, uint2* __restrict__ po) {
-  const uint32_t g = blockIdx.y;
-  const uint64_t n = gcnt[g], i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kBoundPer;
-  if (g >= ng || i0 >= n) return;
-  const uint64_t* k = keys + gs[g];
-  uint32_t prev = i0 ? (uint32_t)(k[i0 - 1] >> 32) : 0xFFFFFFFFu;
-  uint32_t cur = (uint32_t)(k[i0] >> 32);
-#pragma unroll
-  for (int j = 0; j < kBoundPer; j++) {
-    const uint64_t i = i0 + j;
-    if (i >= n) break;
-    const uint32_t next = i + 1 < n ? (uint32_t)(k[i + 1] >> 32) : 0xFFFFFFFFu;
-    if (cur != prev) po[cur].x = (uint32_t)(gs[g] + i);
-    if (cur != next) po[cur].y = (uint32_t)(gs[g] + i + 1);
-    prev = cur;
-    cur = next;
+// empty), from the run boundaries of the sorted keys: a thread per key
+// against the next one (both loads coalesced)
+__global__ void k_own_bounds(const uint64_t* __restrict__ k, uint64_t n, uint2* __restrict__ po) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t cur = (uint32_t)(k[i] >> 32);
+  if (i == 0) po[cur].x = 0;
+  if (i + 1 == n) {
+    po[cur].y = (uint32_t)n;
+    return;
+  }
+  const uint32_t next = (uint32_t)(k[i + 1] >> 32);
+  if (cur != next) {
+    po[cur].y = (uint32_t)(i + 1);
+    po[next].x = (uint32_t)(i + 1);
   }
 }
 
@@ -799,16 +934,18 @@ static int run_emit(sg_ctx* ctx, const uint32_t* vals, uint64_t n, const uint64_
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // the per-record sweeps of one slice: the wave kernel over the resident grid
-// (each wave takes every grid-th record), then the listed large records
+// (records every grid-th, or blocks of 64 by ticket), then the listed large
+// records
 template <bool kAligned>
 static int launch_own(sg_ctx* ctx, const OwnArgs& oa, uint64_t nr, bool dedup) {
-  const void* kw = dedup ? (const void*)k_own_wave<kAligned, true> : (const void*)k_own_wave<kAligned, false>;
-  const uint32_t wg = std::min<uint32_t>(div_up(nr, kOwnWaves), persistent_grid(ctx, kw, kOwnWaves * 64));
+  const void* kw = dedup ? (const void*)k_own_wave<kAligned, true> : (const void*)k_own_pipe<kAligned>;
+  const uint32_t wg = std::min<uint32_t>(div_up(nr, dedup ? kOwnWaves : 64 * kOwnWaves),
+                                         persistent_grid(ctx, kw, kOwnWaves * 64));
   if (dedup) {
     hipLaunchKernelGGL((k_own_wave<kAligned, true>), dim3(wg), dim3(kOwnWaves * 64), 0, ctx->stream, oa);
     hipLaunchKernelGGL((k_own_big<kAligned, true>), dim3(512), dim3(kOwnBigT), 0, ctx->stream, oa);
   } else {
-    hipLaunchKernelGGL((k_own_wave<kAligned, false>), dim3(wg), dim3(kOwnWaves * 64), 0, ctx->stream, oa);
+    hipLaunchKernelGGL((k_own_pipe<kAligned>), dim3(wg), dim3(kOwnWaves * 64), 0, ctx->stream, oa);
     hipLaunchKernelGGL((k_own_big<kAligned, false>), dim3(512), dim3(kOwnBigT), 0, ctx->stream, oa);
   }
   SG_HIP(hipGetLastError());
@@ -853,7 +990,7 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
     const uint64_t nr = cuts[j + 1] - cuts[j], ns = cuts[j + 3] - cuts[j + 2];
     if (!ns) continue;
     part = std::max(part, al256(std::max<size_t>(bucket_plan_bytes(ns, nr), ns * 8)));
-    tail = std::max(tail, al256(ns * 8) + al256(radix_sort_ws(ns)) + al256(nr * 8) + al256((nr + 2) * 4) +
+    tail = std::max(tail, al256(ns * 8) + al256(std::max(radix_sort_ws(ns), radix_pass_runs_ws(ns, (nr >> 16) + 1))) + al256(nr * 8) + al256((nr + 2) * 4) +
                                al256((nr + 1) * 8) + al256(((nr >> kRecGroupBits) + 1) * 16));
   }
   rc = ws_reserve(ctx, S0 + part + tail);
@@ -869,10 +1006,10 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
     uint64_t* keys_a = (uint64_t*)ws_at(ctx, at);
     at += al256(ns * 8);
     const size_t sort_at = at;
-    at += al256(radix_sort_ws(ns));
+    at += al256(std::max(radix_sort_ws(ns), radix_pass_runs_ws(ns, (nr >> 16) + 1)));
     uint2* po = (uint2*)ws_at(ctx, at);
     at += al256(nr * 8);
-    uint32_t* big = (uint32_t*)ws_at(ctx, at);
+    uint32_t* big = (uint32_t*)ws_at(ctx, at);  // count, records, ticket
     at += al256((nr + 2) * 4);
     uint64_t* roff = (uint64_t*)ws_at(ctx, at);
     at += al256((nr + 1) * 8);
@@ -889,28 +1026,42 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
     std::vector<uint64_t> gh(2 * (size_t)ng);  // counts, starts
     SG_HIP(hipMemcpyAsync(gh.data(), gcur, gh.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
+    // the pairs by record: two stable passes over the record's low 16 bits,
+    // the first reading the groups' runs in group order, so equal low bits
+    // keep group order and every record's pairs end up together (records in
+    // (low 16 bits, group) order)
+    std::vector<uint64_t> rs, rc_;
+    uint64_t np = 0;
+    for (uint32_t g = 0; g < ng; g++)
+      if (gh[g]) {
+        rs.push_back(gh[ng + g]);
+        rc_.push_back(gh[g]);
+        np += gh[g];
+      }
+    uint64_t* sorted = keys_b;
     {
-      // each group's pairs by record: the record's low 16 bits, two passes
-      // (the group itself is the bucket stage's placement), back in keys_a
       ScopedTimer tm(ctx, "owned_sort");
-      for (uint32_t g = 0; g < ng; g++) {
-        const uint64_t cnt = gh[g], st = gh[ng + g];
-        if (cnt < 2) continue;
-        uint64_t* sorted = nullptr;
-        rc = radix_sort_u64(ctx, keys_a + st, keys_b + st, cnt, sort_at, &sorted, 0xFFFFull << 32);
+      if (np >= 2) {
+        rc = radix_pass_runs(ctx, keys_a, rs, rc_, 32, keys_b, sort_at);
         if (rc) return rc;
-        if (sorted != keys_a + st)
-          SG_HIP(hipMemcpyAsync(keys_a + st, sorted, cnt * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        rc = radix_sort_u64(ctx, keys_b, keys_a, np, sort_at, &sorted, 0xFF00ull << 32);
+        if (rc) return rc;
+      } else if (np == 1) {
+        SG_HIP(hipMemcpyAsync(keys_b, keys_a + rs[0], 8, hipMemcpyDeviceToDevice, ctx->stream));
       }
     }
     ScopedTimer tm(ctx, "owned_sweep");
-    uint64_t gmax = 0;
-    for (uint32_t g = 0; g < ng; g++) gmax = std::max<uint64_t>(gmax, gh[g]);
     SG_HIP(hipMemsetAsync(po, 0, nr * 8, ctx->stream));
-    if (gmax)
-      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(gmax, 256 * kBoundPer), ng), dim3(256), 0, ctx->stream,
-                         (const uint64_t*)keys_a, (const uint64_t*)gs, (const unsigned long long*)gcur, ng, po);
-    OwnArgs oa{d_vals, roff, e0, (uint32_t)nr, keys_a, po, d_rec_new ? d_rec_new + r0 : nullptr, s.dmask, big, nvals};
+    if (np)
+      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(np, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)sorted, np,
+                         po);
+    static const uint32_t own_dbg = [] {
+      const char* e = getenv("SG_OWN_DBG");
+      return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    OwnArgs oa{d_vals, roff, e0, (uint32_t)nr, sorted, po, d_rec_new ? d_rec_new + r0 : nullptr, s.dmask, big, nvals,
+               big + nr + 1, own_dbg};
+    SG_HIP(hipMemsetAsync(big + nr + 1, 0, 4, ctx->stream));
     if (aligned)
       rc = launch_own<true>(ctx, oa, nr, dedup);
     else
