@@ -358,50 +358,43 @@ __global__ __launch_bounds__(kOwnWaves * 64) void k_own_wave(OwnArgs a) {
 
 // The flags-and-diff sweep (no dedup).  A wave takes 64 consecutive records
 // at a time: their keys ranges and element ranges come in one coalesced load
-// (a lane per record) and are read per record from registers, so a record
-// costs no dependent global load before its data; its flags go out as one
-// 64-byte store.  Per record: the keys and the first kOwnCB chunks loaded
-// together, the set built, the ballots computed, then the mask words stored
-// (OR-ed into a chunk the record shares with a neighbour).
-template <bool kAligned>
-__device__ __forceinline__ uint32_t own_issue(const OwnArgs& a, int lane, uint32_t p0, uint32_t np, uint64_t elo,
-                                              uint64_t ehi, uint32_t (&kv)[kOwnKB], uint32_t (&x)[kOwnCB][4]) {
-  uint32_t pf = 0;  // chunks loaded
-#pragma unroll
-  for (int j = 0; j < kOwnKB; j++) {
-    const uint32_t i = j * 64 + lane;
-    if (j * 64 < np) kv[j] = i < np ? ((a.dbg & 8) ? i * 0x9E3779B1u : (uint32_t)a.keys[p0 + i]) : 0u;
-  }
-  const uint64_t c0 = elo / kChunk, c1 = (ehi - 1) / kChunk;
-#pragma unroll
-  for (int j = 0; j < kOwnCB; j++)
-    if (c0 + j <= c1 && (c0 + j + 1) * kChunk <= a.n) {
-      if (a.dbg & 4) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) x[j][k] = (uint32_t)(c0 + j) * 977u + lane * 4 + k;
-      } else {
-        own_load<kAligned>(a, c0 + j, lane, x[j]);
-      }
-      pf |= 1u << j;
-    }
-  return pf;
-}
-
+// (a lane per record) and their flags go out as one 64-byte store.  The
+// records of the block it decides here (owning 1 .. kOwnWave signals, spanning
+// <= kOwnCB chunks, not the batch's partial last chunk; the rest are listed for
+// k_own_big) are software-pipelined: the next record's keys and chunks are
+// loaded before this record is decided, and every record issues the same
+// memory instructions (kOwnKB + kOwnCB loads, clamped to readable addresses
+// when unused; one 64-lane atomic OR of its mask words), so the compiler's
+// wait for a record's loads leaves the next record's loads and the previous
+// record's OR in flight.
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
 __device__ __forceinline__ uint64_t lane_get(uint64_t v, int i) {
   return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), i) << 32) | __builtin_amdgcn_readlane((uint32_t)v, i);
 }
 
-// the four words of chunk c: stored, or OR-ed into what another wave may hold
-__device__ __forceinline__ void own_put(uint64_t* mask, uint64_t c, const uint64_t (&b)[4], bool shared) {
-  unsigned long long* m = reinterpret_cast<unsigned long long*>(mask + c * 4);
-  if (shared) {
+struct OwnSet {
+  uint32_t kv[kOwnKB];
+  uint32_t x[kOwnCB][4];
+};
+
+template <bool kAligned>
+__device__ __forceinline__ void own_fetch(const OwnArgs& a, int lane, uint32_t p0, uint32_t np, uint64_t c0,
+                                          uint64_t c1, OwnSet& d) {
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (b[k]) atomicOr(m + k, (unsigned long long)b[k]);
-  } else if (b[0] | b[1] | b[2] | b[3]) {
-    reinterpret_cast<ulonglong2*>(m)[0] = make_ulonglong2(b[0], b[1]);
-    reinterpret_cast<ulonglong2*>(m)[1] = make_ulonglong2(b[2], b[3]);
+  for (int j = 0; j < kOwnKB; j++) d.kv[j] = (uint32_t)a.keys[p0 + min((uint32_t)(j * 64 + lane), np - 1)];
+#pragma unroll
+  for (int j = 0; j < kOwnCB; j++) {
+    const uint64_t p = min(c0 + j, c1) * kChunk + 4 * (uint64_t)lane;
+    if (kAligned) {
+      const uint4 q = *reinterpret_cast<const uint4*>(a.vals + p);
+      d.x[j][0] = q.x;
+      d.x[j][1] = q.y;
+      d.x[j][2] = q.z;
+      d.x[j][3] = q.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) d.x[j][k] = a.vals[p + k];
+    }
   }
 }
 
@@ -409,9 +402,11 @@ template <bool kAligned>
 __global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
   __shared__ alignas(16) uint32_t hts[kOwnWaves][kOwnSlots];
   static_assert(kOwnWave <= 64 * kOwnKB, "a wave-path record's keys: one batch");
+  static_assert(4 * kOwnCB <= 64, "a record's mask words: one per lane");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t* ht = hts[w];
   const uint32_t nblk = (a.nrec + 63) / 64;
+  const uint64_t nfull = a.n / kChunk;  // chunks wholly inside the batch
   // blocks by ticket (records own very different amounts of work)
   for (uint32_t blk = uni32(lane == 0 ? atomicAdd(a.ticket, 1u) : 0u); blk < nblk;
        blk = uni32(lane == 0 ? atomicAdd(a.ticket, 1u) : 0u)) {
@@ -420,19 +415,28 @@ __global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
     uint64_t glo = 0, ghi = 0;
     if ((uint32_t)lane < nb) {
       gq = a.po[R0 + lane];
-      glo = a.roff[R0 + lane];
-      ghi = a.roff[R0 + lane + 1];
+      glo = a.e0 + a.roff[R0 + lane];
+      ghi = a.e0 + a.roff[R0 + lane + 1];
     }
     const uint32_t gnp = gq.y - gq.x;
-    if (gnp > kOwnWave) a.big[1 + atomicAdd(a.big, 1u)] = R0 + lane;
     if ((uint32_t)lane < nb) a.rec_new[R0 + lane] = gnp ? 1 : 0;  // queued iff it owns a signal (fuzzer.go:678-690)
-    for (int i = 0; i < (int)nb; i++) {
-      const uint32_t p0 = lane_get(gq.x, i), np = lane_get(gq.y, i) - p0;
-      if (!np || np > kOwnWave) continue;
-      const uint64_t elo = a.e0 + lane_get(glo, i), ehi = a.e0 + lane_get(ghi, i);
-      uint32_t kv[kOwnKB], x[kOwnCB][4];
-      const uint32_t pf = own_issue<kAligned>(a, lane, p0, np, elo, ehi, kv, x);
-      const uint64_t c0 = elo / kChunk, c1 = (ehi - 1) / kChunk;
+    const uint64_t gc0 = glo / kChunk, gc1 = gnp ? (ghi - 1) / kChunk : gc0;
+    const bool mine = gnp && gnp <= kOwnWave && gc1 - gc0 < (uint64_t)kOwnCB && gc1 < nfull;
+    if (gnp && !mine) a.big[1 + atomicAdd(a.big, 1u)] = R0 + lane;
+    uint64_t vm = __ballot(mine);
+    if (!vm) continue;
+    int i = __builtin_ctzll(vm);
+    vm &= vm - 1;
+    OwnSet A, B;
+    own_fetch<kAligned>(a, lane, lane_get(gq.x, i), lane_get(gnp, i), lane_get(gc0, i), lane_get(gc1, i), A);
+    for (;;) {
+      const bool more = vm != 0;
+      const int in = more ? __builtin_ctzll(vm) : i;  // (no next record: this one's loads again)
+      vm &= vm - 1;
+      own_fetch<kAligned>(a, lane, lane_get(gq.x, in), lane_get(gnp, in), lane_get(gc0, in), lane_get(gc1, in), B);
+      // decide record i from A
+      const uint32_t np = lane_get(gnp, i);
+      const uint64_t elo = lane_get(glo, i), ehi = lane_get(ghi, i), c0 = lane_get(gc0, i), c1 = lane_get(gc1, i);
       uint32_t bb = 4;  // buckets: >= np (load <= 1/4)
       while ((1u << bb) < np) bb++;
       const uint32_t size = 4u << bb;
@@ -444,32 +448,34 @@ __global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
       for (int j = 0; j < kOwnKB; j++) {
         if (j * 64 >= np) break;
         if (j * 64 + lane >= np) continue;
-        if (kv[j] == kOwnEmpty)
+        if (A.kv[j] == kOwnEmpty)
           ff = true;
         else if (!(a.dbg & 1))
-          own_insert(ht, bb, kv[j]);
+          own_insert(ht, bb, A.kv[j]);
       }
       const bool has_ff = __ballot(ff) != 0;
       wave_sync();
+      // lane 4 j + k ORs word k of chunk c0 + j (past c1: 0 into chunk c1)
+      uint64_t word = 0;
 #pragma unroll
       for (int j = 0; j < kOwnCB; j++)
-        if ((pf >> j) & 1u) {
-          const uint64_t c = c0 + j;
-          const uint32_t hit = (a.dbg & 2) ? (x[j][0] & 15u)
-                                           : own_hits<false, 1>(ht, nullptr, bb, has_ff, lane, elo, ehi, c, x[j]);
-          uint64_t b[4];
+        if (c0 + j <= c1) {
+          const uint32_t hit = (a.dbg & 2) ? (A.x[j][0] & 15u)
+                                           : own_hits<false, 1>(ht, nullptr, bb, has_ff, lane, elo, ehi, c0 + j, A.x[j]);
 #pragma unroll
-          for (int k = 0; k < 4; k++) b[k] = __ballot((hit >> k) & 1u);
-          if (lane == 0 && !(a.dbg & 16)) own_put(a.mask, c, b, !own_inner(elo, ehi, c));
+          for (int k = 0; k < 4; k++) {
+            const uint64_t bk = __ballot((hit >> k) & 1u);
+            word = lane == 4 * j + k ? bk : word;
+          }
         }
-      // chunks not loaded ahead (past kOwnCB, or the batch's partial last one): OR-ed
-      for (uint64_t c = c0; c <= c1; c++)
-        if (c - c0 >= (uint64_t)kOwnCB || !((pf >> (c - c0)) & 1u)) {
-          uint32_t y[4];
-          own_load<kAligned>(a, c, lane, y);
-          own_chunk<false, 1, true>(a, ht, nullptr, bb, has_ff, lane, elo, ehi, c, y);
-        }
+      const uint64_t cj = min(c0 + (uint64_t)(lane >> 2), c1);
+      if (!(a.dbg & 16))
+        atomicOr(reinterpret_cast<unsigned long long*>(a.mask + cj * 4 + (lane & 3)),
+                 (unsigned long long)(lane < 4 * kOwnCB ? word : 0ull));
       wave_sync();  // (the set is cleared for the next record)
+      if (!more) break;
+      A = B;
+      i = in;
     }
   }
 }
@@ -521,21 +527,28 @@ __global__ __launch_bounds__(kOwnBigT) void k_own_big(OwnArgs a) {
 }
 
 // [po[r].x, po[r].y): record r's keys (po zeroed: records without keys stay
-// empty), from the run boundaries of the sorted keys: a thread per key
-// against the next one (both loads coalesced)
-__global__ void k_own_bounds(const uint64_t* __restrict__ k, uint64_t n, uint2* __restrict__ po) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t cur = (uint32_t)(k[i] >> 32);
-  if (i == 0) po[cur].x = 0;
-  if (i + 1 == n) {
-    po[cur].y = (uint32_t)n;
-    return;
+// empty), from the run boundaries of the sorted keys: each key against the
+// next one, kBoundPer keys per thread a block apart (all loads coalesced)
+constexpr int kBoundPer = 8;
+__global__ __launch_bounds__(256) void k_own_bounds(const uint64_t* __restrict__ k, uint64_t n,
+                                                    uint2* __restrict__ po) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * (256 * kBoundPer) + threadIdx.x;
+  uint32_t cur[kBoundPer], nxt[kBoundPer];
+#pragma unroll
+  for (int j = 0; j < kBoundPer; j++) {
+    const uint64_t i = i0 + 256 * j;
+    cur[j] = i < n ? (uint32_t)(k[i] >> 32) : 0u;
+    nxt[j] = i + 1 < n ? (uint32_t)(k[i + 1] >> 32) : 0xFFFFFFFFu;
   }
-  const uint32_t next = (uint32_t)(k[i + 1] >> 32);
-  if (cur != next) {
-    po[cur].y = (uint32_t)(i + 1);
-    po[next].x = (uint32_t)(i + 1);
+#pragma unroll
+  for (int j = 0; j < kBoundPer; j++) {
+    const uint64_t i = i0 + 256 * j;
+    if (i >= n) break;
+    if (i == 0) po[cur[j]].x = 0;
+    if (cur[j] != nxt[j]) {
+      po[cur[j]].y = (uint32_t)(i + 1);
+      if (i + 1 < n) po[nxt[j]].x = (uint32_t)(i + 1);
+    }
   }
 }
 
@@ -1053,8 +1066,8 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
     ScopedTimer tm(ctx, "owned_sweep");
     SG_HIP(hipMemsetAsync(po, 0, nr * 8, ctx->stream));
     if (np)
-      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(np, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)sorted, np,
-                         po);
+      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(np, 256 * kBoundPer)), dim3(256), 0, ctx->stream,
+                         (const uint64_t*)sorted, np, po);
     static const uint32_t own_dbg = [] {
       const char* e = getenv("SG_OWN_DBG");
       return e ? (uint32_t)atoi(e) : 0u;

@@ -637,16 +637,20 @@ def test_exec_signal_region_boundaries_vs_oracle(C):
     """Signals crowded onto the slots where the slot-region kernel's lanes meet
     (home % 128 in 124..127 and 0..3, table wrap-around 8189..8191 -> 0..2), a
     few distinct high parts so probe windows fill and home slots get
-    overwritten, the zero signal, repeats, empty calls: every window's
-    decisions in program order, as executor.h:507-526 takes them."""
+    overwritten, the zero signal, repeats, empty calls, high parts up to
+    0xFFFFE000 (the table keeps 22-bit slot codes): every window's decisions
+    in program order, as executor.h:507-526 takes them."""
     rng = np.random.default_rng(117)
     homes = np.array([(r * 128 + d) % 8192 for r in (0, 1, 2, 31, 63) for d in range(-4, 4)], np.uint64)
-    for nprog, calls, pcs, nhigh in [(2, 3, 700, 3), (6, 4, 1500, 6), (3, 2, 5000, 40)]:
+    for nprog, calls, pcs, nhigh, top in [(2, 3, 700, 3, False), (6, 4, 1500, 6, False), (3, 2, 5000, 40, False),
+                                          (4, 3, 1500, 5, True)]:
         lens = rng.integers(1, 2 * pcs, size=nprog * calls).astype(np.uint64)
         lens[rng.random(lens.size) < 0.2] = 0  # empty calls between full ones
         call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
         n = int(call_off[-1])
         hi = rng.integers(0, nhigh, size=n).astype(np.uint64) * 8192 + 8192 * 977
+        if top:  # the largest high parts (s >> 13 near 2^19: the 22-bit slot codes' top values)
+            hi = ((1 << 19) - 1 - rng.integers(0, nhigh, size=n).astype(np.uint64)) * 8192
         sigs = (hi + rng.choice(homes, size=n)) & 0xFFFFFFFF
         sigs[rng.random(n) < 0.02] = 0
         far = rng.random(n) < 0.3  # anywhere in the table
