@@ -1187,7 +1187,10 @@ __device__ __forceinline__ bool map_insert(uint32_t* ht, uint32_t sl, uint32_t r
 __device__ __forceinline__ uint32_t take_ticket(uint32_t* p) { return atomicAdd(p, 1u); }
 __device__ __forceinline__ void take_wait(uint32_t&) {}
 
-template <bool kDbg, bool kEmit>
+// kEmit: 0 flags and set updates, 1 candidate pairs (counted per owning
+// shard), 2 the ordered outputs' new-signal pairs, group-major, with the set
+// updates
+template <bool kDbg, int kEmit>
 __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWaves))) void k_bucket(BucketArgs a) {
   __shared__ uint32_t mslice[kBucketWords];
   __shared__ uint32_t nbits[kBucketWords];
@@ -1196,14 +1199,14 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
   __shared__ uint32_t sh_fail;         // some insert found the map full: the bucket spills
   __shared__ uint32_t sh_b[2];
   __shared__ uint4 sh_q[2];
-  __shared__ uint32_t shcnt[kEmit ? kMaxShards : 1];  // emitted pairs per owning shard
-  __shared__ uint32_t lcnt[kEmit ? kMaxGroups : 1];   // group-major emission: pairs per record group ...
-  __shared__ unsigned long long lbase[kEmit ? kMaxGroups : 1];  // ... and where they go
+  __shared__ uint32_t shcnt[kEmit == 1 ? kMaxShards : 1];  // emitted pairs per owning shard
+  __shared__ uint32_t lcnt[kEmit == 2 ? kMaxGroups : 1];    // group-major emission: pairs per record group ...
+  __shared__ unsigned long long lbase[kEmit == 2 ? kMaxGroups : 1];  // ... and where they go
   const int tid = threadIdx.x;
-  if (kEmit) {
+  if (kEmit == 1)
     for (uint32_t i = tid; i < kMaxShards; i += kBThreads) shcnt[i] = 0;
+  if (kEmit == 2)
     for (uint32_t i = tid; i < kMaxGroups; i += kBThreads) lcnt[i] = 0;
-  }
   const uint32_t NG = a.NG;
   constexpr uint32_t kRound = kBThreads * kBU;
   // diagnostics (kDbg): block span, buckets, rounds, cycles per phase as wave 0 sees them
@@ -1269,7 +1272,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       take_wait(pend_t);  // (taken a bucket ago; the install waited for older loads already)
       pend_b = list_bucket(a, 2 * gridDim.x + pend_t, nl, &pend_q);
       pend_t = take_ticket(a.ticket);
-      if (kEmit) take_wait(pend_t);  // (this form spills; a spilled ticket must have landed)
+      if (kEmit) take_wait(pend_t);
       sh_fail = 0;  // (every wave read the previous bucket's before the barrier above)
     }
     lds_barrier();
@@ -1429,25 +1432,37 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
       if (tid == 0) a.spill[atomicAdd(a.nspill, 1u)] = b;
       for (uint32_t i = tid; i < kHash; i += kBThreads) ht[i] = kEmpty;
       for (uint32_t i = tid; i < kBucketWords; i += kBThreads) nbits[i] = 0;
-    } else if (kEmit && a.gcur) {
-      // the ordered outputs: every new signal with its first record, group-major
+    } else if (kEmit == 2) {
+      // the ordered outputs: every new signal with its first record,
+      // group-major (the slots read twice: counted per group, then placed;
+      // order inside a group is free, the pairs are sorted by record later)
       constexpr int kOwn = kHash / kBThreads;
-      uint32_t sg[kOwn], rc[kOwn];
+#pragma unroll
+      for (int k = 0; k < kOwn; k++) {
+        const uint32_t v = ht[k * kBThreads + tid];
+        if (v != kEmpty) {
+          atomicAdd(&lcnt[(v & kRecMask) >> kGroupBits], 1u);
+          const uint32_t sl = map_signal(k * kBThreads + tid, v);
+          atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+        }
+      }
+      __syncthreads();
+      for (uint32_t g = tid; g < a.NG; g += kBThreads) {
+        const uint32_t c = lcnt[g];
+        lbase[g] = c ? a.goff[(uint64_t)g << kGroupBits] + atomicAdd(&a.gcur[g], (unsigned long long)c) : 0ull;
+        lcnt[g] = 0;
+      }
+      __syncthreads();
 #pragma unroll
       for (int k = 0; k < kOwn; k++) {
         const uint32_t i = k * kBThreads + tid;
         const uint32_t v = ht[i];
-        rc[k] = kEmpty;
-        sg[k] = 0;
         if (v != kEmpty) {
-          const uint32_t sl = map_signal(i, v);
-          sg[k] = part_sig((b << 16) | sl);
-          rc[k] = v & kRecMask;
-          atomicOr(&nbits[sl >> 5], 1u << (sl & 31));
+          const uint32_t r = v & kRecMask, g = r >> kGroupBits;
+          a.pairs[lbase[g] + atomicAdd(&lcnt[g], 1u)] = make_uint2(part_sig((b << 16) | map_signal(i, v)), r);
           ht[i] = kEmpty;
         }
       }
-      emit_grouped(a, sg, rc, lcnt, lbase);  // (its barriers also complete nbits)
       const wvec nb = reinterpret_cast<const wvec*>(nbits)[tid];
       const wvec mw = reinterpret_cast<const wvec*>(mslice)[tid];
       const uint64_t w0 = bucket_word(b, kWPT * tid);
@@ -1458,7 +1473,9 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
           if (a.nwords) a.nwords[w0 + j] = ns[j] | nb[j];
         }
       reinterpret_cast<wvec*>(nbits)[tid] = wvec{};
-    } else if (kEmit) {
+      __syncthreads();  // (every placement read its lcnt before the reset)
+      for (uint32_t g = tid; g < a.NG; g += kBThreads) lcnt[g] = 0;
+    } else if (kEmit == 1) {
       // every distinct candidate of the bucket with its first record: the
       // thread's occupied slots counted, one block scan and one global
       // atomic for the bucket's run of pairs, then the slots re-read and
@@ -1580,7 +1597,7 @@ __global__ __launch_bounds__(kBThreads) __attribute__((amdgpu_waves_per_eu(kBWav
 #pragma unroll
     for (int u = 0; u < kBU; u++) x[u] = y[u];
   }
-  if (kEmit) {
+  if (kEmit == 1) {
     __syncthreads();
     flush_shard_counts(a, shcnt);
   }
@@ -2059,7 +2076,7 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
     ba.gcur = emit->gcur;
     ba.goff = emit->goff;
   }
-  uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, false>, kBThreads);
+  uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, 0>, kBThreads);
   // diagnostics: SG_BUCKET_BLOCKS caps the persistent grid (leaves CUs to
   // kernels on other streams)
   static const uint32_t cap_blocks = [] {
@@ -2079,12 +2096,14 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
   ba.nlist = blpos + kNumBuckets;
   {
     ScopedTimer tm(ctx, "bucket_triage");
-    if (emit)
-      hipLaunchKernelGGL((k_bucket<false, true>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+    if (emit && emit->gcur)
+      hipLaunchKernelGGL((k_bucket<false, 2>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+    else if (emit)
+      hipLaunchKernelGGL((k_bucket<false, 1>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
     else if (dbg)
-      hipLaunchKernelGGL((k_bucket<true, false>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+      hipLaunchKernelGGL((k_bucket<true, 0>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
     else
-      hipLaunchKernelGGL((k_bucket<false, false>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
+      hipLaunchKernelGGL((k_bucket<false, 0>), dim3(bgrid), dim3(kBThreads), 0, ctx->stream, ba);
   }
   {
     ScopedTimer tm(ctx, "bucket_spill");

@@ -399,12 +399,14 @@ __device__ __forceinline__ void own_fetch(const OwnArgs& a, int lane, uint32_t p
 }
 
 template <bool kAligned>
-__global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
+__global__ __launch_bounds__(kOwnWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_own_pipe(OwnArgs a) {
   __shared__ alignas(16) uint32_t hts[kOwnWaves][kOwnSlots];
+  __shared__ alignas(16) uint32_t hcs[kOwnWaves][kOwnSlots / 4];  // keys per bucket
   static_assert(kOwnWave <= 64 * kOwnKB, "a wave-path record's keys: one batch");
   static_assert(4 * kOwnCB <= 64, "a record's mask words: one per lane");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t* ht = hts[w];
+  uint32_t* hc = hcs[w];
   const uint32_t nblk = (a.nrec + 63) / 64;
   const uint64_t nfull = a.n / kChunk;  // chunks wholly inside the batch
   // blocks by ticket (records own very different amounts of work)
@@ -442,16 +444,28 @@ __global__ __launch_bounds__(kOwnWaves * 64) void k_own_pipe(OwnArgs a) {
       const uint32_t size = 4u << bb;
       for (uint32_t t = 4 * lane; t < size; t += 256)
         *reinterpret_cast<uint4*>(ht + t) = make_uint4(kOwnEmpty, kOwnEmpty, kOwnEmpty, kOwnEmpty);
+      for (uint32_t t = 4 * lane; t < (1u << bb); t += 256) *reinterpret_cast<uint4*>(hc + t) = make_uint4(0, 0, 0, 0);
       wave_sync();
+      // inserts by counting: a key takes the next slot of its home bucket
+      // (one LDS round trip, no compare-and-swap retries), the next bucket's
+      // when it is full -- the buckets still fill in slot order
       bool ff = false;
 #pragma unroll
       for (int j = 0; j < kOwnKB; j++) {
         if (j * 64 >= np) break;
         if (j * 64 + lane >= np) continue;
-        if (A.kv[j] == kOwnEmpty)
+        if (A.kv[j] == kOwnEmpty) {
           ff = true;
-        else if (!(a.dbg & 1))
-          own_insert(ht, bb, A.kv[j]);
+        } else if (!(a.dbg & 1)) {
+          const uint32_t m = (1u << bb) - 1;
+          for (uint32_t b = own_home(A.kv[j], bb);; b = (b + 1) & m) {
+            const uint32_t at = atomicAdd(&hc[b], 1u);
+            if (at < 4) {
+              ht[4 * b + at] = A.kv[j];
+              break;
+            }
+          }
+        }
       }
       const bool has_ff = __ballot(ff) != 0;
       wave_sync();
