@@ -55,21 +55,16 @@ using sgd::exec_hash;  // executor.h:497-505
 // across it).  39 KiB of LDS: four programs per CU.  (Measured and removed in
 // r05: a speculative one-wave kernel -- every edge of a window probes at
 // once, the decided prefix commits -- 1.96 ms per 134M PCs against 1.51, a
-// one-wave slot-region kernel 2.01 ms, 2 or 4 deciding waves 1.59 / 3.09 ms.)
+// one-wave slot-region kernel 2.01 ms, 2 or 4 deciding waves 1.59 / 3.09 ms.
+// Also measured in r05: the table as 22-bit slot codes -- a signal's low 13
+// bits are implied by its slot and probe offset -- in a 16-bit and an 8-bit
+// array, 24 KiB, five programs per CU: steady flags + queued lists 14.3 ->
+// 18.3 ms, executor-exact C2 from traces 19.9 -> 27.3 ms; each deciding step
+// then reads eight LDS values instead of four, on the critical chain.)
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// The dedup table's slot for signal s at probe offset j (slot (s + j) % 8192,
-// executor.h:510): s's low 13 bits are implied by the slot and j, so the slot
-// keeps (s >> 13, j) as the 22-bit code ((s >> 13) << 2 | j) + 1, 0 = empty.
-// The reference's empty marker is the signal 0 itself (executor.h:513 finds
-// 0 == sig in an empty slot), so code_of(0, j) = 0: equal codes <=> equal
-// table values, empty slots included.
-__device__ __forceinline__ uint32_t code_of(uint32_t s, uint32_t j) {
-  return s ? (((s >> 13) << 2) | j) + 1u : 0u;
-}
 
 template <int K>
 __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict__ pcs,
@@ -78,13 +73,8 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
                                                       uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
                                                       const uint8_t* __restrict__ emit) {
   constexpr int W = 64 * K;
-  // the dedup table as 22-bit slot codes (code_of), low 16 bits and high 6
-  // bits in two arrays: 24 KiB where the signals themselves took 32 KiB, so
-  // five programs fit a CU instead of four; + mirror of slots 0..2, dummy slot 8196
-  __shared__ alignas(16) uint16_t tlo[kDedupSize + 8];
-  __shared__ alignas(16) uint8_t thi[kDedupSize + 8];
-  __shared__ uint32_t wsig[2][W];                   // signal, region-major ...
-  __shared__ uint8_t wpos[2][W];                    // ... and its position in the window
+  __shared__ uint32_t table[kDedupSize + 8];        // + mirror of slots 0..2, dummy slot 8196
+  __shared__ unsigned long long wlist[2][W];        // position << 32 | signal, region-major
   __shared__ uint32_t wbc[2][64];                   // region lane: base << 16 | count
   __shared__ uint32_t wlive[2];                     // buffer holds a window to decide
   __shared__ unsigned long long wmask[K][64];       // producer scratch
@@ -94,8 +84,7 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
   const uint64_t p = blockIdx.x;
   const uint64_t c0 = prog_off[p], c1 = pstop ? pstop[p] : prog_off[p + 1];
   if (c1 <= c0) return;
-  for (uint32_t i = tid; i < (kDedupSize + 8) / 2; i += 128) reinterpret_cast<uint32_t*>(tlo)[i] = 0;
-  for (uint32_t i = tid; i < (kDedupSize + 8) / 4; i += 128) reinterpret_cast<uint32_t*>(thi)[i] = 0;
+  for (uint32_t i = tid; i < kDedupSize + 8; i += 128) table[i] = 0;
   if (prod) {
 #pragma unroll
     for (int k = 0; k < K; k++) wmask[k][lane] = 0;
@@ -213,11 +202,8 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
 #pragma unroll
     for (int k = 0; k < K; k++) {
       const uint32_t at = (uint32_t)__shfl((int)(base + rowb[k]), (int)rg[k]);
-      if (64 * k + lane < nv) {
-        const uint32_t j = at + (uint32_t)__popcll(em_[k] & lt);
-        wsig[nb][j] = sb[k];
-        wpos[nb][j] = (uint8_t)(64u * k + lane);
-      }
+      if (64 * k + lane < nv)
+        wlist[nb][at + (uint32_t)__popcll(em_[k] & lt)] = ((unsigned long long)(64u * k + lane) << 32) | sb[k];
     }
     wbc[nb][lane] = (base << 16) | n_r;
     if (lane == 0) wlive[nb] = 1;
@@ -252,8 +238,9 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
         const uint32_t bcw = wbc[buf][lane];
         const uint32_t base = bcw >> 16, iend = base + (bcw & 0xFFFFu);
         uint32_t i = base;
-        uint32_t pos = i < iend ? (uint32_t)wpos[buf][i] : kNoPos;
-        uint32_t s = wsig[buf][i < iend ? i : 0];
+        unsigned long long cur = wlist[buf][i < iend ? i : 0];
+        uint32_t pos = i < iend ? (uint32_t)(cur >> 32) : kNoPos;
+        uint32_t s = (uint32_t)cur;
         while (__ballot(pos != kNoPos)) {
           const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
           const uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
@@ -261,30 +248,21 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
           const bool go = (pos != kNoPos) & ((hr > 2u) | (left > pos)) & ((hr < 125u) | (right > pos));
           const uint32_t i2 = i + (go ? 1u : 0u);
           const uint32_t home = s & (kDedupSize - 1);
-          // slot codes of the four probe slots (the next entry read with them)
-          const uint32_t t0 = tlo[home] | ((uint32_t)thi[home] << 16), t1 = tlo[home + 1] | ((uint32_t)thi[home + 1] << 16);
-          const uint32_t t2 = tlo[home + 2] | ((uint32_t)thi[home + 2] << 16);
-          const uint32_t t3 = tlo[home + 3] | ((uint32_t)thi[home + 3] << 16);
-          const uint32_t ni = i2 < iend ? i2 : 0;
-          const uint32_t npos = wpos[buf][ni], nsig = wsig[buf][ni];
-          // s at probe offset j has code code_of(s, j): equal codes <=> equal signals
-          const uint32_t e0 = code_of(s, 0), e1 = code_of(s, 1), e2 = code_of(s, 2), e3 = code_of(s, 3);
-          const bool h0 = (t0 == e0) | (t0 == 0u), h1 = (t1 == e1) | (t1 == 0u), h2 = (t2 == e2) | (t2 == 0u);
-          const bool h3 = (t3 == e3) | (t3 == 0u);
+          const uint32_t t0 = table[home], t1 = table[home + 1], t2 = table[home + 2], t3 = table[home + 3];
+          const unsigned long long nx = wlist[buf][i2 < iend ? i2 : 0];
+          const bool h0 = (t0 == s) | (t0 == 0u), h1 = (t1 == s) | (t1 == 0u), h2 = (t2 == s) | (t2 == 0u);
+          const bool h3 = (t3 == s) | (t3 == 0u);
           const uint32_t q = h0 ? 0u : h1 ? 1u : h2 ? 2u : h3 ? 3u : 0u;
-          const bool dup = h0 ? t0 == e0 : h1 ? t1 == e1 : h2 ? t2 == e2 : h3 ? t3 == e3 : false;
+          const uint32_t tq = h0 ? t0 : h1 ? t1 : h2 ? t2 : t3;
+          const bool dup = (tq == s) & (h0 | h1 | h2 | h3);
           const bool wr = go & !dup;
           const uint32_t dd = (home + q) & (kDedupSize - 1);
-          const uint32_t cw = code_of(s, q);
-          const uint32_t wi = wr ? dd : kDedupSize + 4, mi = wr && dd < 3u ? dd + kDedupSize : kDedupSize + 4;
-          tlo[wi] = (uint16_t)cw;
-          thi[wi] = (uint8_t)(cw >> 16);
-          tlo[mi] = (uint16_t)cw;
-          thi[mi] = (uint8_t)(cw >> 16);
+          table[wr ? dd : kDedupSize + 4] = s;
+          table[wr && dd < 3u ? dd + kDedupSize : kDedupSize + 4] = s;
           wres[buf][go ? (pos & 63u) * K + (pos >> 6) : (uint32_t)W] = dup ? 0 : 1;
           i = i2;
-          pos = i < iend ? npos : kNoPos;
-          s = nsig;
+          pos = i < iend ? (uint32_t)(nx >> 32) : kNoPos;
+          s = (uint32_t)nx;
         }
       }
     } else {
