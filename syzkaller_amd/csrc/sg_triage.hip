@@ -89,7 +89,6 @@ struct OwnArgs {
   uint32_t* big;         // [0]: count, then the records left for k_own_big
   uint64_t n;            // elements in the batch (vals[0 .. n) readable)
   uint32_t* ticket;      // k_own_pipe's next block of 64 records (zeroed)
-  uint32_t dbg;          // diagnostics (SG_OWN_DBG, results wrong): 1 no inserts, 2 no lookups, 4 no chunk loads, 8 no key loads
 };
 
 // The set: 1 << bb buckets of four slots, a key in the first bucket from its
@@ -456,7 +455,7 @@ __global__ __launch_bounds__(kOwnWaves * 64) __attribute__((amdgpu_waves_per_eu(
         if (j * 64 + lane >= np) continue;
         if (A.kv[j] == kOwnEmpty) {
           ff = true;
-        } else if (!(a.dbg & 1)) {
+        } else {
           const uint32_t m = (1u << bb) - 1;
           for (uint32_t b = own_home(A.kv[j], bb);; b = (b + 1) & m) {
             const uint32_t at = atomicAdd(&hc[b], 1u);
@@ -474,8 +473,7 @@ __global__ __launch_bounds__(kOwnWaves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < kOwnCB; j++)
         if (c0 + j <= c1) {
-          const uint32_t hit = (a.dbg & 2) ? (A.x[j][0] & 15u)
-                                           : own_hits<false, 1>(ht, nullptr, bb, has_ff, lane, elo, ehi, c0 + j, A.x[j]);
+          const uint32_t hit = own_hits<false, 1>(ht, nullptr, bb, has_ff, lane, elo, ehi, c0 + j, A.x[j]);
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             const uint64_t bk = __ballot((hit >> k) & 1u);
@@ -483,9 +481,8 @@ __global__ __launch_bounds__(kOwnWaves * 64) __attribute__((amdgpu_waves_per_eu(
           }
         }
       const uint64_t cj = min(c0 + (uint64_t)(lane >> 2), c1);
-      if (!(a.dbg & 16))
-        atomicOr(reinterpret_cast<unsigned long long*>(a.mask + cj * 4 + (lane & 3)),
-                 (unsigned long long)(lane < 4 * kOwnCB ? word : 0ull));
+      atomicOr(reinterpret_cast<unsigned long long*>(a.mask + cj * 4 + (lane & 3)),
+               (unsigned long long)(lane < 4 * kOwnCB ? word : 0ull));
       wave_sync();  // (the set is cleared for the next record)
       if (!more) break;
       A = B;
@@ -1082,12 +1079,8 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
     if (np)
       hipLaunchKernelGGL(k_own_bounds, dim3(div_up(np, 256 * kBoundPer)), dim3(256), 0, ctx->stream,
                          (const uint64_t*)sorted, np, po);
-    static const uint32_t own_dbg = [] {
-      const char* e = getenv("SG_OWN_DBG");
-      return e ? (uint32_t)atoi(e) : 0u;
-    }();
     OwnArgs oa{d_vals, roff, e0, (uint32_t)nr, sorted, po, d_rec_new ? d_rec_new + r0 : nullptr, s.dmask, big, nvals,
-               big + nr + 1, own_dbg};
+               big + nr + 1};
     SG_HIP(hipMemsetAsync(big + nr + 1, 0, 4, ctx->stream));
     if (aligned)
       rc = launch_own<true>(ctx, oa, nr, dedup);
