@@ -204,14 +204,15 @@ def row_f2(ctx, rng):
     calls = rng.integers(0, ncalls, size=n).astype(np.uint32)
     res = {}
     for name, grp, ng in [("per_call_html84", calls, ncalls), ("all_html306", None, 1)]:
-        # warm the same path (grouped: the key sort; one group: the byte map) --
+        # warm the same path (grouped: the per-group LDS sort; one group: the byte map) --
         # a kernel's first launch in the process loads its code
         C.union_fold(vals[:10], np.array([0, 10], np.uint64), None if grp is None else grp[:1], ng, ctx=ctx)
         ctx.timing(True)
         t0 = time.perf_counter()
         fv, fo = C.union_fold(vals, off, grp, ng, ctx=ctx)
         wall = time.perf_counter() - t0
-        kt = ktime(ctx, ["union_fold", "fold_keys", "fold_sort", "fold_unique", "fold_map", "merge_small", "merge_keep",
+        kt = ktime(ctx, ["union_fold", "fold_keys", "fold_sort", "fold_unique", "fold_map", "fold_pack", "fold_lds",
+                         "fold_move", "merge_small", "merge_keep",
                          "merge_scatter", "scan"])
         ctx.timing(False)
         dev = kt.get("union_fold", 0.0)

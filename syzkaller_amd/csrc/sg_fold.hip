@@ -44,6 +44,23 @@ __global__ void k_fold_pack(const uint32_t* __restrict__ src, const uint64_t* __
   for (uint64_t i = threadIdx.x & 63; i < L; i += 64) dst[d + i] = src[s + i];
 }
 
+// the same, and *rep = 1 when some list holds a value twice in a row (then
+// the lists are not canonical covers and the per-group LDS fold is not theirs)
+__global__ void k_fold_pack_chk(const uint32_t* __restrict__ src, const uint64_t* __restrict__ src_beg,
+                                const uint64_t* __restrict__ len, const uint64_t* __restrict__ dst_off, uint64_t n,
+                                uint32_t* __restrict__ dst, uint32_t* __restrict__ rep) {
+  const uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const uint64_t s = src_beg[k], d = dst_off[k], L = len[k];
+  bool r = false;
+  for (uint64_t i = threadIdx.x & 63; i < L; i += 64) {
+    const uint32_t v = src[s + i];
+    dst[d + i] = v;
+    r |= i > 0 && src[s + i - 1] == v;
+  }
+  if (__ballot(r) && (threadIdx.x & 63) == 0) *rep = 1;
+}
+
 struct Item {
   uint64_t beg, len;
 };
@@ -226,9 +243,277 @@ __global__ __launch_bounds__(kFmThreads) void k_fold_map_write(const uint8_t* __
     if ((qw[j >> 2] >> (8 * (j & 3))) & 0xFFu) out[at++] = lo + (uint32_t)(b + j);
 }
 
+// Many groups of canonical lists (the per-syscall folds of html.go:84, each
+// group a few thousand PCs): a workgroup per group sorts the group's values in
+// LDS (stable 8-bit LSD passes over the bits that vary within the group, each
+// pass a wave multisplit rank, a scan of the 256 digit counts and a scatter
+// through LDS) and keeps the first of each run, the sentinel dropped -- one
+// read of the values and one write of the folds, where the 64-bit key sort
+// made five passes over (group, value) keys.  Groups are packed group-major
+// first; a group of more than kFgCap values takes the key sort.
+constexpr int kFgSteps = 16;
+constexpr uint32_t kFgCap = 1024 * kFgSteps;  // 16384 values per group (the 1024-thread form)
+
+__device__ __forceinline__ uint64_t fg_peers(uint32_t d, bool live) {  // lanes holding digit d
+  uint64_t eq = __ballot(live);
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+    const uint64_t bal = __ballot((d >> b) & 1u);
+    eq &= ((d >> b) & 1u) ? bal : ~bal;
+  }
+  return eq;
+}
+
+// kT threads, groups of <= kT * kFgSteps values (the host gives each form
+// its groups: 512 threads for <= 8192 values, four workgroups per CU; 1024 for
+// the rest).  A wave's steps past the group's end are skipped (wave-uniform).
+template <int kT>
+__global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ packed, const uint64_t* __restrict__ gstart,
+                                                 const uint32_t* __restrict__ glist, uint32_t* __restrict__ out,
+                                                 uint32_t* __restrict__ gcnt) {
+  constexpr int kW = kT / 64;
+  constexpr uint32_t kCap = kT * kFgSteps;
+  __shared__ uint32_t stage[kCap];
+  __shared__ uint32_t cnt[kW][256];  // per-wave digit counts, then the waves' offsets in the digit
+  __shared__ uint32_t dstart[256];
+  __shared__ uint32_t red[2][kW];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint32_t g = glist[blockIdx.x];
+  const uint64_t b0 = gstart[g];
+  const uint32_t n = (uint32_t)(gstart[g + 1] - b0);
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // positions of wave w: [64 kFgSteps w, + 64 kFgSteps), step s at + 64 s + lane
+  const uint32_t base = (uint32_t)w * 64 * kFgSteps;
+  const int nst = base >= n ? 0 : (int)min<uint32_t>(kFgSteps, (n - base + 63) / 64);  // this wave's live steps
+  uint32_t k[kFgSteps];
+  uint32_t va = 0xFFFFFFFFu, vo = 0;
+#pragma unroll
+  for (int st = 0; st < kFgSteps; st++) {
+    const uint32_t p = base + st * 64 + lane;
+    k[st] = 0xFFFFFFFFu;
+    if (st < nst && p < n) {
+      k[st] = packed[b0 + p];
+      va &= k[st];
+      vo |= k[st];
+    }
+  }
+  // the bits that vary within the group
+#pragma unroll
+  for (int d = 32; d; d >>= 1) {
+    va &= (uint32_t)__shfl_xor((int)va, d);
+    vo |= (uint32_t)__shfl_xor((int)vo, d);
+  }
+  if (lane == 0) {
+    red[0][w] = va;
+    red[1][w] = vo;
+  }
+  __syncthreads();
+  uint32_t A = 0xFFFFFFFFu, O = 0;
+#pragma unroll
+  for (int i = 0; i < kW; i++) {
+    A &= red[0][i];
+    O |= red[1][i];
+  }
+  const uint32_t vary = A ^ O;
+  for (uint32_t shift = 0; shift < 32; shift += 8) {
+    if (((vary >> shift) & 255u) == 0) continue;  // (block-uniform)
+    for (int i = tid; i < kW * 256; i += kT) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t rank[kFgSteps];
+#pragma unroll
+    for (int st = 0; st < kFgSteps; st++) {
+      rank[st] = 0;
+      if (st < nst) {  // (wave-uniform)
+        const bool live = base + st * 64 + lane < n;
+        const uint32_t d = (k[st] >> shift) & 255u;
+        const uint64_t eq = fg_peers(d, live);
+        const uint32_t before = live ? cnt[w][d] : 0u;
+        rank[st] = before + (uint32_t)__popcll(eq & lt);
+        if (live && (eq & lt) == 0) cnt[w][d] = before + (uint32_t)__popcll(eq);
+      }
+    }
+    __syncthreads();
+    if (tid < 256) {  // per digit: the waves' offsets, the digit's count
+      uint32_t acc = 0;
+#pragma unroll
+      for (int i = 0; i < kW; i++) {
+        const uint32_t c = cnt[i][tid];
+        cnt[i][tid] = acc;
+        acc += c;
+      }
+      dstart[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 digit counts
+      uint32_t c[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        c[j] = dstart[tid * 4 + j];
+        sum += c[j];
+      }
+      uint32_t run = sgd::wave_incl_add(sum) - sum;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        dstart[tid * 4 + j] = run;
+        run += c[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kFgSteps; st++) {
+      if (st >= nst) break;
+      if (base + st * 64 + lane < n) {
+        const uint32_t d = (k[st] >> shift) & 255u;
+        stage[dstart[d] + cnt[w][d] + rank[st]] = k[st];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kFgSteps; st++) {
+      if (st >= nst) break;
+      const uint32_t p = base + st * 64 + lane;
+      k[st] = p < n ? stage[p] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+  }
+  // sorted: keep the first of each run, the sentinel dropped (cover.go:63-70, :97)
+#pragma unroll
+  for (int st = 0; st < kFgSteps; st++) {
+    if (st >= nst) break;
+    stage[base + st * 64 + lane] = k[st];
+  }
+  __syncthreads();
+  uint32_t keep = 0, c = 0;
+#pragma unroll
+  for (int st = 0; st < kFgSteps; st++) {
+    if (st < nst) {
+      const uint32_t p = base + st * 64 + lane;
+      const bool kp = p < n && k[st] != 0xFFFFFFFFu && (p == 0 || stage[p - 1] != k[st]);
+      keep |= (kp ? 1u : 0u) << st;
+      c += (uint32_t)__popcll(__ballot(kp));
+    }
+  }
+  if (lane == 0) red[0][w] = c;
+  __syncthreads();
+  uint32_t at = 0;
+  for (int i = 0; i < w; i++) at += red[0][i];
+  if (tid == kT - 1) {
+    uint32_t t = 0;
+    for (int i = 0; i < kW; i++) t += red[0][i];
+    gcnt[g] = t;
+  }
+#pragma unroll
+  for (int st = 0; st < kFgSteps; st++) {
+    if (st < nst) {
+      const bool kp = (keep >> st) & 1u;
+      const uint64_t m = __ballot(kp);
+      if (kp) out[b0 + at + (uint32_t)__popcll(m & lt)] = k[st];
+      at += (uint32_t)__popcll(m);
+    }
+  }
+}
+
+// dst[doff[g] ..] = src[sbeg[g] .. + len[g]) for u32 lengths, one wave per group
+__global__ void k_fold_move(const uint32_t* __restrict__ src, const uint64_t* __restrict__ sbeg,
+                            const uint32_t* __restrict__ len, const uint64_t* __restrict__ doff, uint64_t n,
+                            uint32_t* __restrict__ dst) {
+  const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (g >= n) return;
+  const uint64_t s = sbeg[g], d = doff[g], L = len[g];
+  for (uint64_t i = threadIdx.x & 63; i < L; i += 64) dst[d + i] = src[s + i];
+}
+
 constexpr int SG_EOVERFLOW_FOLD = 1;  // internal: the keys do not fit 64 bits
+constexpr int SG_EREPEATS_FOLD = 2;   // internal: a list repeats a value (not the per-group LDS fold's)
 
 static uint32_t bits_for(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+
+// The per-group LDS fold (k_fold_lds): the lists packed group-major, a
+// workgroup per group, the folds moved together (ctx lock held).
+static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off, size_t n, const uint32_t* group,
+                           size_t ngroups, const std::vector<uint64_t>& gs, uint32_t* out_vals, size_t cap,
+                           uint64_t* out_off) {
+  const uint64_t N = gs[ngroups];
+  // every list's place in the group-major packing: its group's start + the
+  // lengths of the group's earlier lists (host, from the offsets it was given)
+  std::vector<uint64_t> lst(n), len(n), at(gs.begin(), gs.end() - 1);
+  WsPlan p;
+  const size_t oP = p.add(N * 4), oO = p.add(N * 4), oG = p.add((ngroups + 1) * 8), oL = p.add(n * 8),
+               oB = p.add(n * 8), oN = p.add(n * 8), oC = p.add(ngroups * 4), oF = p.add((ngroups + 1) * 8),
+               oQ = p.add(ngroups * 4), oR = p.add(4);
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(ngroups));
+  if (rc) return rc;
+  uint32_t* packed = (uint32_t*)ws_at(ctx, oP);
+  uint32_t* folded = (uint32_t*)ws_at(ctx, oO);
+  uint64_t* dgs = (uint64_t*)ws_at(ctx, oG);
+  uint64_t* dlst = (uint64_t*)ws_at(ctx, oL);
+  uint64_t* dbeg = (uint64_t*)ws_at(ctx, oB);
+  uint64_t* dlen = (uint64_t*)ws_at(ctx, oN);
+  uint32_t* gcnt = (uint32_t*)ws_at(ctx, oC);
+  uint64_t* fo = (uint64_t*)ws_at(ctx, oF);
+  uint32_t* dq = (uint32_t*)ws_at(ctx, oQ);
+  uint32_t* rep = (uint32_t*)ws_at(ctx, oR);
+  // the groups by form: <= 8192 values (512 threads), the rest (1024)
+  std::vector<uint32_t> ql;
+  uint32_t nsmall = 0;
+  for (uint32_t gi = 0; gi < ngroups; gi++)
+    if (gs[gi + 1] - gs[gi] <= 512u * kFgSteps) ql.push_back(gi);
+  nsmall = (uint32_t)ql.size();
+  for (uint32_t gi = 0; gi < ngroups; gi++)
+    if (gs[gi + 1] - gs[gi] > 512u * kFgSteps) ql.push_back(gi);
+  for (size_t k = 0; k < n; k++) {
+    const uint32_t gi = group ? group[k] : 0u;
+    len[k] = off[k + 1] - off[k];
+    lst[k] = at[gi];
+    at[gi] += len[k];
+  }
+  SG_HIP(hipMemcpyAsync(dgs, gs.data(), (ngroups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dq, ql.data(), ngroups * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemsetAsync(rep, 0, 4, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dlst, lst.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dbeg, off, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dlen, len.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+  {
+    ScopedTimer tm(ctx, "union_fold");
+    {
+      ScopedTimer tk(ctx, "fold_pack");
+      hipLaunchKernelGGL(k_fold_pack_chk, dim3(div_up(n, 4)), dim3(256), 0, ctx->stream, dv, (const uint64_t*)dbeg,
+                         (const uint64_t*)dlen, (const uint64_t*)dlst, (uint64_t)n, packed, rep);
+    }
+    {
+      ScopedTimer tk(ctx, "fold_lds");
+      if (nsmall)
+        hipLaunchKernelGGL(k_fold_lds<512>, dim3(nsmall), dim3(512), 0, ctx->stream, (const uint32_t*)packed,
+                           (const uint64_t*)dgs, (const uint32_t*)dq, folded, gcnt);
+      if (ngroups > nsmall)
+        hipLaunchKernelGGL(k_fold_lds<1024>, dim3((uint32_t)(ngroups - nsmall)), dim3(1024), 0, ctx->stream,
+                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nsmall, folded, gcnt);
+    }
+    rc = scan_counts(ctx, gcnt, fo, ngroups, p.total);
+    if (rc) return rc;
+    {
+      ScopedTimer tk(ctx, "fold_move");
+      hipLaunchKernelGGL(k_fold_move, dim3(div_up(ngroups, 4)), dim3(256), 0, ctx->stream, (const uint32_t*)folded,
+                         (const uint64_t*)dgs, (const uint32_t*)gcnt, (const uint64_t*)fo, (uint64_t)ngroups, packed);
+    }
+    SG_HIP(hipGetLastError());
+  }
+  uint32_t hrep = 0;
+  SG_HIP(hipMemcpyAsync(out_off, fo, (ngroups + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipMemcpyAsync(&hrep, rep, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (hrep) return SG_EREPEATS_FOLD;  // (not canonical: the multiset fold)
+  const uint64_t total = out_off[ngroups];
+  if (total > cap) {
+    set_error("sg_union_fold: %llu values, capacity %zu", (unsigned long long)total, cap);
+    return SG_EINVAL;
+  }
+  if (total == 0) return SG_OK;
+  if (!out_vals) return SG_EINVAL;
+  SG_HIP(hipMemcpyAsync(out_vals, packed, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return SG_OK;
+}
 
 // The sort + unique fold (ctx lock held; arguments checked, N > 0).
 static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n, const uint32_t* group,
@@ -259,6 +544,28 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
   SG_HIP(hipMemcpyAsync(dv, vals, N * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   if (group) SG_HIP(hipMemcpyAsync(dgrp, group, n * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (ngroups > 1) {
+    // many groups of canonical covers, each small enough for LDS: the
+    // per-group fold (it checks for repeats itself; a list with one takes the
+    // key sort below)
+    std::vector<uint64_t> gs(ngroups + 1, 0);
+    for (size_t k = 0; k < n; k++) gs[(group ? group[k] : 0) + 1] += off[k + 1] - off[k];
+    uint64_t gmax = 0;
+    for (size_t gi = 0; gi < ngroups; gi++) {
+      gmax = std::max(gmax, gs[gi + 1]);
+      gs[gi + 1] += gs[gi];
+    }
+    if (gmax <= kFgCap) {
+      rc = fold_groups_lds(ctx, dv, off, n, group, ngroups, gs, out_vals, cap, out_off);
+      if (rc != SG_EREPEATS_FOLD) return rc;
+      rc = ws_reserve(ctx, need);  // (the workspace may have moved)
+      if (rc) return rc;
+      ka = (uint64_t*)ws_at(ctx, oA), kb = (uint64_t*)ws_at(ctx, oB), tpos = (uint64_t*)ws_at(ctx, oP);
+      tcnt = (uint32_t*)ws_at(ctx, oK);
+      first = (uint64_t*)ws_at(ctx, oF);
+      stats = (unsigned long long*)ws_at(ctx, oJ);
+    }
+  }
   unsigned long long st[3] = {0, 0xFFFFFFFFull, 0};
   SG_HIP(hipMemcpyAsync(stats, st, 24, hipMemcpyHostToDevice, ctx->stream));
   const dim3 lgrid(div_up(n, 4));

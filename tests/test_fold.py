@@ -142,3 +142,40 @@ def test_union_fold_byte_map_edges(ctx, monkeypatch):
         sv, so = C.union_fold(vals, off, ctx=ctx)
         monkeypatch.delenv("SG_FOLD_MAP")
         assert np.array_equal(so, eo) and np.array_equal(sv, ev), span
+
+
+@pytest.mark.gpu
+def test_union_fold_lds_groups(ctx):
+    """Many groups of canonical lists: a workgroup sorts each group in LDS
+    (sg_fold.hip k_fold_lds, groups of <= 16384 values).  Groups at and around
+    that size (one past it: the whole fold takes the key sort), empty groups,
+    one-value groups, constant groups (no digit pass), values over the whole
+    32-bit range (four passes), the sentinel at the ends of lists."""
+    from syzkaller_amd import cover as C
+
+    rng = np.random.default_rng(57)
+    for top in (16384, 16385):
+        covs, calls = [], []
+        sizes = [top, 16000, 1, 0, 5, 300, 8191, 8192, 2, 2]
+        for gi, sz in enumerate(sizes):
+            left = sz
+            while left > 0:  # a group's values over several lists, repeats across lists
+                m = int(min(left, rng.integers(1, 3000)))
+                if gi == 4:
+                    v = np.full(1, 0x12345678, np.uint32)  # a constant group
+                    m = 1
+                elif gi == 5:
+                    v = np.unique(rng.integers(0, 1 << 32, size=m, dtype=np.uint64)).astype(np.uint32)
+                else:
+                    v = (0x81000000 + 16 * rng.choice(1 << 20, size=m, replace=False)).astype(np.uint32)
+                if gi == 9:
+                    v = np.array([7, 0xFFFFFFFF], np.uint32)
+                covs.append(np.sort(v))
+                calls.append(gi)
+                left -= max(1, v.size)
+        calls = np.array(calls, np.uint32)
+        vals, off = C.to_csr(covs)
+        ng = len(sizes) + 2  # two empty groups past the last
+        gv, go = C.union_fold(vals, off, calls, ng, ctx=ctx)
+        ev, eo = O.union_fold(vals, off, calls, ng)
+        assert np.array_equal(go, eo) and np.array_equal(gv, ev), top
