@@ -19,8 +19,8 @@ from collections import defaultdict
 
 KERNELS = {"p1_hist": ("k_hist_rep<false>", "k_hist_trace", "k_p1_hist"), "p1_scatter": ("k_p1_scatter",),
            "p2_hist": ("k_hist_bytes",), "p2_scatter": ("k_p2_scatter",),
-           "bucket_triage": ("k_bucket<false, false>", "k_bucket<false, true>", "k_bucket_ring"), "bucket_spill": ("k_bucket_direct<false>",),
-           "triage_claim": ("k_claim<true>",), "triage_resolve": ("k_resolve<true>",),
+           "bucket_triage": ("k_bucket<false, 0>", "k_bucket<false, 1>", "k_bucket<false, 2>"),
+           "bucket_spill": ("k_bucket_direct<false>",),
            "count_missing": ("k_count_missing",), "emit_scatter": ("k_scatter(",),
            "bucket_mark": ("k_bucket_mark",), "prefix_or": ("k_prefix_or",), "prefix_flags": ("k_prefix_flags",),
            "prefix_merge": ("k_prefix_merge",), "set_or": ("k_set_or(",), "set_or_new": ("k_set_or_new(",), "set_or_new_or": ("k_set_or_new_or",)}

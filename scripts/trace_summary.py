@@ -10,7 +10,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_hist_rep<false>", "k_hist_trace", "k_p1_scatter<false", "k_hist_bytes", "k_p2_scatter", "k_bucket<false, false>",
+KERNELS = ["k_hist_rep<false>", "k_hist_trace", "k_p1_scatter<false", "k_hist_bytes", "k_p2_scatter", "k_bucket<false, 0>",
            "k_bucket_direct<false>", "k_bucket_groups", "k_chunk_desc", "k_cuts", "k_scan32_reduce", "k_scan32_apply",
            "k_set_copy"]
 
