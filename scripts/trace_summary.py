@@ -2,7 +2,8 @@
 """Timed-step launches of the triage kernels from a rocprofv3 --kernel-trace
 CSV: the launches between the REGION-th k_mark_begin / k_mark_end pair
 (bench.py brackets each timed region with sg_ctx_marker; in run order region
-0 = C2, 1 = C2 from traces, 2 = the steady state), their durations and launch
+0 = C2, 1 = C2 with the ordered outputs, 2 = C2 from traces, 3 = the steady
+state), their durations and launch
 resources.
 usage: trace_summary.py KERNEL_TRACE_CSV COMMAND OUT_JSON [REGION]"""
 import csv

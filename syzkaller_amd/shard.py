@@ -593,7 +593,8 @@ class PrefixTriage:
         else:
             exchange(st)
         xb = 4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))
-        pend["last"] = {"nrec_total": nrec_total, "exchange": "dense", "exchange_bytes": xb + 16 * (G - 1),
+        pend["last"] = {"nrec_total": nrec_total, "exchange": "dense" if G > 1 else "local",
+                        "exchange_bytes": xb + 16 * (G - 1),
                         "form": {0: "kept", 1: "pairs", None: "default"}[form]}
         return pend
 
