@@ -66,10 +66,10 @@ void* sg_ctx_stream(sg_ctx* ctx);
  * enable != 0 starts recording (and resets the tallies). */
 int sg_ctx_timing(sg_ctx* ctx, int enable);
 /* Total device milliseconds and launch count recorded for kernel `name`
- * (e.g. "triage_claim"); syncs the stream. */
+ * (e.g. "bucket_triage"); syncs the stream. */
 int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* launches);
-/* Context counters: "owner_resets" (first-owner table generations started
- * after the key space ran out), "owner_floor", "owner_key_space",
+/* Context counters: "owner_resets" (Minimize's first-owner table generations
+ * started after the key space ran out), "owner_floor", "owner_key_space",
  * "max_launch_records".  The environment switches SG_OWNER_KEY_SPACE and
  * SG_TRIAGE_MAX_RECS (test knobs that lower the key space / the records per
  * partitioned launch) are read once, by sg_ctx_create. */

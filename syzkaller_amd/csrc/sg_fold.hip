@@ -250,9 +250,9 @@ __global__ __launch_bounds__(kFmThreads) void k_fold_map_write(const uint8_t* __
 // through LDS) and keeps the first of each run, the sentinel dropped -- one
 // read of the values and one write of the folds, where the 64-bit key sort
 // made five passes over (group, value) keys.  Groups are packed group-major
-// first; a group of more than kFgCap values takes the key sort.
+// first; the groups of more than kFgCap values take the key sort, beside.
 constexpr int kFgSteps = 16;
-constexpr uint32_t kFgCap = 1024 * kFgSteps;  // 16384 values per group (the 1024-thread form)
+constexpr uint32_t kFgCap = 1024 * 2 * kFgSteps;  // 32768 values per group (the 1024 x 32 form)
 
 __device__ __forceinline__ uint64_t fg_peers(uint32_t d, bool live) {  // lanes holding digit d
   uint64_t eq = __ballot(live);
@@ -264,15 +264,16 @@ __device__ __forceinline__ uint64_t fg_peers(uint32_t d, bool live) {  // lanes 
   return eq;
 }
 
-// kT threads, groups of <= kT * kFgSteps values (the host gives each form
-// its groups: 512 threads for <= 8192 values, four workgroups per CU; 1024 for
-// the rest).  A wave's steps past the group's end are skipped (wave-uniform).
-template <int kT>
+// kT threads, kS steps of 64 values per wave: groups of <= kT kS values (the
+// host gives each form its groups: 512 x 16 for <= 8192 values, four
+// workgroups per CU; 1024 x 16 for <= 16384; 1024 x 32, 144 KiB of LDS, for
+// <= 32768).  A wave's steps past the group's end are skipped (wave-uniform).
+template <int kT, int kS>
 __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ packed, const uint64_t* __restrict__ gstart,
                                                  const uint32_t* __restrict__ glist, uint32_t* __restrict__ out,
                                                  uint32_t* __restrict__ gcnt) {
   constexpr int kW = kT / 64;
-  constexpr uint32_t kCap = kT * kFgSteps;
+  constexpr uint32_t kCap = kT * kS;
   __shared__ uint32_t stage[kCap];
   __shared__ uint32_t cnt[kW][256];  // per-wave digit counts, then the waves' offsets in the digit
   __shared__ uint32_t dstart[256];
@@ -282,13 +283,13 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
   const uint64_t b0 = gstart[g];
   const uint32_t n = (uint32_t)(gstart[g + 1] - b0);
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // positions of wave w: [64 kFgSteps w, + 64 kFgSteps), step s at + 64 s + lane
-  const uint32_t base = (uint32_t)w * 64 * kFgSteps;
-  const int nst = base >= n ? 0 : (int)min<uint32_t>(kFgSteps, (n - base + 63) / 64);  // this wave's live steps
-  uint32_t k[kFgSteps];
+  // positions of wave w: [64 kS w, + 64 kS), step s at + 64 s + lane
+  const uint32_t base = (uint32_t)w * 64 * kS;
+  const int nst = base >= n ? 0 : (int)min<uint32_t>(kS, (n - base + 63) / 64);  // this wave's live steps
+  uint32_t k[kS];
   uint32_t va = 0xFFFFFFFFu, vo = 0;
 #pragma unroll
-  for (int st = 0; st < kFgSteps; st++) {
+  for (int st = 0; st < kS; st++) {
     const uint32_t p = base + st * 64 + lane;
     k[st] = 0xFFFFFFFFu;
     if (st < nst && p < n) {
@@ -315,13 +316,15 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
     O |= red[1][i];
   }
   const uint32_t vary = A ^ O;
-  for (uint32_t shift = 0; shift < 32; shift += 8) {
+  // 8-bit digits from the lowest varying bit (PCs 16 B apart: bits 4.. -- one
+  // pass fewer than digits at bit 0)
+  for (uint32_t shift = vary ? (uint32_t)__builtin_ctz(vary) : 32u; shift < 32; shift += 8) {
     if (((vary >> shift) & 255u) == 0) continue;  // (block-uniform)
     for (int i = tid; i < kW * 256; i += kT) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    uint32_t rank[kFgSteps];
+    uint32_t rank[kS];
 #pragma unroll
-    for (int st = 0; st < kFgSteps; st++) {
+    for (int st = 0; st < kS; st++) {
       rank[st] = 0;
       if (st < nst) {  // (wave-uniform)
         const bool live = base + st * 64 + lane < n;
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
     }
     __syncthreads();
 #pragma unroll
-    for (int st = 0; st < kFgSteps; st++) {
+    for (int st = 0; st < kS; st++) {
       if (st >= nst) break;
       if (base + st * 64 + lane < n) {
         const uint32_t d = (k[st] >> shift) & 255u;
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
     }
     __syncthreads();
 #pragma unroll
-    for (int st = 0; st < kFgSteps; st++) {
+    for (int st = 0; st < kS; st++) {
       if (st >= nst) break;
       const uint32_t p = base + st * 64 + lane;
       k[st] = p < n ? stage[p] : 0xFFFFFFFFu;
@@ -378,14 +381,14 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
   }
   // sorted: keep the first of each run, the sentinel dropped (cover.go:63-70, :97)
 #pragma unroll
-  for (int st = 0; st < kFgSteps; st++) {
+  for (int st = 0; st < kS; st++) {
     if (st >= nst) break;
     stage[base + st * 64 + lane] = k[st];
   }
   __syncthreads();
   uint32_t keep = 0, c = 0;
 #pragma unroll
-  for (int st = 0; st < kFgSteps; st++) {
+  for (int st = 0; st < kS; st++) {
     if (st < nst) {
       const uint32_t p = base + st * 64 + lane;
       const bool kp = p < n && k[st] != 0xFFFFFFFFu && (p == 0 || stage[p - 1] != k[st]);
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
     gcnt[g] = t;
   }
 #pragma unroll
-  for (int st = 0; st < kFgSteps; st++) {
+  for (int st = 0; st < kS; st++) {
     if (st < nst) {
       const bool kp = (keep >> st) & 1u;
       const uint64_t m = __ballot(kp);
@@ -423,13 +426,40 @@ __global__ void k_fold_move(const uint32_t* __restrict__ src, const uint64_t* __
   for (uint64_t i = threadIdx.x & 63; i < L; i += 64) dst[d + i] = src[s + i];
 }
 
+// Groups of more than kFgCap values (beside the LDS-folded ones): each big
+// group's packed values as keys b << 32 | v (b = the group's index among the
+// big ones) at bk[b] .., for the key sort; grid (x, nbig).
+__global__ void k_fold_bigkeys(const uint32_t* __restrict__ packed, const uint64_t* __restrict__ gs,
+                               const uint32_t* __restrict__ blist, const uint64_t* __restrict__ bk,
+                               uint64_t* __restrict__ keys) {
+  const uint32_t b = blockIdx.y, g = blist[b];
+  const uint64_t src = gs[g], len = gs[g + 1] - src, dst = bk[b];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (uint64_t)gridDim.x * blockDim.x)
+    keys[dst + i] = ((uint64_t)b << 32) | packed[src + i];
+}
+
+// Each big group's fold (the unique pass's output from first[b] to first[b +
+// 1], or the total for the last) into folded at the group's start, its count
+// into gcnt -- where the LDS fold leaves the small groups'.  A block per group.
+__global__ void k_fold_bigmove(const uint32_t* __restrict__ uout, const uint64_t* __restrict__ first,
+                               const uint64_t* __restrict__ total, uint32_t nbig, const uint32_t* __restrict__ blist,
+                               const uint64_t* __restrict__ gs, uint32_t* __restrict__ folded,
+                               uint32_t* __restrict__ gcnt) {
+  const uint32_t b = blockIdx.x, g = blist[b];
+  const uint64_t s = first[b], e = b + 1 < nbig ? first[b + 1] : *total, d = gs[g];
+  for (uint64_t i = threadIdx.x; i < e - s; i += blockDim.x) folded[d + i] = uout[s + i];
+  if (threadIdx.x == 0) gcnt[g] = (uint32_t)(e - s);
+}
+
 constexpr int SG_EOVERFLOW_FOLD = 1;  // internal: the keys do not fit 64 bits
 constexpr int SG_EREPEATS_FOLD = 2;   // internal: a list repeats a value (not the per-group LDS fold's)
 
 static uint32_t bits_for(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
 
 // The per-group LDS fold (k_fold_lds): the lists packed group-major, a
-// workgroup per group, the folds moved together (ctx lock held).
+// workgroup per group, the folds moved together (ctx lock held).  Groups of
+// more than kFgCap values (a few, when some inputs are long) are folded beside
+// them by the 64-bit key sort over their values alone.
 static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off, size_t n, const uint32_t* group,
                            size_t ngroups, const std::vector<uint64_t>& gs, uint32_t* out_vals, size_t cap,
                            uint64_t* out_off) {
@@ -437,11 +467,24 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
   // every list's place in the group-major packing: its group's start + the
   // lengths of the group's earlier lists (host, from the offsets it was given)
   std::vector<uint64_t> lst(n), len(n), at(gs.begin(), gs.end() - 1);
+  // the big groups, their keys' places
+  std::vector<uint32_t> bl;
+  std::vector<uint64_t> bk(1, 0);
+  for (uint32_t gi = 0; gi < ngroups; gi++)
+    if (gs[gi + 1] - gs[gi] > kFgCap) {
+      bl.push_back(gi);
+      bk.push_back(bk.back() + (gs[gi + 1] - gs[gi]));
+    }
+  const uint32_t nbig = (uint32_t)bl.size();
+  const uint64_t NB = bk.back(), ntb = div_up(NB, (uint64_t)kFuTile);
   WsPlan p;
   const size_t oP = p.add(N * 4), oO = p.add(N * 4), oG = p.add((ngroups + 1) * 8), oL = p.add(n * 8),
                oB = p.add(n * 8), oN = p.add(n * 8), oC = p.add(ngroups * 4), oF = p.add((ngroups + 1) * 8),
-               oQ = p.add(ngroups * 4), oR = p.add(4);
-  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(ngroups));
+               oQ = p.add(ngroups * 4), oR = p.add(4), oKA = p.add(NB * 8), oKB = p.add(NB * 8),
+               oBL = p.add(nbig * 4 + 4), oBK = p.add((nbig + 1) * 8), oBF = p.add(nbig * 8 + 8),
+               oTC = p.add(ntb * 4 + 4), oTP = p.add((ntb + 1) * 8);
+  int rc = ws_reserve(ctx, p.total + std::max({scan_ws_bytes(ngroups), nbig ? radix_sort_ws(NB) : 0,
+                                               nbig ? scan_ws_bytes(ntb) : 0}));
   if (rc) return rc;
   uint32_t* packed = (uint32_t*)ws_at(ctx, oP);
   uint32_t* folded = (uint32_t*)ws_at(ctx, oO);
@@ -453,14 +496,17 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
   uint64_t* fo = (uint64_t*)ws_at(ctx, oF);
   uint32_t* dq = (uint32_t*)ws_at(ctx, oQ);
   uint32_t* rep = (uint32_t*)ws_at(ctx, oR);
-  // the groups by form: <= 8192 values (512 threads), the rest (1024)
+  // the groups by form: <= 8192 values (512 x 16), <= 16384 (1024 x 16),
+  // <= kFgCap (1024 x 32), the big ones (the key sort)
   std::vector<uint32_t> ql;
-  uint32_t nsmall = 0;
-  for (uint32_t gi = 0; gi < ngroups; gi++)
-    if (gs[gi + 1] - gs[gi] <= 512u * kFgSteps) ql.push_back(gi);
-  nsmall = (uint32_t)ql.size();
-  for (uint32_t gi = 0; gi < ngroups; gi++)
-    if (gs[gi + 1] - gs[gi] > 512u * kFgSteps) ql.push_back(gi);
+  uint32_t nform[3] = {0, 0, 0};
+  const uint64_t lim[4] = {0, 512u * kFgSteps, 1024u * kFgSteps, kFgCap};
+  for (int f = 0; f < 3; f++) {
+    for (uint32_t gi = 0; gi < ngroups; gi++)
+      if ((f == 0 || gs[gi + 1] - gs[gi] > lim[f]) && gs[gi + 1] - gs[gi] <= lim[f + 1]) ql.push_back(gi);
+    nform[f] = (uint32_t)ql.size();
+  }
+  ql.resize(ngroups);  // (the tail unused)
   for (size_t k = 0; k < n; k++) {
     const uint32_t gi = group ? group[k] : 0u;
     len[k] = off[k + 1] - off[k];
@@ -482,12 +528,45 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
     }
     {
       ScopedTimer tk(ctx, "fold_lds");
-      if (nsmall)
-        hipLaunchKernelGGL(k_fold_lds<512>, dim3(nsmall), dim3(512), 0, ctx->stream, (const uint32_t*)packed,
-                           (const uint64_t*)dgs, (const uint32_t*)dq, folded, gcnt);
-      if (ngroups > nsmall)
-        hipLaunchKernelGGL(k_fold_lds<1024>, dim3((uint32_t)(ngroups - nsmall)), dim3(1024), 0, ctx->stream,
-                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nsmall, folded, gcnt);
+      if (nform[0])
+        hipLaunchKernelGGL((k_fold_lds<512, kFgSteps>), dim3(nform[0]), dim3(512), 0, ctx->stream,
+                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq, folded, gcnt);
+      if (nform[1] > nform[0])
+        hipLaunchKernelGGL((k_fold_lds<1024, kFgSteps>), dim3(nform[1] - nform[0]), dim3(1024), 0, ctx->stream,
+                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nform[0], folded,
+                           gcnt);
+      if (nform[2] > nform[1])
+        hipLaunchKernelGGL((k_fold_lds<1024, 2 * kFgSteps>), dim3(nform[2] - nform[1]), dim3(1024), 0, ctx->stream,
+                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nform[1], folded,
+                           gcnt);
+    }
+    if (nbig) {
+      ScopedTimer tk(ctx, "fold_big");
+      uint64_t* ka = (uint64_t*)ws_at(ctx, oKA);
+      uint64_t* kb = (uint64_t*)ws_at(ctx, oKB);
+      uint32_t* dbl = (uint32_t*)ws_at(ctx, oBL);
+      uint64_t* dbk = (uint64_t*)ws_at(ctx, oBK);
+      uint64_t* bfirst = (uint64_t*)ws_at(ctx, oBF);
+      uint32_t* tcnt = (uint32_t*)ws_at(ctx, oTC);
+      uint64_t* tpos = (uint64_t*)ws_at(ctx, oTP);
+      SG_HIP(hipMemcpyAsync(dbl, bl.data(), nbig * 4, hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(dbk, bk.data(), (nbig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+      hipLaunchKernelGGL(k_fold_bigkeys, dim3(64, nbig), dim3(256), 0, ctx->stream, (const uint32_t*)packed,
+                         (const uint64_t*)dgs, (const uint32_t*)dbl, (const uint64_t*)dbk, ka);
+      const uint32_t bb = bits_for(nbig - 1);
+      uint64_t* sorted = nullptr;
+      rc = radix_sort_u64(ctx, ka, kb, NB, p.total, &sorted, (((1ull << bb) - 1) << 32) | 0xFFFFFFFFull);
+      if (rc) return rc;
+      uint32_t* uout = (uint32_t*)(sorted == ka ? kb : ka);  // (the other key buffer, free now)
+      hipLaunchKernelGGL(k_fold_count, dim3((uint32_t)ntb), dim3(kFuThreads), 0, ctx->stream, (const uint64_t*)sorted,
+                         NB, 0u, tcnt);
+      rc = scan_counts(ctx, tcnt, tpos, ntb, p.total);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_fold_write, dim3((uint32_t)ntb), dim3(kFuThreads), 0, ctx->stream, (const uint64_t*)sorted,
+                         NB, 0u, (const uint64_t*)tpos, uout, bfirst);
+      hipLaunchKernelGGL(k_fold_bigmove, dim3(nbig), dim3(256), 0, ctx->stream, (const uint32_t*)uout,
+                         (const uint64_t*)bfirst, (const uint64_t*)(tpos + ntb), nbig, (const uint32_t*)dbl,
+                         (const uint64_t*)dgs, folded, gcnt);
     }
     rc = scan_counts(ctx, gcnt, fo, ngroups, p.total);
     if (rc) return rc;
@@ -545,9 +624,8 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
   SG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   if (group) SG_HIP(hipMemcpyAsync(dgrp, group, n * 4, hipMemcpyHostToDevice, ctx->stream));
   if (ngroups > 1) {
-    // many groups of canonical covers, each small enough for LDS: the
-    // per-group fold (it checks for repeats itself; a list with one takes the
-    // key sort below)
+    // many groups of canonical covers: the per-group fold (it checks for
+    // repeats itself; a list with one takes the key sort below)
     std::vector<uint64_t> gs(ngroups + 1, 0);
     for (size_t k = 0; k < n; k++) gs[(group ? group[k] : 0) + 1] += off[k + 1] - off[k];
     uint64_t gmax = 0;
@@ -555,7 +633,7 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
       gmax = std::max(gmax, gs[gi + 1]);
       gs[gi + 1] += gs[gi];
     }
-    if (gmax <= kFgCap) {
+    if (gmax < (1ull << 32)) {  // (group folds counted in 32 bits)
       rc = fold_groups_lds(ctx, dv, off, n, group, ngroups, gs, out_vals, cap, out_off);
       if (rc != SG_EREPEATS_FOLD) return rc;
       rc = ws_reserve(ctx, need);  // (the workspace may have moved)

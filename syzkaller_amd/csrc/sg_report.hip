@@ -114,7 +114,9 @@ struct RepArgs {
   uint32_t* last_del;     // per call site: 1 + last deleting query (0 none)
   uint8_t* flag;          // per call site: uncovered
   uint64_t* qbits;        // per query: inside a symbol (pass 1 -> pass 2)
+  uint32_t* leader;       // per symbol: the first symbol with its start (handledFuncs' key, cover.go:288)
   RadixIdx iend, ipcs;    // indexes over send and pcs
+  RadixIdx istart;        // index over sstart
 };
 
 // Two passes over the queries, each ordered so that its read-check skips
@@ -185,7 +187,8 @@ constexpr uint32_t kChunkIdx = 8192;     // radix buckets over the chunk bounds
 constexpr uint32_t kSiteIdx = 1024;      // radix buckets over one chunk's sites
 constexpr uint32_t kSymCap = 1024;       // symbols of a chunk held in LDS
 constexpr int kQT = 1024;                // threads of the count / scatter kernels
-constexpr int kSQPer = 8;                // queries per thread there
+constexpr int kSQPer = 8;                // queries per thread there, per sub-tile
+constexpr int kSQSub = 8;                // sub-tiles per query tile (64K queries: one count-table column)
 constexpr int kCT = 512;                 // threads of the chunk kernel
 constexpr uint32_t kCTile = 32768;       // grouped queries per chunk-kernel tile
 
@@ -251,7 +254,7 @@ __global__ void k_chunk_prep(ChunkArgs a) {
 // per site, the symbol a query at it lands in (cover.go:278)
 __global__ void k_site_sym(ChunkArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < a.npcs) a.ssym[j] = (uint32_t)ub64(a.send, a.nsym, a.pcs[j]);
+  if (j < a.npcs) a.ssym[j] = (uint32_t)ub_idx(a.send, a.nsym, a.iend, a.pcs[j]);
 }
 
 // per chunk, a radix index over its sites: sidx[c][k] = sites of chunk c
@@ -326,21 +329,33 @@ __device__ __forceinline__ uint32_t chunk_of(const ChunkArgs& a, const ChunkLds&
   return lds_lb(L.bnd, L.idx[k], L.idx[k + 1], pc);
 }
 
-template <int kPer>
+// Query tiles of kQT kPer kSub queries: one column of the count table each
+// (a table of 8K-query columns was 15M counts per 100M queries, and its scan
+// and the scatter's column reads -- a cache line per (chunk, tile) -- cost
+// more than the scatter's stores).
+template <int kPer, int kSub>
 __global__ __launch_bounds__(kQT) void k_q_count(ChunkArgs a) {
   __shared__ ChunkLds L;
   __shared__ uint32_t hist[kMaxChunks + 1];
   load_chunks(a, L);
   for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
   __syncthreads();
-  const uint64_t q0 = (uint64_t)blockIdx.x * kQT * kPer + threadIdx.x;
+  const uint64_t q0 = (uint64_t)blockIdx.x * kQT * kPer * kSub + threadIdx.x;
+  for (int sub = 0; sub < kSub; sub++) {
+    uint32_t cv[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint64_t i = q0 + (uint64_t)k * kQT;
-    if (i < a.ncov) {
-      const uint32_t c = chunk_of(a, L, query_pc(a.hi32, a.cov[i]));
-      atomicAdd(&hist[c], 1u);
-      a.qchunk[i] = (uint16_t)c;  // (kMaxChunks + 1 <= 2^16)
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = q0 + (uint64_t)(sub * kPer + k) * kQT;
+      cv[k] = i < a.ncov ? a.cov[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = q0 + (uint64_t)(sub * kPer + k) * kQT;
+      if (i < a.ncov) {
+        const uint32_t c = chunk_of(a, L, query_pc(a.hi32, cv[k]));
+        atomicAdd(&hist[c], 1u);
+        a.qchunk[i] = (uint16_t)c;  // (kMaxChunks + 1 <= 2^16)
+      }
     }
   }
   __syncthreads();
@@ -359,79 +374,91 @@ __global__ void k_q_chunk_off(ChunkArgs a) {
 // (LDS atomics) on top of the (chunk, tile) offset from the scan; each
 // query's chunk comes from the count kernel.  The tile is staged in LDS in
 // chunk order, then written out slot by slot, so a wave's stores are runs of
-// consecutive addresses.  (Measured and removed in r05: one 8-B store per
-// query, 1.08 ms against 0.84 per 100M queries; the chunk searched again
-// instead of read back, +0.27 ms.)
-template <int kPer>
+// consecutive addresses.  A workgroup takes kSub sub-tiles of one count-table
+// column, each chunk's slots carried from one sub-tile to the next.  (Measured
+// and removed: one 8-B store per query, 1.08 ms against 0.84 per 100M
+// queries; the chunk searched again instead of read back, +0.27 ms; r05:
+// sub-tiles of 4K queries at two workgroups per CU, 0.74 against 0.61 ms --
+// the shorter runs cost more than the occupancy gains; the next sub-tile's
+// loads issued before the write-out, no change.)
+template <int kPer, int kSub>
 __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
   constexpr uint32_t kT = kQT * kPer;
-  __shared__ uint32_t hist[kMaxChunks + 1];  // counts, then the tile's chunk offsets
-  __shared__ uint32_t base[kMaxChunks + 1];  // each chunk's first slot for this tile
+  __shared__ uint32_t hist[kMaxChunks + 1];  // counts, then the sub-tile's chunk offsets
+  __shared__ uint32_t base[kMaxChunks + 1];  // each chunk's next slot (the tile's first, then carried)
   __shared__ uint2 stage[kT];
   __shared__ uint16_t cid[kT];
   __shared__ uint32_t wsum[kQT / 64 + 1];
-  for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
-  __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * kT;
-  const uint64_t q0 = t0 + threadIdx.x;
-  uint32_t cv[kPer], ch[kPer], rk[kPer];
+  {
+    const uint32_t col = tile_col(blockIdx.x, a.tw);
+    for (uint32_t c = threadIdx.x; c <= a.nch; c += kQT) base[c] = (uint32_t)a.toff[(uint64_t)c * a.tw + col];
+  }
+  for (int sub = 0; sub < kSub; sub++) {
+    const uint64_t t0 = ((uint64_t)blockIdx.x * kSub + sub) * kT;
+    if (t0 >= a.ncov) break;  // (block-uniform)
+    for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
+    __syncthreads();
+    const uint64_t q0 = t0 + threadIdx.x;
+    uint32_t cv[kPer], ch[kPer], rk[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint64_t i = q0 + (uint64_t)k * kQT;
-    ch[k] = 0xFFFFFFFFu;
-    if (i < a.ncov) {
-      cv[k] = a.cov[i];
-      ch[k] = a.qchunk[i];
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = q0 + (uint64_t)k * kQT;
+      ch[k] = 0xFFFFFFFFu;
+      if (i < a.ncov) {
+        cv[k] = a.cov[i];
+        ch[k] = a.qchunk[i];
+      }
     }
-  }
 #pragma unroll
-  for (int k = 0; k < kPer; k++)
-    if (ch[k] != 0xFFFFFFFFu) rk[k] = atomicAdd(&hist[ch[k]], 1u);
-  __syncthreads();
-  // per thread kPerT consecutive chunks: the (chunk, tile) base and the
-  // exclusive scan of the counts (the chunk's first staging slot)
-  constexpr uint32_t kPerT = (kMaxChunks + 1 + kQT - 1) / kQT;
-  const uint32_t c0 = threadIdx.x * kPerT;
-  uint32_t h[kPerT], run = 0;
+    for (int k = 0; k < kPer; k++)
+      if (ch[k] != 0xFFFFFFFFu) rk[k] = atomicAdd(&hist[ch[k]], 1u);
+    __syncthreads();
+    // per thread kPerT consecutive chunks: the (chunk, tile) base and the
+    // exclusive scan of the counts (the chunk's first staging slot)
+    constexpr uint32_t kPerT = (kMaxChunks + 1 + kQT - 1) / kQT;
+    const uint32_t c0 = threadIdx.x * kPerT;
+    uint32_t h[kPerT], run = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < kPerT; j++) {
-    const uint32_t c = c0 + j;
-    h[j] = c <= a.nch ? hist[c] : 0u;
-    run += h[j];
-  }
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t incl = sgd::wave_incl_add(run);
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const uint32_t x = threadIdx.x < kQT / 64 ? wsum[threadIdx.x] : 0u;
-    const uint32_t xi = sgd::wave_incl_add(x);
-    if (threadIdx.x < kQT / 64) wsum[threadIdx.x] = xi - x;
-  }
-  __syncthreads();
-  uint32_t off = wsum[wv] + incl - run;
-#pragma unroll
-  for (uint32_t j = 0; j < kPerT; j++) {
-    const uint32_t c = c0 + j;
-    if (c <= a.nch) {
-      base[c] = h[j] ? (uint32_t)a.toff[(uint64_t)c * a.tw + tile_col(blockIdx.x, a.tw)] : 0u;
-      hist[c] = off;
+    for (uint32_t j = 0; j < kPerT; j++) {
+      const uint32_t c = c0 + j;
+      h[j] = c <= a.nch ? hist[c] : 0u;
+      run += h[j];
     }
-    off += h[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPer; k++)
-    if (ch[k] != 0xFFFFFFFFu) {
-      const uint32_t slot = hist[ch[k]] + rk[k];
-      stage[slot] = make_uint2(cv[k], (uint32_t)(q0 + (uint64_t)k * kQT));
-      cid[slot] = (uint16_t)ch[k];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t incl = sgd::wave_incl_add(run);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const uint32_t x = threadIdx.x < kQT / 64 ? wsum[threadIdx.x] : 0u;
+      const uint32_t xi = sgd::wave_incl_add(x);
+      if (threadIdx.x < kQT / 64) wsum[threadIdx.x] = xi - x;
     }
-  __syncthreads();
-  const uint32_t nv = (uint32_t)min<uint64_t>(kT, a.ncov - t0);
-  for (uint32_t i = threadIdx.x; i < nv; i += kQT) {
-    const uint32_t c = cid[i];
-    a.grouped[base[c] + (i - hist[c])] = stage[i];
+    __syncthreads();
+    uint32_t off = wsum[wv] + incl - run;
+#pragma unroll
+    for (uint32_t j = 0; j < kPerT; j++) {
+      const uint32_t c = c0 + j;
+      if (c <= a.nch) hist[c] = off;
+      off += h[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (ch[k] != 0xFFFFFFFFu) {
+        const uint32_t slot = hist[ch[k]] + rk[k];
+        stage[slot] = make_uint2(cv[k], (uint32_t)(q0 + (uint64_t)k * kQT));
+        cid[slot] = (uint16_t)ch[k];
+      }
+    __syncthreads();
+    const uint32_t nv = (uint32_t)min<uint64_t>(kT, a.ncov - t0);
+    for (uint32_t i = threadIdx.x; i < nv; i += kQT) {
+      const uint32_t c = cid[i];
+      a.grouped[base[c] + (i - hist[c])] = stage[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPerT; j++)  // (the next sub-tile's slots follow this one's)
+      if (c0 + j <= a.nch) base[c0 + j] += h[j];
   }
 }
 
@@ -596,14 +623,26 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
       }
     };
     if (!kDirect) {
-      for (uint64_t i = p + threadIdx.x; i < e; i += kCT) {
-        const uint2 g = a.grouped[i];
-        uint32_t j;
-        bool exact, hit;
-        uint64_t sym;
-        lookup(query_pc(a.hi32, g.x), j, exact, hit, sym);
-        if (hit) first_query(sym, g.y);
-        if (hit && exact && ldel[j] < g.y + 1) atomicMax(&ldel[j], g.y + 1);
+      // four queries per thread in flight (their loads issued together)
+      constexpr int kU = 4;
+      for (uint64_t i0 = p + threadIdx.x; i0 < e; i0 += (uint64_t)kU * kCT) {
+        uint2 gq[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const uint64_t i = i0 + (uint64_t)u * kCT;
+          gq[u] = i < e ? a.grouped[i] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          if (i0 + (uint64_t)u * kCT >= e) break;
+          const uint2 g = gq[u];
+          uint32_t j;
+          bool exact, hit;
+          uint64_t sym;
+          lookup(query_pc(a.hi32, g.x), j, exact, hit, sym);
+          if (hit) first_query(sym, g.y);
+          if (hit && exact && ldel[j] < g.y + 1) atomicMax(&ldel[j], g.y + 1);
+        }
       }
     } else {
       // Queries in PC order: each thread takes a contiguous run, so a PC
@@ -656,13 +695,19 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
   }
 }
 
+// per symbol, the first symbol with the same start (handledFuncs is keyed by
+// start, cover.go:288)
+__global__ void k_sym_leader(RepArgs a) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < a.nsym) a.leader[s] = (uint32_t)lb_idx(a.sstart, a.nsym, a.istart, a.sstart[s]);
+}
+
 __global__ void k_rep_group(RepArgs a) {
   uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.nsym) return;
   uint32_t f = a.first_q[s];
   if (f == 0xFFFFFFFFu) return;
-  uint64_t leader = lb64(a.sstart, a.nsym, a.sstart[s]);  // handledFuncs keyed by start, cover.go:288
-  atomicMin((unsigned long long*)&a.group_first[leader], ((unsigned long long)f << 32) | (unsigned long long)s);
+  atomicMin((unsigned long long*)&a.group_first[a.leader[s]], ((unsigned long long)f << 32) | (unsigned long long)s);
 }
 
 __global__ void k_rep_final(RepArgs a) {
@@ -670,11 +715,11 @@ __global__ void k_rep_final(RepArgs a) {
   if (j >= a.npcs) return;
   uint64_t c = a.pcs[j];
   int64_t best = -1;  // latest add time
-  uint64_t g = ub64(a.sstart, a.nsym, c);  // symbols [0, g) have start <= c
+  uint64_t g = ub_idx(a.sstart, a.nsym, a.istart, c);  // symbols [0, g) have start <= c
   while (g > 0) {
     uint64_t last = g - 1;                 // last symbol of the group
     if (a.send[last] < c) break;           // ends non-decreasing: nothing earlier reaches c
-    uint64_t leader = lb64(a.sstart, a.nsym, a.sstart[last]);
+    uint64_t leader = a.leader[last];
     uint64_t gf = a.group_first[leader];
     if (gf != ~0ull) {
       uint32_t sym = (uint32_t)gf;
@@ -766,10 +811,12 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     I.sh = sh;
     I.nb = nb;
   };
-  RadixIdx iend{}, ipcs{};
+  RadixIdx iend{}, ipcs{}, istart{};
   plan_idx(nsym, sym_end[0], sym_end[nsym - 1], iend);
   plan_idx(nall, all_pcs[0], all_pcs[nall - 1], ipcs);
-  const size_t o_ie = p.add(((uint64_t)iend.nb + 1) * 4), o_ip = p.add(((uint64_t)ipcs.nb + 1) * 4);
+  plan_idx(nsym, sym_start[0], sym_start[nsym - 1], istart);
+  const size_t o_ie = p.add(((uint64_t)iend.nb + 1) * 4), o_ip = p.add(((uint64_t)ipcs.nb + 1) * 4),
+               o_is = p.add(((uint64_t)istart.nb + 1) * 4), o_ld2 = p.add(nsym * 4);
   // chunked query path (k_q_*) up to kMaxChunks chunks of call sites, the
   // per-query search passes (k_rep_first / k_rep_del) past them;
   // SG_REPORT_DIRECT=1 takes the latter at any size (a test hook for the
@@ -777,8 +824,8 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   const char* direct_env = getenv("SG_REPORT_DIRECT");
   const bool chunked = nall <= (uint64_t)kSites * kMaxChunks && !(direct_env && atoi(direct_env));
   const uint32_t nch = div_up(nall, kSites);
-  // query tiles: 8K queries per count / scatter workgroup
-  const uint32_t ntq = div_up(ncov, (uint64_t)kQT * kSQPer);
+  // query tiles: 64K queries per count / scatter workgroup
+  const uint32_t ntq = div_up(ncov, (uint64_t)kQT * kSQPer * kSQSub);
   const uint32_t tw = 8 * div_up(ntq, 8);
   const uint64_t ntc = chunked ? ((uint64_t)nch + 1) * tw : 1;
   const size_t o_bnd = p.add((uint64_t)nch * 8), o_sr = p.add(((uint64_t)nch + 1) * 8),
@@ -812,8 +859,11 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
   uint64_t* dout = (uint64_t*)ws_at(ctx, o_out);
   iend.r = (const uint32_t*)ws_at(ctx, o_ie);
   ipcs.r = (const uint32_t*)ws_at(ctx, o_ip);
+  istart.r = (const uint32_t*)ws_at(ctx, o_is);
   a.iend = iend;
   a.ipcs = ipcs;
+  a.istart = istart;
+  a.leader = (uint32_t*)ws_at(ctx, o_ld2);
   SG_HIP(hipMemcpyAsync((void*)a.cov, cov, ncov * 4, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync((void*)a.sstart, sym_start, nsym * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync((void*)a.send, sym_end, nsym * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -828,6 +878,9 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
                        (uint64_t)nsym, iend.lo, iend.sh, iend.nb, (uint32_t*)iend.r);
     hipLaunchKernelGGL(k_radix_index, dim3(div_up((uint64_t)ipcs.nb + 1, 256)), dim3(256), 0, ctx->stream, a.pcs,
                        (uint64_t)nall, ipcs.lo, ipcs.sh, ipcs.nb, (uint32_t*)ipcs.r);
+    hipLaunchKernelGGL(k_radix_index, dim3(div_up((uint64_t)istart.nb + 1, 256)), dim3(256), 0, ctx->stream,
+                       a.sstart, (uint64_t)nsym, istart.lo, istart.sh, istart.nb, (uint32_t*)istart.r);
+    hipLaunchKernelGGL(k_sym_leader, dim3(div_up(nsym, 256)), dim3(256), 0, ctx->stream, a);
   }
   if (chunked) {
     ChunkArgs k{};
@@ -903,7 +956,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
       hipLaunchKernelGGL(k_site_index, dim3(div_up((uint64_t)nch * (kSiteIdx + 1), 256)), dim3(256), 0, ctx->stream,
                          k);
       if (tw != ntq) SG_HIP(hipMemsetAsync(k.tcount, 0, ntc * 4, ctx->stream));  // (the padding columns)
-      hipLaunchKernelGGL(k_q_count<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      hipLaunchKernelGGL((k_q_count<kSQPer, kSQSub>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
       rc = scan_counts(ctx, k.tcount, k.toff, ntc, scan_off);
       if (rc) return rc;
       hipLaunchKernelGGL(k_q_chunk_off, dim3(div_up((uint64_t)nch + 2, 256)), dim3(256), 0, ctx->stream, k);
@@ -912,7 +965,7 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
     }
     if (unsorted) {
       ScopedTimer tm(ctx, "report_scatter_q");
-      hipLaunchKernelGGL(k_q_scatter<kSQPer>, dim3(ntq), dim3(kQT), 0, ctx->stream, k);
+      hipLaunchKernelGGL((k_q_scatter<kSQPer, kSQSub>), dim3(ntq), dim3(kQT), 0, ctx->stream, k);
     }
     {
       ScopedTimer tm(ctx, "report_chunks");

@@ -147,16 +147,19 @@ def test_union_fold_byte_map_edges(ctx, monkeypatch):
 @pytest.mark.gpu
 def test_union_fold_lds_groups(ctx):
     """Many groups of canonical lists: a workgroup sorts each group in LDS
-    (sg_fold.hip k_fold_lds, groups of <= 16384 values).  Groups at and around
-    that size (one past it: the whole fold takes the key sort), empty groups,
-    one-value groups, constant groups (no digit pass), values over the whole
-    32-bit range (four passes), the sentinel at the ends of lists."""
+    (sg_fold.hip k_fold_lds, groups of <= 32768 values in three forms), the
+    bigger groups fold beside them by the key sort (k_fold_bigkeys /
+    k_fold_bigmove).
+    Groups at and around that size, several big ones (one holding the
+    sentinel, one of a single repeated value spread over many lists), empty
+    groups, one-value groups, constant groups (no digit pass), values over the
+    whole 32-bit range (four passes), the sentinel at the ends of lists."""
     from syzkaller_amd import cover as C
 
     rng = np.random.default_rng(57)
-    for top in (16384, 16385):
+    for top, extra in ((16384, []), (16385, []), (16385, [70000, 20000, 40000, 32768, 32769])):
         covs, calls = [], []
-        sizes = [top, 16000, 1, 0, 5, 300, 8191, 8192, 2, 2]
+        sizes = [top, 16000, 1, 0, 5, 300, 8191, 8192, 2, 2] + extra
         for gi, sz in enumerate(sizes):
             left = sz
             while left > 0:  # a group's values over several lists, repeats across lists
@@ -164,12 +167,16 @@ def test_union_fold_lds_groups(ctx):
                 if gi == 4:
                     v = np.full(1, 0x12345678, np.uint32)  # a constant group
                     m = 1
-                elif gi == 5:
+                elif gi in (5, 12):
                     v = np.unique(rng.integers(0, 1 << 32, size=m, dtype=np.uint64)).astype(np.uint32)
+                elif gi == 11:
+                    v = np.full(1, 0xABCD, np.uint32)  # a big group of one value
                 else:
                     v = (0x81000000 + 16 * rng.choice(1 << 20, size=m, replace=False)).astype(np.uint32)
                 if gi == 9:
                     v = np.array([7, 0xFFFFFFFF], np.uint32)
+                if gi == 12 and left == sz:
+                    v = np.unique(np.append(v, 0xFFFFFFFF).astype(np.uint32))
                 covs.append(np.sort(v))
                 calls.append(gi)
                 left -= max(1, v.size)
