@@ -341,13 +341,21 @@ __global__ __launch_bounds__(kQT) void k_q_count(ChunkArgs a) {
   for (uint32_t i = threadIdx.x; i <= a.nch; i += kQT) hist[i] = 0;
   __syncthreads();
   const uint64_t q0 = (uint64_t)blockIdx.x * kQT * kPer * kSub + threadIdx.x;
-  for (int sub = 0; sub < kSub; sub++) {
-    uint32_t cv[kPer];
+  // each sub-tile's loads issued before the one before is looked up
+  uint32_t cn[kPer];
+  auto load = [&](int sub) {
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const uint64_t i = q0 + (uint64_t)(sub * kPer + k) * kQT;
-      cv[k] = i < a.ncov ? a.cov[i] : 0u;
+      cn[k] = a.cov[i < a.ncov ? i : 0];
     }
+  };
+  load(0);
+  for (int sub = 0; sub < kSub; sub++) {
+    uint32_t cv[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) cv[k] = cn[k];
+    if (sub + 1 < kSub) load(sub + 1);
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const uint64_t i = q0 + (uint64_t)(sub * kPer + k) * kQT;
@@ -623,15 +631,23 @@ __global__ __launch_bounds__(kCT) void k_q_chunk(ChunkArgs a) {
       }
     };
     if (!kDirect) {
-      // four queries per thread in flight (their loads issued together)
+      // four queries per thread per step, the next step's loads in flight
+      // while this one's are looked up
       constexpr int kU = 4;
-      for (uint64_t i0 = p + threadIdx.x; i0 < e; i0 += (uint64_t)kU * kCT) {
-        uint2 gq[kU];
+      uint2 gn[kU];
+      auto load = [&](uint64_t i0) {
 #pragma unroll
         for (int u = 0; u < kU; u++) {
           const uint64_t i = i0 + (uint64_t)u * kCT;
-          gq[u] = i < e ? a.grouped[i] : make_uint2(0u, 0u);
+          gn[u] = a.grouped[i < e ? i : p];
         }
+      };
+      load(p + threadIdx.x);
+      for (uint64_t i0 = p + threadIdx.x; i0 < e; i0 += (uint64_t)kU * kCT) {
+        uint2 gq[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) gq[u] = gn[u];
+        load(i0 + (uint64_t)kU * kCT);
 #pragma unroll
         for (int u = 0; u < kU; u++) {
           if (i0 + (uint64_t)u * kCT >= e) break;
