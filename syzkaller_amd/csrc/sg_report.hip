@@ -388,7 +388,10 @@ __global__ void k_q_chunk_off(ChunkArgs a) {
 // queries; the chunk searched again instead of read back, +0.27 ms; r05:
 // sub-tiles of 4K queries at two workgroups per CU, 0.74 against 0.61 ms --
 // the shorter runs cost more than the occupancy gains; the next sub-tile's
-// loads issued before the write-out, no change.)
+// loads issued before the write-out, no change; 8K-query sub-tiles at two
+// workgroups per CU -- each staged entry carrying its chunk, the slots in
+// registers, 80 KiB of LDS -- 0.64 ms: the write pattern, not occupancy,
+// bounds this kernel.)
 template <int kPer, int kSub>
 __global__ __launch_bounds__(kQT) void k_q_scatter(ChunkArgs a) {
   constexpr uint32_t kT = kQT * kPer;
