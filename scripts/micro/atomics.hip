@@ -1,7 +1,7 @@
 // Microbenchmark: global u32 atomicMin throughput at random addresses -- the
-// access of the claim path's first-owner table (sg_triage.hip k_claim: a
-// relaxed load, then atomicMin if it lowers the owner; 4 B per signal, 2^32
-// entries = 16 GiB).  Forms: no-return atomicMin, returning atomicMin, and the
+// access of a first-owner table (Minimize's k_min_claim, and round 4's
+// claim path for the triage: a relaxed load, then atomicMin if it lowers the
+// owner; 4 B per signal, 2^32 entries = 16 GiB).  Forms: no-return atomicMin, returning atomicMin, and the
 // read-checked form (load, then atomicMin when larger) on a table whose
 // entries are all larger (every check passes: the claim path's worst case).
 // Tables of 256 MiB, 4 GiB and 16 GiB; 256M atomics per launch.  Rates in

@@ -691,13 +691,13 @@ __global__ __launch_bounds__(kBlock) void k_add_flagged_segs(const uint32_t* __r
 // ---- Minimize (cover.go:120-146) -----------------------------------------------
 // One workgroup per input: its elements all carry its rank key, so there is
 // no per-element item search.  Each element lowers owner[v] to the key
-// (read-checked atomicMin, the same first-owner rule as k_claim).  An element
+// (read-checked atomicMin: the smallest key -- the earliest input -- owns v).  An element
 // that reads a key of an older generation (>= key_end: no element of this
 // call has written v yet) also sets v's bit in the touched bitmap (2^32 bits,
 // the set layout), so about one global atomicOr per distinct value: the
 // first current-generation writer of v always sets it.  The owners are then
 // flagged from the touched bitmap alone (k_min_owners, one read of 512 MiB)
-// instead of re-reading the corpus (k_resolve).
+// instead of re-reading the corpus.
 // Workgroups run in processing order (block b = the input of rank b, key
 // key_lo + b): the early ranks claim the corpus's common values first, so a
 // later element's read-check mostly finds a smaller key and issues no atomic,
