@@ -444,17 +444,6 @@ __global__ __launch_bounds__(kHBThreads) void k_hist_bytes(const uint8_t* __rest
 constexpr uint32_t kTraceDedup = 1024;  // slots (8 KiB of LDS)
 __device__ __forceinline__ uint32_t dedup_slot(uint32_t sig) { return (sig * 0x9E3779B1u) >> 22; }
 
-// Call starts inside a pass-1 tile: its <= kRecCap + 1 record offsets as an
-// LDS bitmap over the tile's positions.
-__device__ __forceinline__ void trace_starts(const uint64_t* __restrict__ rec_off, uint64_t nrec, uint32_t r0,
-                                             uint32_t s0, uint32_t s1, uint32_t* cs, int tid) {
-  const uint32_t wn = (uint32_t)(nrec + 1 - r0 < kRecCap + 1 ? nrec + 1 - r0 : kRecCap + 1);
-  for (uint32_t i = tid; i < wn; i += kPThreads) {
-    const uint64_t o = rec_off[r0 + i];
-    if (o >= s0 && o < s1) atomicOr(&cs[(o - s0) >> 5], 1u << ((o - s0) & 31));
-  }
-}
-
 // the previous PC of position e for lane-strided loads (x = this lane's PC,
 // xp = pcs[e - 1] loaded by lane 0 of the wave)
 __device__ __forceinline__ uint32_t trace_prev(uint32_t x, uint32_t xp) {
@@ -487,6 +476,13 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
     x[k] = e < s1 ? pcs[e] : 0u;
     xp[k] = lane == 0 && e < s1 && e > 0 ? pcs[e - 1] : 0u;
   }
+  // the tile's record offsets, loaded with the PCs (one per thread: a barrier
+  // waits for every load in flight, so a load after the first one would add a
+  // second memory round trip per tile)
+  static_assert(kRecCap + 1 <= kPThreads, "one record offset per thread");
+  const uint32_t r0 = trec[t];
+  const uint32_t wn = (uint32_t)(nrec + 1 - r0 < kRecCap + 1 ? nrec + 1 - r0 : kRecCap + 1);
+  const uint64_t ro = (uint32_t)tid < wn ? rec_off[r0 + tid] : ~0ull;
 #pragma unroll
   for (int k = 0; k < 256 * 32 / 4 / kPThreads; k++)
     reinterpret_cast<uint4*>(rc)[k * kPThreads + tid] = make_uint4(0, 0, 0, 0);
@@ -494,7 +490,7 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
   for (int i = tid; i < (int)kTraceDedup; i += kPThreads) dd[i] = ~0ull;
   __syncthreads();
 #if SG_HT_ABL != 2  // (SG_HT_ABL: timing ablations, wrong results)
-  trace_starts(rec_off, nrec, trec[t], s0, s1, cs, tid);
+  if (ro >= s0 && ro < s1) atomicOr(&cs[(ro - s0) >> 5], 1u << ((ro - s0) & 31));  // call starts in the tile
 #endif
   __syncthreads();
   uint32_t live = 0;
@@ -715,6 +711,14 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
   // come from the wave itself)
   const uint32_t xp0 = kTrace && lane == 0 && ebase < s1 && ebase > 0 ? a.vals[ebase - 1] : 0u;
   const bool start0 = kTrace && a.rec_off[r0] == s0;  // does a call start at the tile's first position
+  // trace batches: the kept-entry words of the wave's steps, loaded before the
+  // barrier (which waits for every load in flight)
+  uint64_t kwv[kTrace ? kSteps : 1];
+  if (kTrace) {
+    const uint64_t* kw = a.keep + (uint64_t)t * (kPT / 64) + __builtin_amdgcn_readfirstlane(w) * (kPerWave / 64);
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) kwv[k] = kw[k];
+  }
   for (uint32_t i = tid; i < wn; i += kPThreads) {
     const uint64_t o = a.rec_off[r0 + i];
     win[i] = (uint16_t)(o <= s0 ? 0 : (o - s0 >= (uint64_t)kPT ? kPT : o - s0));
@@ -747,12 +751,9 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
     }
     // kept entries (non-zero, not an in-tile repeat): the histogram's words,
     // one per 64 positions -- wave w's step k is positions w kPerWave + 64 k ..
-    const uint64_t* kw = a.keep + (uint64_t)t * (kPT / 64) + __builtin_amdgcn_readfirstlane(w) * (kPerWave / 64);
 #pragma unroll
-    for (int k = 0; k < kSteps; k++) {
-      const uint64_t b = kw[k];
-      if (!((b >> lane) & 1ull)) vmask &= ~(1u << k);
-    }
+    for (int k = 0; k < kSteps; k++)
+      if (!((kwv[k] >> lane) & 1ull)) vmask &= ~(1u << k);
   }
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
@@ -834,7 +835,9 @@ __device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint3
   __syncthreads();
   const uint32_t nt = s1 - s0;
   // segments = the chunk's tiles (runs of this slice); value = the tile's
-  // first record relative to the group
+  // first record relative to the group.  (Loading thread k's tile values
+  // before the barrier, which waits for every load in flight, measured slower
+  // in r05: 1.65 against 1.59 ms per C2 launch.)
   const uint32_t* row = a.goff1 + (uint64_t)d * a.T + tf;
   seg_build(
       L, sidx,
