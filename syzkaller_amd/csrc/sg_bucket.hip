@@ -476,9 +476,8 @@ __global__ __launch_bounds__(kPThreads) void k_hist_trace(const uint32_t* __rest
     x[k] = e < s1 ? pcs[e] : 0u;
     xp[k] = lane == 0 && e < s1 && e > 0 ? pcs[e - 1] : 0u;
   }
-  // the tile's record offsets, loaded with the PCs (one per thread: a barrier
-  // waits for every load in flight, so a load after the first one would add a
-  // second memory round trip per tile)
+  // the tile's record offsets, loaded with the PCs (one per thread), so their
+  // round trip overlaps the PCs' instead of following the first barrier
   static_assert(kRecCap + 1 <= kPThreads, "one record offset per thread");
   const uint32_t r0 = trec[t];
   const uint32_t wn = (uint32_t)(nrec + 1 - r0 < kRecCap + 1 ? nrec + 1 - r0 : kRecCap + 1);
@@ -711,8 +710,9 @@ __device__ __forceinline__ void p1_tile(const P1Args& a, uint32_t* stage, uint32
   // come from the wave itself)
   const uint32_t xp0 = kTrace && lane == 0 && ebase < s1 && ebase > 0 ? a.vals[ebase - 1] : 0u;
   const bool start0 = kTrace && a.rec_off[r0] == s0;  // does a call start at the tile's first position
-  // trace batches: the kept-entry words of the wave's steps, loaded before the
-  // barrier (which waits for every load in flight)
+  // trace batches: the kept-entry words of the wave's steps, loaded with the
+  // tile (loaded where they are used, after the segment build, their round
+  // trip was exposed: 2.38 -> 2.21 ms per C2 trace launch)
   uint64_t kwv[kTrace ? kSteps : 1];
   if (kTrace) {
     const uint64_t* kw = a.keep + (uint64_t)t * (kPT / 64) + __builtin_amdgcn_readfirstlane(w) * (kPerWave / 64);
@@ -835,9 +835,9 @@ __device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint3
   __syncthreads();
   const uint32_t nt = s1 - s0;
   // segments = the chunk's tiles (runs of this slice); value = the tile's
-  // first record relative to the group.  (Loading thread k's tile values
-  // before the barrier, which waits for every load in flight, measured slower
-  // in r05: 1.65 against 1.59 ms per C2 launch.)
+  // first record relative to the group.  (Loading thread k's tile values with
+  // the chunk instead, selected inside the build, measured slower in r05: 1.65
+  // against 1.59 ms per C2 launch.)
   const uint32_t* row = a.goff1 + (uint64_t)d * a.T + tf;
   seg_build(
       L, sidx,
