@@ -615,19 +615,33 @@ __device__ __forceinline__ void seg_clear(SegLds<IdxT>& L, int tid) {
   if (tid == 0) L.kinit = 0;
 }
 
+// one segment: start p, the next segment's start nx (0xFFFFFFFF: none), value v
+template <typename IdxT>
+__device__ __forceinline__ void seg_mark(SegLds<IdxT>& L, IdxT* sidx, uint32_t p, uint32_t nx, uint32_t v,
+                                         uint32_t n) {
+  if (p == 0) {
+    if (nx > 0) atomicMax(&L.kinit, v);
+  } else if (p < n && nx > p) {
+    atomicOr(&L.sbits[p >> 5], 1u << (p & 31));
+    sidx[p] = (IdxT)v;
+  }
+}
+
+template <typename IdxT>
+__device__ __forceinline__ void seg_finish(SegLds<IdxT>& L, IdxT* sidx, int tid);
+
 // call after seg_clear + a barrier; ends with a barrier
 template <typename IdxT, typename StF, typename ValF>
 __device__ __forceinline__ void seg_build(SegLds<IdxT>& L, IdxT* sidx, StF st, ValF val, uint32_t m, uint32_t n,
                                           int tid) {
-  for (uint32_t k = tid; k < m; k += kPThreads) {
-    const uint32_t p = st(k), nx = k + 1 < m ? st(k + 1) : 0xFFFFFFFFu;
-    if (p == 0) {
-      if (nx > 0) atomicMax(&L.kinit, val(k));
-    } else if (p < n && nx > p) {
-      atomicOr(&L.sbits[p >> 5], 1u << (p & 31));
-      sidx[p] = (IdxT)val(k);
-    }
-  }
+  for (uint32_t k = tid; k < m; k += kPThreads)
+    seg_mark(L, sidx, st(k), k + 1 < m ? st(k + 1) : 0xFFFFFFFFu, val(k), n);
+  seg_finish(L, sidx, tid);
+}
+
+// the segments' marks -> the per-word maxima (after seg_mark; ends with a barrier)
+template <typename IdxT>
+__device__ __forceinline__ void seg_finish(SegLds<IdxT>& L, IdxT* sidx, int tid) {
   __syncthreads();
   constexpr int kWL = kPT / 32 / 64;  // bitmap words per lane
   if (tid < 64) {  // prefix max over the kPT / 32 words
@@ -831,21 +845,31 @@ __device__ __forceinline__ void p2_chunk(const P2Args& a, uint32_t* stage, uint3
     gbase[f] = a.goff2[(uint64_t)f * G2 + c];
     cnt[f] = a.hist2[(uint64_t)f * G2 + c];
   }
+  // segments = the chunk's tiles (runs of this slice); value = the tile's
+  // first record relative to the group.  A chunk of at most kPThreads tiles
+  // (nearly all) has thread k's tile loaded with the chunk's entries, so the
+  // loads' round trip is not exposed after the barrier.
+  const uint32_t* row = a.goff1 + (uint64_t)d * a.T + tf;
+  auto clampst = [&](uint32_t o) { return o <= s0 ? 0u : (o - s0 >= (uint32_t)kPT ? (uint32_t)kPT : o - s0); };
+  const bool one = m <= (uint32_t)kPThreads;  // (block-uniform)
+  const uint32_t ku = (uint32_t)tid;
+  uint32_t pst = 0, pnx = 0, pvl = 0;
+  if (one && ku < m) {
+    pst = row[ku];
+    pnx = ku + 1 < m ? row[ku + 1] : 0u;
+    pvl = a.trec[tf + ku];
+  }
   seg_clear(L, tid);
   __syncthreads();
   const uint32_t nt = s1 - s0;
-  // segments = the chunk's tiles (runs of this slice); value = the tile's
-  // first record relative to the group.  (Loading thread k's tile values with
-  // the chunk instead, selected inside the build, measured slower in r05: 1.65
-  // against 1.59 ms per C2 launch.)
-  const uint32_t* row = a.goff1 + (uint64_t)d * a.T + tf;
-  seg_build(
-      L, sidx,
-      [&](uint32_t k) {
-        const uint32_t o = row[k];
-        return o <= s0 ? 0u : (o - s0 >= (uint32_t)kPT ? (uint32_t)kPT : o - s0);
-      },
-      [&](uint32_t k) { return a.trec[tf + k] - rg0; }, m, nt, tid);
+  if (one) {
+    if (ku < m) seg_mark(L, sidx, clampst(pst), ku + 1 < m ? clampst(pnx) : 0xFFFFFFFFu, pvl - rg0, nt);
+    seg_finish(L, sidx, tid);
+  } else {
+    seg_build(
+        L, sidx, [&](uint32_t k) { return clampst(row[k]); }, [&](uint32_t k) { return a.trec[tf + k] - rg0; }, m,
+        nt, tid);
+  }
   const uint32_t el0 = ebase + lane - s0;
   uint32_t rp[kSteps / 2] = {};  // records in group, two 16-bit per register
 #pragma unroll
