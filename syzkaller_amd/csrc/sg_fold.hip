@@ -452,7 +452,8 @@ __global__ void k_fold_bigmove(const uint32_t* __restrict__ uout, const uint64_t
 }
 
 constexpr int SG_EOVERFLOW_FOLD = 1;  // internal: the keys do not fit 64 bits
-constexpr int SG_EREPEATS_FOLD = 2;   // internal: a list repeats a value (not the per-group LDS fold's)
+constexpr int SG_EREPEATS_FOLD = 2;   // internal: not the per-group LDS fold's (a list repeats a value, or
+                                      // more big groups than one launch's grid holds): the key sort
 
 static uint32_t bits_for(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
 
@@ -475,6 +476,7 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
       bl.push_back(gi);
       bk.push_back(bk.back() + (gs[gi + 1] - gs[gi]));
     }
+  if (bl.size() > 65535) return SG_EREPEATS_FOLD;  // (k_fold_bigkeys: a grid row per big group)
   const uint32_t nbig = (uint32_t)bl.size();
   const uint64_t NB = bk.back(), ntb = div_up(NB, (uint64_t)kFuTile);
   WsPlan p;
