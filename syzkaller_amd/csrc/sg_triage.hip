@@ -537,30 +537,38 @@ __global__ __launch_bounds__(kOwnBigT) void k_own_big(OwnArgs a) {
   }
 }
 
-// [po[r].x, po[r].y): record r's keys (po zeroed: records without keys stay
-// empty), from the run boundaries of the sorted keys: each key against the
-// next one, kBoundPer keys per thread a block apart (all loads coalesced)
-constexpr int kBoundPer = 8;
-__global__ __launch_bounds__(256) void k_own_bounds(const uint64_t* __restrict__ k, uint64_t n,
-                                                    uint2* __restrict__ po) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * (256 * kBoundPer) + threadIdx.x;
-  uint32_t cur[kBoundPer], nxt[kBoundPer];
-#pragma unroll
-  for (int j = 0; j < kBoundPer; j++) {
-    const uint64_t i = i0 + 256 * j;
-    cur[j] = i < n ? (uint32_t)(k[i] >> 32) : 0u;
-    nxt[j] = i + 1 < n ? (uint32_t)(k[i + 1] >> 32) : 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (int j = 0; j < kBoundPer; j++) {
-    const uint64_t i = i0 + 256 * j;
-    if (i >= n) break;
-    if (i == 0) po[cur[j]].x = 0;
-    if (cur[j] != nxt[j]) {
-      po[cur[j]].y = (uint32_t)(i + 1);
-      if (i + 1 < n) po[nxt[j]].x = (uint32_t)(i + 1);
+// [po[r].x, po[r].y): record r's keys.  The sorted keys are ordered by
+// (record & 0xFFFF, record >> 16) -- two 8-bit passes over the low 16 bits
+// of group-major pairs -- so a thread per record finds the first and
+// one-past-last positions of its composite rank with two interleaved binary
+// searches (every record written, no memset).  (r05: 0.31 ms per C2 batch
+// against 0.40 for a coalesced pass over all 208M keys comparing neighbours.)
+__device__ __forceinline__ uint32_t own_rank(uint32_t rec) { return (rec << 16) | (rec >> 16); }
+
+__global__ __launch_bounds__(256) void k_own_bounds_search(const uint64_t* __restrict__ k, uint64_t n, uint32_t nr,
+                                                           uint2* __restrict__ po) {
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= nr) return;
+  const uint32_t t = own_rank(r);
+  uint64_t lo0 = 0, hi0 = n, lo1 = 0, hi1 = n;  // first rank >= t, first rank > t
+  while (lo0 < hi0 || lo1 < hi1) {
+    const uint64_t m0 = (lo0 + hi0) >> 1, m1 = (lo1 + hi1) >> 1;
+    const uint32_t c0 = lo0 < hi0 ? own_rank((uint32_t)(k[m0] >> 32)) : 0u;
+    const uint32_t c1 = lo1 < hi1 ? own_rank((uint32_t)(k[m1] >> 32)) : 0u;
+    if (lo0 < hi0) {
+      if (c0 < t)
+        lo0 = m0 + 1;
+      else
+        hi0 = m0;
+    }
+    if (lo1 < hi1) {
+      if (c1 <= t)
+        lo1 = m1 + 1;
+      else
+        hi1 = m1;
     }
   }
+  po[r] = make_uint2((uint32_t)lo0, (uint32_t)lo1);
 }
 
 // gs[g] = roff[g << 16] (g < ng): where group g's pairs start
@@ -1075,10 +1083,8 @@ static int owned_outputs(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const 
       }
     }
     ScopedTimer tm(ctx, "owned_sweep");
-    SG_HIP(hipMemsetAsync(po, 0, nr * 8, ctx->stream));
-    if (np)
-      hipLaunchKernelGGL(k_own_bounds, dim3(div_up(np, 256 * kBoundPer)), dim3(256), 0, ctx->stream,
-                         (const uint64_t*)sorted, np, po);
+    hipLaunchKernelGGL(k_own_bounds_search, dim3(div_up(nr, 256)), dim3(256), 0, ctx->stream, (const uint64_t*)sorted,
+                       np, (uint32_t)nr, po);
     OwnArgs oa{d_vals, roff, e0, (uint32_t)nr, sorted, po, d_rec_new ? d_rec_new + r0 : nullptr, s.dmask, big, nvals,
                big + nr + 1};
     SG_HIP(hipMemsetAsync(big + nr + 1, 0, 4, ctx->stream));
