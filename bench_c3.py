@@ -171,6 +171,9 @@ def run_c3(ctx, args, cfg, rank, world):
     tri.step(maxsig, None, b.vals, b.off, b.nvals, b.nrec, rec_base, rec_new)
     torch.cuda.synchronize()
     last = dict(tri.last)
+    # the same batch's exchange in both forms (the one it took and the other),
+    # from the counts every rank gathered with it
+    xmodel = tri.exchange_model() if prefix else None
     queued = int(rec_new[: b.nrec].sum().item())
     acct_rank = {"n_in": b.nvals, "n_uniq": n_uniq(b, calls), "n_cand": c.value, "n_rec": b.nrec,
                  "n_queued": queued, "pairs_sent": last.get("pairs_sent", 0),
@@ -256,6 +259,7 @@ def run_c3(ctx, args, cfg, rank, world):
         "kernels": kernels,
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,
+        "exchange_bytes_by_form_first_batch": xmodel,
         "prefix_forms": forms[-args.steps:] if prefix and forms else None,
         "exchange_forms": [f for f, _ in xchg[-args.steps:]] if prefix else None,
         "path": ("prefix (syzkaller_amd/shard.py PrefixTriage)" if prefix else

@@ -489,6 +489,21 @@ class PrefixTriage:
         frac = max(n / max(e, 1) for n, e in c)
         return "sparse" if frac < self.sparse_below else "dense"
 
+    def exchange_model(self):
+        """Bytes per rank that the last finished batch's exchange takes in each
+        form, whichever it used: dense (the bitmaps: fixed) and sparse (the
+        candidate lists, from every rank's count of distinct signals outside
+        maxSignal, gathered with the batch; the caller has synchronised).  None
+        when the batch ran without the counts (one rank without collectives,
+        or a form that does not count)."""
+        last, G = self.last, self.comm.world
+        if "slot" not in last or last.get("form") == "default":
+            return None
+        counts = self.slots[last["slot"]]["cnts_h"].view(-1, 2)[:, 0].tolist()
+        m = max(counts)
+        dense = (4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))) + 16 * (G - 1)
+        return {"dense": dense, "sparse": (4 * m + 16) * (G - 1), "candidates_max": m}
+
     def _buf(self, name, n, dtype=torch.int32):
         b = self._bufs.get(name)
         if b is None or b.numel() < n:
@@ -561,7 +576,7 @@ class PrefixTriage:
             pend["sparse"] = (allc, counts, m)
             pend["got_p"] = pend["got_t"] = _Done()
             pend["last"] = {"nrec_total": nrec_total, "exchange": "sparse", "form": "pairs",
-                            "exchange_bytes": (4 * m + 16) * (G - 1), "candidates": counts}
+                            "exchange_bytes": (4 * m + 16) * (G - 1), "candidates": counts, "slot": slot}
             return pend
         if c.rank > 0:
             b["pclean"] = False  # (the dense prefix lands in P)
@@ -595,7 +610,7 @@ class PrefixTriage:
         xb = 4 * self.W * (G - 1) if self.gather else 4 * self.S * (3 * (G - 1))
         pend["last"] = {"nrec_total": nrec_total, "exchange": "dense" if G > 1 else "local",
                         "exchange_bytes": xb + 16 * (G - 1),
-                        "form": {0: "kept", 1: "pairs", None: "default"}[form]}
+                        "form": {0: "kept", 1: "pairs", None: "default"}[form], "slot": slot}
         return pend
 
     def finish(self, pend):

@@ -178,6 +178,7 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
                            sparse_below=sparse_below)
         xforms = []  # each started batch's exchange form
         xbytes = []
+        models = []  # non-pipelined: tri.exchange_model() agrees with the bytes sent
         ms, ns = BitSet(), BitSet()
         ms.add(M0)
         out = []
@@ -204,6 +205,10 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
                 assert tri.step(ms, ns, v, o, e1 - e0, r1 - r0, r0, rec_new) == nrec
                 xforms.append(tri.last["exchange"])
                 xbytes.append(tri.last["exchange_bytes"])
+                # the batch's exchange in both forms: the one it took is what it sent
+                model = tri.exchange_model()
+                models.append(model is not None and model[tri.last["exchange"]] == tri.last["exchange_bytes"]
+                              and model["sparse"] == (4 * model["candidates_max"] + 16) * (world - 1))
                 continue
             # the next batch started (marked against the maxSignal that still
             # lacks this batch's total) before the previous one is finished
@@ -214,7 +219,7 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
         if pend is not None:
             finish(pend)
         q.put((rank, [(r0, fl[: r1 - r0].tolist()) for r0, r1, fl in out], ms.export(),
-               drained if drain else ns.export(), stages.forms, xforms, xbytes))
+               drained if drain else ns.export(), stages.forms, xforms, xbytes, models))
     finally:
         dist.destroy_process_group()
 
@@ -248,7 +253,8 @@ def _run_and_check(world, pipelined, gather, drain, pairs_below, exchange, spars
     res = {}
     xall = []
     for _ in range(world):
-        r, out, m, n, forms, xforms, xbytes = q.get(timeout=240)
+        r, out, m, n, forms, xforms, xbytes, models = q.get(timeout=240)
+        assert all(models), models
         if expect_x is None:  # (the default sparse_below, 0.05, is below the novelty here)
             assert set(xforms) == {"dense"}, xforms
         else:
