@@ -248,6 +248,108 @@ __device__ __forceinline__ uint32_t ballot_count(const uint32_t* sv, uint32_t ns
   }
 }
 
+// Difference / Intersection with every pair's first list of <= kMS values (C1:
+// traces against one large corpus signal): a workgroup per pair keeps a's
+// copy t of value x iff t >= (Difference) / < (Intersection) the count of x
+// in b, i.e. iff b[lower_bound(b, x) + t] != x (resp. ==); t from a search of
+// the staged a in LDS, the kept values written in order by a block scan (the
+// sentinel never kept, cover.go:97).  One
+// launch, no masks or global scan; each thread's four searches of b
+// interleaved.
+constexpr int kDU = 4;  // consecutive a elements per thread (kMT kDU = kMS)
+static_assert(kMT * kDU == kMS, "k_diff_small covers a small side");
+__global__ __launch_bounds__(kMT) void k_diff_small(SmallArgs m) {
+  __shared__ uint32_t sv[kMS];
+  __shared__ uint32_t wsum[kMWaves + 1];
+  const uint32_t k = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t na = (uint32_t)m.alen[k];
+  const uint64_t nb = m.blen[k];
+  const uint32_t* A = m.a + m.abeg[k];
+  const uint32_t* B = m.b + m.bbeg[k];
+  uint32_t x[kDU];
+#pragma unroll
+  for (int u = 0; u < kDU; u++) {
+    const uint32_t j = (uint32_t)tid * kDU + u;
+    x[u] = j < na ? A[j] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kDU; u++) {
+    const uint32_t j = (uint32_t)tid * kDU + u;
+    if (j < na) sv[j] = x[u];
+  }
+  __syncthreads();
+  // t: the copy index of x among a's equal values (a sorted)
+  uint32_t t[kDU];
+#pragma unroll
+  for (int u = 0; u < kDU; u++) {
+    const uint32_t j = (uint32_t)tid * kDU + u;
+    uint32_t lo = 0, hi = j < na ? j : 0;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sv[mid] < x[u])
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    t[u] = j - lo;
+  }
+  // lower_bound(b, x), four searches in flight
+  uint64_t lo[kDU], hi[kDU];
+#pragma unroll
+  for (int u = 0; u < kDU; u++) {
+    lo[u] = 0;
+    hi[u] = (uint32_t)tid * kDU + u < na ? nb : 0;
+  }
+  for (;;) {
+    bool any = false;
+    uint32_t v[kDU];
+#pragma unroll
+    for (int u = 0; u < kDU; u++) v[u] = lo[u] < hi[u] ? B[(lo[u] + hi[u]) >> 1] : 0u;
+#pragma unroll
+    for (int u = 0; u < kDU; u++)
+      if (lo[u] < hi[u]) {
+        const uint64_t mid = (lo[u] + hi[u]) >> 1;
+        if (v[u] < x[u])
+          lo[u] = mid + 1;
+        else
+          hi[u] = mid;
+        any |= lo[u] < hi[u];
+      }
+    if (!any) break;
+  }
+  // the count of x in b exceeds t iff b[lo + t] == x
+  uint32_t keep = 0, nk = 0;
+#pragma unroll
+  for (int u = 0; u < kDU; u++) {
+    const uint32_t j = (uint32_t)tid * kDU + u;
+    const uint64_t q = lo[u] + t[u];
+    const bool more = j < na && q < nb && B[q] == x[u];
+    const bool kp = j < na && x[u] != kSent && (m.op == SG_OP_DIFFERENCE ? !more : more);  // (cover.go:97)
+    keep |= (kp ? 1u : 0u) << u;
+    nk += kp ? 1u : 0u;
+  }
+  const uint32_t incl = sgd::wave_incl_add(nk);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < kMWaves; i++) {
+      const uint32_t c = wsum[i];
+      wsum[i] = acc;
+      acc += c;
+    }
+    wsum[kMWaves] = acc;
+  }
+  __syncthreads();
+  uint32_t at = wsum[w] + incl - nk;
+  uint32_t* out = m.out + m.obeg[k];
+#pragma unroll
+  for (int u = 0; u < kDU; u++)
+    if ((keep >> u) & 1u) out[at++] = x[u];
+  if (tid == 0) m.olen[k] = wsum[kMWaves];
+}
+
 template <bool kGap>
 __global__ __launch_bounds__(kMT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_merge_small(SmallArgs m) {
   __shared__ uint32_t sv[kMS];
@@ -1134,6 +1236,8 @@ int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint3
   bool bside = op == SG_OP_UNION || op == SG_OP_SYMDIFF;
   bool small = bside;  // every pair has a side that fits in LDS: one workgroup per pair
   for (size_t k = 0; k < npair && small; k++) small = std::min(a_len[k], b_len[k]) <= (uint64_t)kMS;
+  bool asmall = !bside;  // Difference / Intersection, every first list fits in LDS
+  for (size_t k = 0; k < npair && asmall; k++) asmall = a_len[k] <= (uint64_t)kMS;
   uint64_t na = aoff[npair], nb = bside ? boff[npair] : 0;
   uint64_t nca = ((na + kTile - 1) / kTile) * kChunksPerTile, ncb = ((nb + kTile - 1) / kTile) * kChunksPerTile;
   WsPlan p;
@@ -1155,7 +1259,11 @@ int merge_dev(sg_ctx* ctx, int op, const uint32_t* da, const uint32_t* db, uint3
   SG_HIP(hipMemcpyAsync(m_blen, b_len, npair * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_boff, boff.data(), (npair + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   SG_HIP(hipMemcpyAsync(m_obeg, out_beg, npair * 8, hipMemcpyHostToDevice, ctx->stream));
-  if (small) {
+  if (asmall) {
+    SmallArgs sm{op, da, db, m_abeg, m_alen, m_bbeg, m_blen, m_obeg, m_olen, dout};
+    ScopedTimer tm(ctx, "merge_small");
+    hipLaunchKernelGGL(k_diff_small, dim3((uint32_t)npair), dim3(kMT), 0, ctx->stream, sm);
+  } else if (small) {
     SmallArgs sm{op, da, db, m_abeg, m_alen, m_bbeg, m_blen, m_obeg, m_olen, dout};
     {
       ScopedTimer tm(ctx, "merge_small");

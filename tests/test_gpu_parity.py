@@ -128,7 +128,8 @@ def test_merge_batch_small_side_multisets(C):
     """The one-small-side merge (sg_merge.hip k_merge_small): pairs whose
     small list fits in LDS against large lists with long runs of one value
     (across its 4096-element tiles), sentinels on both sides, either side
-    small, and a mix with a pair too large for it (generic path)."""
+    small, and a mix with a pair too large for it (generic path); then
+    Difference / Intersection with every first list small (k_diff_small)."""
     rng = np.random.default_rng(115)
     lists = []
     for it in range(24):
@@ -145,15 +146,17 @@ def test_merge_batch_small_side_multisets(C):
         if it % 4 == 1:
             large = np.sort(np.concatenate([large, np.full(3, SENT, np.uint32)]))
         lists.append((small, large) if it % 2 else (large, small))
-    for op in range(4):
-        a = np.concatenate([x for x, _ in lists])
-        b = np.concatenate([y for _, y in lists])
-        al = np.array([x.size for x, _ in lists], np.uint64)
-        bl = np.array([y.size for _, y in lists], np.uint64)
+    # and every first list small (Difference / Intersection: k_diff_small)
+    firsts = [(x, y) if x.size <= y.size else (y, x) for x, y in lists]
+    for op, pairs in [(op, lists) for op in range(4)] + [(0, firsts), (3, firsts)]:
+        a = np.concatenate([x for x, _ in pairs])
+        b = np.concatenate([y for _, y in pairs])
+        al = np.array([x.size for x, _ in pairs], np.uint64)
+        bl = np.array([y.size for _, y in pairs], np.uint64)
         ab = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.uint64)
         bb = np.concatenate([[0], np.cumsum(bl)[:-1]]).astype(np.uint64)
         outs = C.merge_batch(op, a, ab, al, b, bb, bl)
-        for k, (x, y) in enumerate(lists):
+        for k, (x, y) in enumerate(pairs):
             assert np.array_equal(outs[k], O.foreach(op, x, y)), (op, k, x.size, y.size)
 
 
