@@ -228,7 +228,8 @@ def row_f2(ctx, rng):
         pv, po = C.union_fold(sv, so, gs, ng, ctx=ctx)
         parity = bool(np.array_equal(pv, ev) and np.array_equal(po, eo))
         gsz = np.bincount(grp, weights=np.diff(off).astype(np.float64), minlength=ng) if grp is not None else [vals.size]
-        res[name] = {"inputs": n, "groups": ng, "groups_over_16384": int(np.sum(np.asarray(gsz) > 16384)),
+        res[name] = {"inputs": n, "groups": ng,
+                     "groups_past_lds_fold": int(np.sum(np.asarray(gsz) > 32768)),  # (sg_fold.hip kFgCap: key sort)
                      "elements_in": int(vals.size), "elements_out": int(fv.size),
                      "device_ms": dev, "wall_ms_host_api": wall * 1e3, "kernels_ms": kt,
                      "device_GBs_algo": algo / (dev / 1e3) / 1e9 if dev else None,
