@@ -493,9 +493,10 @@ class PrefixTriage:
         """Bytes per rank that the last finished batch's exchange takes in each
         form, whichever it used: dense (the bitmaps: fixed) and sparse (the
         candidate lists, from every rank's count of distinct signals outside
-        maxSignal, gathered with the batch; the caller has synchronised).  None
-        when the batch ran without the counts (one rank without collectives,
-        or a form that does not count)."""
+        maxSignal, gathered with the batch; the caller has synchronised, and
+        calls before the batch after next starts: the two slots alternate).
+        None when the batch ran without the counts (one rank without
+        collectives, or a form that does not count)."""
         last, G = self.last, self.comm.world
         if "slot" not in last or last.get("form") == "default":
             return None
