@@ -339,25 +339,60 @@ __global__ void k_dec_values(const uint32_t* __restrict__ delta, const uint64_t*
   }
 }
 
-// Pass 2 (one wave per list, four per workgroup): the list's bytes in steps
-// of 64 x 16, each lane an aligned 16-B load (steps start at the list's first
-// byte rounded down to 16; bytes before the list stop a run's walk back,
-// bytes after it are never terminators), the 5 bytes before a lane's 16 from
-// the lane before (DPP) or the step before (lane 63, carried).  Each
-// terminator decodes its run backwards (LEB128: the earlier byte holds the
-// lower bits), the lanes' value counts and 64-bit delta sums are scanned
-// across the wave, each value goes to LDS at its place in the step as the
-// running sum, and the step's values leave as consecutive dwords at the
-// list's value offset (pass 1).  Checks (binary.Uvarint, then the running
-// sum): a run of <= 5 bytes fitting 32 bits, the list ending on a terminator,
-// every sum within 32 bits.  The input buffer is padded to 16 bytes.
-constexpr int kDecB = 16, kDecPre = 5;
+// Per-list decode, pass 1 (one wave per list, four per workgroup): the list's
+// terminators, counted over 16-B loads (bytes outside the list masked off);
+// a scan of the n counts gives the lists' value offsets.
+__global__ __launch_bounds__(256) void k_dec_list_cnt(const uint8_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ in_off, uint64_t n,
+                                                      uint32_t* __restrict__ lcnt) {
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = in_off[k], b1 = in_off[k + 1];
+  uint32_t c = 0;
+  for (uint64_t cb = b0 & ~15ull; cb < b1; cb += 64 * 16) {
+    const uint64_t base = cb + (uint64_t)lane * 16;
+    if (base >= b1) continue;
+    const uint4 q = *reinterpret_cast<const uint4*>(in + base);
+    const int64_t lo = (int64_t)b0 - (int64_t)base, hi = (int64_t)b1 - (int64_t)base;  // bytes [lo, hi) are the list's
+    const uint32_t m = (hi >= 16 ? 0xFFFFu : (1u << hi) - 1u) & ~(lo <= 0 ? 0u : (1u << lo) - 1u);
+    const uint32_t x[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t bm = m >> (4 * d);
+      const uint32_t e = ((bm & 1u) << 7) | ((bm & 2u) << 14) | ((bm & 4u) << 21) | ((bm & 8u) << 28);
+      c += __popc(~x[d] & e);
+    }
+  }
+  c = __builtin_amdgcn_readlane(sgd::wave_incl_add(c), 63);
+  if (lane == 0) lcnt[k] = c;
+}
+
+// Pass 2 (one wave per list, four per workgroup): the list's bytes in steps of
+// kDecRows rows of 256 bytes, lane L holding the row's dword at 4 L (one
+// coalesced load per row, all of a step's rows in flight; steps start at the
+// list's first byte rounded down to 4).  The 5 bytes before a lane's 4 come
+// from the two lanes before (DPP wave shifts; lanes 0 and 1 from the row
+// before, carried).  Each terminator decodes its run backwards (LEB128: the
+// earlier byte holds the lower bits); the lanes' value counts and delta sums
+// are scanned across the wave (32-bit DPP scans), so byte order = (row, lane)
+// order = value order, and each value is stored straight to its slot: the
+// stores of a row land in one contiguous run, and nothing is staged in LDS.
+// Checks (binary.Uvarint, then the running sum): a run of <= 5 bytes fitting
+// 32 bits, the list ending on a terminator, every sum within 32 bits (the sum
+// is kept mod 2^32; a value whose add wraps it is the first past 2^32 - 1).
+// The input buffer is padded to 16 bytes.
+constexpr int kDecRows = 8;
+
+// bits 7, 15, 23, 31 of x to bits 0-3 (one multiply: the four terms land on
+// distinct bit positions, so nothing carries)
+__device__ __forceinline__ int clamp9(int64_t x) { return x < 0 ? 0 : x > 9 ? 9 : (int)x; }
+
+__device__ __forceinline__ uint32_t gather_hi(uint32_t x) { return (((x >> 7) & 0x01010101u) * 0x204081u >> 21) & 0xFu; }
 __global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                    const uint64_t* __restrict__ voff, uint64_t n, uint64_t cap,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
-  __shared__ uint32_t stage[4][64 * kDecB];  // a step's values (at most one per byte)
-  const uint32_t w = threadIdx.x >> 6;
-  const uint64_t k = (uint64_t)blockIdx.x * 4 + w;
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= n) return;  // (a wave leaves whole)
   if (voff[n] > cap) {  // the values would not fit: the host reports it, nothing is written
     if (k == 0 && (threadIdx.x & 63) == 0) atomicOr(err, 2u);
@@ -365,82 +400,74 @@ __global__ __launch_bounds__(256) void k_dec_lists(const uint8_t* __restrict__ i
   }
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t b0 = in_off[k], b1 = in_off[k + 1];
-  uint64_t vi = voff[k], run = 0;
-  bool bad = false;
-  uint32_t cz = 0, cw = 0;  // the step before's lane 63: dwords 2 and 3 of its 16 bytes
-  uint32_t* st = stage[w];
-  for (uint64_t cb = b0 & ~15ull; cb < b1; cb += 64 * kDecB) {
-    const uint64_t base = cb + (uint64_t)lane * kDecB;
-    uint4 q = make_uint4(0, 0, 0, 0);
-    if (base < b1) q = *reinterpret_cast<const uint4*>(in + base);
-    const uint32_t pz = (uint32_t)__builtin_amdgcn_update_dpp((int)cz, (int)q.z, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
-    const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp((int)cw, (int)q.w, 0x138, 0xF, 0xF, false);
-    cz = __builtin_amdgcn_readlane(q.z, 63);
-    cw = __builtin_amdgcn_readlane(q.w, 63);
-    uint32_t c[kDecPre + kDecB];
-    c[0] = pz >> 24;  // byte base - 5
+  uint32_t* o = out + voff[k];
+  uint32_t run = 0, p63 = 0, p62 = 0;  // the running sum; the row before's dwords of lanes 63 and 62
+  uint32_t badv = 0;
+  for (uint64_t cb = b0 & ~3ull; cb < b1; cb += 256 * kDecRows) {
+    uint32_t q[kDecRows];
 #pragma unroll
-    for (int j = 0; j < 4; j++) c[1 + j] = (pw >> (8 * j)) & 0xFFu;
-    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int j = 0; j < kDecB; j++) c[kDecPre + j] = (qw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-#pragma unroll
-    for (int j = 0; j < kDecPre + kDecB; j++) {
-      const uint64_t pj = base + j;  // position + kDecPre
-      // before the list: a stop for the walk back; past it: never a terminator
-      c[j] = pj < b0 + kDecPre ? 0u : (pj >= b1 + kDecPre ? 0x80u : c[j]);
+    for (int r = 0; r < kDecRows; r++) {
+      const uint64_t base = cb + 256 * r + 4 * lane;
+      q[r] = base < b1 ? *reinterpret_cast<const uint32_t*>(in + base) : 0x80808080u;  // past: never terminators
     }
-    uint32_t tmask = 0;  // terminators inside the list (past it: 0x80 above; before it: excluded here)
 #pragma unroll
-    for (int i = 0; i < kDecB; i++)
-      if (base + i >= b0 && !(c[kDecPre + i] & 0x80u)) tmask |= 1u << i;
-    uint32_t d[kDecB];
-    uint64_t t = 0;
+    for (int r = 0; r < kDecRows; r++) {
+      if (cb + 256 * r >= b1) break;  // (uniform)
+      const int64_t base = (int64_t)(cb + 256 * r + 4 * lane);
+      const uint32_t s1 = (uint32_t)__builtin_amdgcn_update_dpp((int)p63, (int)q[r], 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+      const uint32_t s2 = (uint32_t)__builtin_amdgcn_update_dpp((int)p62, (int)s1, 0x138, 0xF, 0xF, false);
+      p63 = __builtin_amdgcn_readlane(q[r], 63);
+      p62 = __builtin_amdgcn_readlane(q[r], 62);
+      // the 9 bytes base - 5 .. base + 3 as bit masks (bit i = byte base - 5 + i):
+      // cm = continuation bytes (high bit set); bytes before the list count as
+      // value ends (they stop a walk back), bytes past it as continuations
+      const int lo = clamp9((int64_t)b0 - base + 5), hi = clamp9((int64_t)b1 - base + 5);
+      const uint32_t before = (1u << lo) - 1u, past = 0x1FFu & ~((1u << hi) - 1u);
+      const uint32_t cm = (((s2 >> 31) | (gather_hi(s1) << 1) | (gather_hi(q[r]) << 5)) & ~before) | past;
+      const uint32_t tm = (~cm >> 5) & (~before >> 5) & 0xFu;  // terminators in the lane's 4 bytes
+      uint32_t c7[9];  // low 7 bits of each byte
+      c7[0] = (s2 >> 24) & 0x7Fu;
 #pragma unroll
-    for (int i = 0; i < kDecB; i++) {
-      d[i] = 0;
-      if ((tmask >> i) & 1u) {
-        const int j = kDecPre + i;
-        uint64_t v = c[j] & 0x7Fu;
-        bool open = true;
-#pragma unroll
-        for (int qq = 1; qq <= kDecPre; qq++) {
-          const uint32_t cc = c[j - qq];
-          if (open && (cc & 0x80u)) {
-            if (qq == kDecPre) bad = true;  // a sixth byte: more than binary.Uvarint's 32-bit range here
-            v = (v << 7) | (cc & 0x7Fu);
-          } else {
-            open = false;
-          }
-        }
-        bad |= v > 0xFFFFFFFFull;
-        d[i] = (uint32_t)v;
-        t += v;
+      for (int j = 0; j < 4; j++) {
+        c7[1 + j] = __builtin_amdgcn_ubfe(s1, 8 * j, 7);
+        c7[5 + j] = __builtin_amdgcn_ubfe(q[r], 8 * j, 7);
       }
-    }
-    const uint32_t cnt = __popc(tmask), ex = sgd::wave_incl_add(cnt) - cnt;
-    uint64_t sc = t;  // inclusive scan of the lanes' delta sums
+      uint32_t d[4], t = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(sc, o);
-      if (lane >= (uint32_t)o) sc += y;
-    }
-    uint64_t acc = run + (sc - t);
-    uint32_t idx = ex;
+      for (int j = 0; j < 4; j++) {
+        // a value ends at byte P = 5 + j: its run is the L continuation bytes
+        // before P (LEB128: the earlier byte holds the lower bits)
+        constexpr uint32_t one = 1;
+        const int P = 5 + j;
+        const uint32_t stops = ~cm & ((one << P) - 1u);
+        const int L = P - 1 - (stops ? 31 - __builtin_clz(stops) : -1);
+        uint32_t v = c7[P];
 #pragma unroll
-    for (int i = 0; i < kDecB; i++)
-      if ((tmask >> i) & 1u) {
-        acc += d[i];
-        bad |= acc > 0xFFFFFFFFull;
-        st[idx++] = (uint32_t)acc;
+        for (int k = 1; k <= 4; k++) v = k <= L ? (v << 7) | c7[P - k] : v;
+        // a sixth byte, or a fifth whose last byte has bits past 32: over
+        // binary.Uvarint's 32-bit range here
+        const uint32_t is_t = (tm >> j) & 1u;
+        badv |= is_t & ((uint32_t)(L >= 5) | ((uint32_t)(L == 4) & (uint32_t)((c7[P] & 0x70u) != 0)));
+        d[j] = is_t ? v : 0u;
+        t += d[j];
       }
-    const uint32_t tot = __builtin_amdgcn_readlane(ex + cnt, 63);
-    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
-    for (uint32_t e = lane; e < tot; e += 64) out[vi + e] = st[e];
-    __builtin_amdgcn_wave_barrier();
-    run += __shfl(sc, 63);
-    vi += tot;
+      const uint32_t cnt = __popc(tm), ic = sgd::wave_incl_add(cnt), it = sgd::wave_incl_add(t);
+      // (d = 0 off the terminators: the sum only moves at values; an add
+      // that wraps it is the first value past 2^32 - 1)
+      uint32_t acc = run + (it - t);
+      const uint32_t ex = ic - cnt;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t a = acc + d[j];
+        badv |= (uint32_t)(a < acc);
+        acc = a;
+        if ((tm >> j) & 1u) o[ex + __popc(tm & ((1u << j) - 1u))] = a;
+      }
+      o += __builtin_amdgcn_readlane(ic, 63);
+      run += __builtin_amdgcn_readlane(it, 63);
+    }
   }
+  bool bad = badv != 0;
   if (lane == 0 && b1 > b0 && (in[b1 - 1] & 0x80u)) bad = true;  // the list ends inside a value
   if (__any(bad) && lane == 0) atomicOr(err, 1u);
 }
@@ -548,14 +575,14 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
                uint64_t cap, uint64_t* h_off, uint64_t* d_voff) {
   const uint64_t nblk = (nb + 31) / 32;
   WsPlan p;
-  const size_t o_tm = p.add(nblk * 4 + 4), o_tc = p.add(nblk * 4 + 4), o_vb = p.add((nblk + 1) * 8),
+  const size_t o_tm = p.add(nblk * 4 + 4), o_tc = p.add(std::max(nblk, n) * 4 + 4), o_vb = p.add((nblk + 1) * 8),
                o_d = p.add(nb * 4 + 4), o_x = p.add((nb + 1) * 8), o_err = p.add(8), o_hd = p.add(nblk * 4 + 4),
                o_kwv = p.add(nblk * 8);
   const size_t scan_off = p.total;
-  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(nb));
+  int rc = ws_reserve(ctx, p.total + scan_ws_bytes(std::max(nb, n)));
   if (rc) return rc;
   uint32_t* tmask = (uint32_t*)ws_at(ctx, o_tm);
-  uint32_t* tcnt = (uint32_t*)ws_at(ctx, o_tc);
+  uint32_t* tcnt = (uint32_t*)ws_at(ctx, o_tc);  // per block, or per list (the per-list form)
   uint64_t* vbase = (uint64_t*)ws_at(ctx, o_vb);
   uint32_t* delta = (uint32_t*)ws_at(ctx, o_d);
   uint64_t* excl = (uint64_t*)ws_at(ctx, o_x);
@@ -564,19 +591,25 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   uint64_t* kwv = (uint64_t*)ws_at(ctx, o_kwv);  // N <= nb
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   ScopedTimer tm(ctx, "rpc_decode");
-  if (nb) hipLaunchKernelGGL(k_dec_count, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, nb, tmask, tcnt);
-  rc = scan_counts(ctx, tcnt, vbase, nblk, scan_off);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_list_vpos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vbase, tmask,
-                     d_voff);
-  SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  const bool lists = nb && !dec_blocks(n, nb);
+  // (a list's value count is a u32: the per-list form when nb cannot overflow it)
+  const bool lists = nb && nb < (1ull << 32) && !dec_blocks(n, nb);
   if (lists) {
-    // no host wait between the passes: the kernel checks the capacity itself
-    // (error bit 2: nothing written)
+    // the lists' value counts, their scan; no host wait between the passes:
+    // the decode checks the capacity itself (error bit 2: nothing written)
+    hipLaunchKernelGGL(k_dec_list_cnt, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_in, d_in_off, n,
+                       tcnt);
+    rc = scan_counts(ctx, tcnt, d_voff, n, scan_off);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_dec_lists, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_in, d_in_off,
                        (const uint64_t*)d_voff, n, cap, d_vals, err);
+    SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   } else {
+    if (nb) hipLaunchKernelGGL(k_dec_count, dim3(grid_for(nblk)), dim3(256), 0, ctx->stream, d_in, nb, tmask, tcnt);
+    rc = scan_counts(ctx, tcnt, vbase, nblk, scan_off);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_list_vpos, dim3(div_up(n + 1, 256)), dim3(256), 0, ctx->stream, d_in_off, n, vbase, tmask,
+                       d_voff);
+    SG_HIP(hipMemcpyAsync(h_off, d_voff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
     const uint64_t N = h_off[n];
     if (N > cap) {

@@ -211,3 +211,35 @@ def test_delta_decode_corrupted_payloads_vs_oracle(ctx, monkeypatch, blocks):
             continue
         gv, go = C.delta_decode(data, doff, ctx=ctx)
         assert [gv[int(go[k]):int(go[k + 1])].tolist() for k in range(len(parts))] == expect, t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocks", ["0", "1"])
+def test_delta_decode_sum_past_32_bits(ctx, monkeypatch, blocks):
+    """A running sum that passes 2^32 - 1 at a chosen value, deep in a long
+    list (across the decoder's lanes, rows and steps): rejected exactly when
+    binary.Uvarint + the sum would overflow the uint32 (oracle), accepted when
+    it ends at 0xFFFFFFFF."""
+    from syzkaller_amd import cover as C
+    from syzkaller_amd._lib import SyzSigError
+
+    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
+    step = (1 << 24) + 1
+    for m, last in ((300, None), (255, None), (256, None), (257, None), (1000, None), (255, 0xFFFFFFFF)):
+        d = [step] * m
+        if last is not None:
+            d[-1] = last - step * (m - 1)
+        payload = b"".join(O.put_uvarint(x) for x in d)
+        lead = O.delta_encode(np.arange(0, 700, 3, dtype=np.uint32))
+        data = lead + payload
+        doff = np.array([0, len(lead), len(data)], np.uint64)
+        try:
+            expect = [O.delta_decode(lead), O.delta_decode(payload)]
+        except ValueError:
+            expect = None
+        if expect is None:
+            with pytest.raises(SyzSigError):
+                C.delta_decode(data, doff, ctx=ctx)
+            continue
+        gv, go = C.delta_decode(data, doff, ctx=ctx)
+        assert [gv[int(go[k]):int(go[k + 1])].tolist() for k in range(2)] == expect, m
