@@ -120,34 +120,38 @@ __global__ __launch_bounds__(256) void k_enc_write(const uint32_t* __restrict__ 
   }
 }
 
-// Encode, one wave per list (four per workgroup): the list in steps of 256
-// values, four consecutive per lane (an aligned 16-B load; steps start at the
-// list's first value rounded down to 4), each value's delta against the one
-// before it (the lane before's last by DPP; lane 0: the step before's lane
-// 63) and its varint length.  Pass A: the list's byte count (and the
-// sortedness check); pass B, after a scan of the counts: the step's bytes
-// into LDS at a wave prefix of the lanes' lengths, then stored as one run of
-// consecutive bytes at the list's start + the bytes before.  No per-value
-// list search (the per-element form looks its list up for every value).  The
-// value buffer is padded to 16 bytes.
-__device__ __forceinline__ void enc_step(const uint32_t* __restrict__ v, uint64_t cb, uint64_t e0, uint64_t e1,
-                                         uint32_t lane, uint32_t& carry, uint32_t (&d)[4], uint32_t (&len)[4],
-                                         bool& bad) {
-  const uint64_t i0 = cb + 4ull * lane;
-  uint4 q = make_uint4(0, 0, 0, 0);
-  if (i0 < e1) q = *reinterpret_cast<const uint4*>(v + i0);
-  const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)q.w, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
-  carry = __builtin_amdgcn_readlane(q.w, 63);
-  const uint32_t x[4] = {q.x, q.y, q.z, q.w};
+// Encode, one wave per list (four per workgroup): the list in steps of
+// kEncRows rows of 64 values, lane L holding value 64 r + L of the step (one
+// coalesced dword load per row, all of a step's rows in flight), each value's
+// delta against the one before it (the lane before's by DPP; lane 0: the row
+// before's lane 63, carried) and its varint length.  Pass A: the list's byte
+// count (and the sortedness check); pass B, after a scan of the counts: a
+// wave prefix of the row's lengths places each value's bytes, stored straight
+// to the payload (store k writes byte k of every value that long: a row's
+// stores cover one contiguous run).  No per-value list search.
+constexpr int kEncRows = 8;
+struct EncRow {
+  uint32_t d, len;
+};
+
+__device__ __forceinline__ void enc_rows(const uint32_t* __restrict__ v, uint64_t cb, uint64_t e0, uint64_t e1,
+                                         uint32_t lane, uint32_t& carry, EncRow (&row)[kEncRows], uint32_t& bad) {
+  uint32_t x[kEncRows];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint64_t i = i0 + j;
-    const uint32_t prev = j ? x[j - 1] : pw;
-    const bool ok = i >= e0 && i < e1, first = i == e0;
-    bad |= ok && !first && x[j] < prev;
-    const uint32_t dd = first ? x[j] : x[j] - prev;
-    d[j] = ok ? dd : 0u;
-    len[j] = ok ? varint_len(dd) : 0u;
+  for (int r = 0; r < kEncRows; r++) {
+    const uint64_t i = cb + 64 * r + lane;
+    x[r] = i < e1 ? v[i] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kEncRows; r++) {
+    const uint64_t i = cb + 64 * r + lane;
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x[r], 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+    carry = __builtin_amdgcn_readlane(x[r], 63);
+    const bool ok = i < e1, first = i == e0;
+    bad |= (uint32_t)(ok && !first && x[r] < prev);
+    const uint32_t dd = first ? x[r] : x[r] - prev;
+    row[r].d = ok ? dd : 0u;
+    row[r].len = ok ? varint_len(dd) : 0u;
   }
 }
 
@@ -158,52 +162,43 @@ __global__ __launch_bounds__(256) void k_enc_list_len(const uint32_t* __restrict
   if (k >= n) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t e0 = off[k], e1 = off[k + 1];
-  uint32_t carry = 0, tot = 0;
-  bool bad = false;
-  for (uint64_t cb = e0 & ~3ull; cb < e1; cb += 256) {
-    uint32_t d[4], len[4];
-    enc_step(v, cb, e0, e1, lane, carry, d, len, bad);
-    tot += __builtin_amdgcn_readlane(sgd::wave_incl_add(len[0] + len[1] + len[2] + len[3]), 63);
+  uint32_t carry = 0, tot = 0, bad = 0;
+  for (uint64_t cb = e0; cb < e1; cb += 64 * kEncRows) {
+    EncRow row[kEncRows];
+    enc_rows(v, cb, e0, e1, lane, carry, row, bad);
+#pragma unroll
+    for (int r = 0; r < kEncRows; r++) tot += row[r].len;
   }
+  tot = __builtin_amdgcn_readlane(sgd::wave_incl_add(tot), 63);
   if (lane == 0) lbytes[k] = tot;
-  if (__any(bad) && lane == 0) atomicOr(err, 1u);
+  if (__any(bad != 0) && lane == 0) atomicOr(err, 1u);
 }
 
 __global__ __launch_bounds__(256) void k_enc_list_write(const uint32_t* __restrict__ v, const uint64_t* __restrict__ off,
                                                         uint64_t n, const uint64_t* __restrict__ boff,
                                                         uint8_t* __restrict__ out) {
-  __shared__ uint8_t stage[4][256 * 5];  // a step's bytes
-  const uint32_t w = threadIdx.x >> 6;
-  const uint64_t k = (uint64_t)blockIdx.x * 4 + w;
+  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= n) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t e0 = off[k], e1 = off[k + 1];
-  uint64_t pos = boff[k];
-  uint32_t carry = 0;
-  bool bad = false;  // (checked by pass A)
-  uint8_t* sb = stage[w];
-  for (uint64_t cb = e0 & ~3ull; cb < e1; cb += 256) {
-    uint32_t d[4], len[4];
-    enc_step(v, cb, e0, e1, lane, carry, d, len, bad);
-    const uint32_t L = len[0] + len[1] + len[2] + len[3];
-    const uint32_t incl = sgd::wave_incl_add(L);
-    uint32_t o = incl - L;
+  uint8_t* o = out + boff[k];
+  uint32_t carry = 0, bad = 0;  // (checked by pass A)
+  for (uint64_t cb = e0; cb < e1; cb += 64 * kEncRows) {
+    EncRow row[kEncRows];
+    enc_rows(v, cb, e0, e1, lane, carry, row, bad);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      uint32_t x = d[j];
+    for (int r = 0; r < kEncRows; r++) {
+      const uint32_t len = row[r].len, incl = sgd::wave_incl_add(len);
+      uint8_t* p = o + (incl - len);
+      uint32_t x = row[r].d;
 #pragma unroll
       for (int b = 0; b < 5; b++)  // binary.PutUvarint
-        if ((uint32_t)b < len[j]) {
-          sb[o + b] = (uint8_t)((uint32_t)b + 1 < len[j] ? (x | 0x80u) : x);
+        if ((uint32_t)b < len) {
+          p[b] = (uint8_t)((uint32_t)b + 1 < len ? (x | 0x80u) : x);
           x >>= 7;
         }
-      o += len[j];
+      o += __builtin_amdgcn_readlane(incl, 63);
     }
-    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
-    for (uint32_t e = lane; e < T; e += 64) out[pos + e] = sb[e];
-    __builtin_amdgcn_wave_barrier();
-    pos += T;
   }
 }
 

@@ -1,6 +1,7 @@
 """Randomised batches through the ordered outputs (sg_triage.hip
-owned_outputs): sg_triage_batch with the diff CSR and sg_merge_poll against
-the oracle's sequential loops (fuzzer.go:645-693, manager.go:949-956), over
+owned_outputs): sg_triage_batch with the diff CSR, sg_merge_poll and
+sg_accept_batch against the oracle's sequential loops (fuzzer.go:645-693,
+manager.go:907-912, 949-956), over
 seeds that put record counts across the 2^16-record group boundaries, records
 past the sweep's chunk and set caps, empty records, repeats, the sentinel and
 maxSignal overlap from none to most."""
@@ -54,5 +55,16 @@ def test_ordered_outputs_random_batches(C, seed):
     pv, po = C.merge_poll(mp, vals, off)
     qv, qo = O.merge_poll(O.OSet(m0), vals, off)
     assert np.array_equal(po, qo) and np.array_equal(pv, qv)
-    for s in (ms, ns, mp):
+    # NewInput over the same batch as RPCs (manager.go:907-912), with cover
+    cl = rng.integers(0, 8, size=off.size - 1)
+    co = np.concatenate([[0], np.cumsum(cl)]).astype(np.uint64)
+    cv = rng.integers(0, 1 << 30, size=int(co[-1]), dtype=np.uint64).astype(np.uint32)
+    cs, cc = C.SignalSet(), C.SignalSet()
+    C.SignalAdd(cs, m0)
+    os_, oc = O.OSet(m0), O.OSet()
+    acc = C.accept_batch(cs, cc, vals, off, cv, co)
+    assert np.array_equal(acc, O.accept_batch(os_, oc, vals, off, cv, co))
+    for a, b in ((cs, os_), (cc, oc)):
+        assert np.array_equal(np.sort(a.export()), np.sort(b.export()))
+    for s in (ms, ns, mp, cs, cc):
         s.close()
