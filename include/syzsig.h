@@ -70,10 +70,34 @@ int sg_ctx_timing(sg_ctx* ctx, int enable);
 int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* launches);
 /* Context counters: "owner_resets" (Minimize's first-owner table generations
  * started after the key space ran out), "owner_floor", "owner_key_space",
- * "max_launch_records".  The environment switches SG_OWNER_KEY_SPACE and
- * SG_TRIAGE_MAX_RECS (test knobs that lower the key space / the records per
- * partitioned launch) are read once, by sg_ctx_create. */
+ * "max_launch_records"; the host ingest's last call (sg_triage_batch /
+ * sg_triage_traces without diff lists): "host_copy_bytes", "host_copy_ns"
+ * (pageable -> pinned copies), "host_wait_ns" (waits for a staging slot's DMA),
+ * "host_copy_threads"; "cpu_quota_milli" (the CPUs this process may use,
+ * x1000). */
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
+/* Context options.  Every path is selected by its regime; an option only
+ * forces one, for a test or a measurement, and no call reads the environment
+ * (sg_ctx_create seeds "debug_part", "bucket_blocks" and "prefix_pairs" from
+ * SG_DEBUG_PART / SG_BUCKET_BLOCKS / SG_PREFIX_PAIRS, for the GPU scripts).
+ * Keys (-1 = the regime's choice where it applies):
+ *   "max_launch_records"   records per partitioned launch (0: 2^24)
+ *   "owner_key_space"      Minimize's first-owner key space (0: 2^32 - 1; set
+ *                          before the first Minimize)
+ *   "debug_part"           phase counters of the partitioned path (stderr)
+ *   "bucket_blocks"        cap of the persistent bucket grid (0: none)
+ *   "prefix_pairs"         sg_prefix_begin_dev's form (0 kept partitions, 1 pairs)
+ *   "fold_map"             sg_union_fold's one-group byte map (-1 by range, 0 never)
+ *   "minimize_filter"      Minimize's value filter (1 on, 0 off)
+ *   "minimize_filter_ranks" Minimize's phase-A inputs (0: the default 4)
+ *   "report_direct"        sg_cover_uncovered's global-search form at any size (1)
+ *   "rpc_encode_elems"     delta encode form (-1 by shape, 0 per list, 1 per element)
+ *   "rpc_decode_blocks"    delta decode form (-1 by shape, 0 per list, 1 per block)
+ *   "host_slice"           host ingest: entries per record slice (0: 64 Mi)
+ *   "host_copy_threads"    host ingest: copy threads (0: half the CPU quota, 2..16)
+ * Unknown keys and out-of-range values return SG_EINVAL. */
+int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value);
+int sg_ctx_get_option(sg_ctx* ctx, const char* key, int64_t* out);
 /* Profiling aid: a one-thread kernel (k_mark_begin, or k_mark_end when end !=
  * 0) on the context's stream, so a kernel trace can cut out a region. */
 int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag);

@@ -41,6 +41,8 @@ SIGNATURES = {
     "sg_ctx_timing": (c_int, [c_void_p, c_int]),
     "sg_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), P64]),
     "sg_ctx_counter": (c_int, [c_void_p, c_char_p, P64]),
+    "sg_ctx_set_option": (c_int, [c_void_p, c_char_p, c_int64]),
+    "sg_ctx_get_option": (c_int, [c_void_p, c_char_p, POINTER(c_int64)]),
     "sg_ctx_marker": (c_int, [c_void_p, c_int, c_uint32]),
     "sg_set_create": (c_int, [c_void_p, POINTER(c_void_p)]),
     "sg_set_destroy": (None, [c_void_p]),

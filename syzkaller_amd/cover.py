@@ -11,7 +11,7 @@ Empty results are returned as empty arrays (Go returns nil; callers only use
 len, and cover_test.go:54 treats two empty results as equal).
 """
 import ctypes
-from ctypes import byref, c_double, c_int, c_size_t, c_uint64, c_void_p
+from ctypes import byref, c_double, c_int, c_int64, c_size_t, c_uint64, c_void_p
 
 import numpy as np
 
@@ -76,9 +76,20 @@ class Context:
         call("sg_ctx_timing", self.h, 1 if enable else 0)
 
     def counter(self, name):
-        """sg_ctx_counter: "owner_resets", "owner_floor", "owner_key_space", "max_launch_records"."""
+        """sg_ctx_counter: "owner_resets", "owner_floor", "owner_key_space", "max_launch_records",
+        the host ingest's "host_copy_bytes" / "host_copy_ns" / "host_wait_ns" / "host_copy_threads",
+        "cpu_quota_milli"."""
         v = c_uint64()
         call("sg_ctx_counter", self.h, name.encode(), byref(v))
+        return v.value
+
+    def set_option(self, key, value):
+        """sg_ctx_set_option: force a path for a test or a measurement (include/syzsig.h lists the keys)."""
+        call("sg_ctx_set_option", self.h, key.encode(), int(value))
+
+    def get_option(self, key):
+        v = c_int64()
+        call("sg_ctx_get_option", self.h, key.encode(), byref(v))
         return v.value
 
     def kernel_time(self, name):

@@ -2104,13 +2104,10 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
     ba.goff = emit->goff;
   }
   uint32_t bgrid = persistent_grid(ctx, (const void*)k_bucket<false, 0>, kBThreads);
-  // diagnostics: SG_BUCKET_BLOCKS caps the persistent grid (leaves CUs to
-  // kernels on other streams)
-  static const uint32_t cap_blocks = [] {
-    const char* e = getenv("SG_BUCKET_BLOCKS");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  if (cap_blocks && cap_blocks < bgrid) bgrid = cap_blocks;
+  // diagnostics: option bucket_blocks caps the persistent grid (leaves CUs
+  // to kernels on other streams)
+  const int64_t cap_blocks = ctx->opt[kOptBucketBlocks];
+  if (cap_blocks > 0 && (uint64_t)cap_blocks < bgrid) bgrid = (uint32_t)cap_blocks;
   uint64_t* ddbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&ddbg, (size_t)bgrid * 88));
@@ -2507,7 +2504,7 @@ int bucket_triage(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
 // against M = maxsig | prefix for any M containing base: every s of the batch
 // outside M is outside base, so its pair is kept, and its first owner is the
 // loop's (a record is queued iff it is the first to hold some s outside M).
-// That is the form SG_PREFIX_PAIRS=1 selects.  The default keeps the
+// That is the form option prefix_pairs 1 selects.  The default keeps the
 // partitions instead: begin marks the buckets (k_bucket_mark, the base slice
 // in LDS), end runs the bucket stage against maxsig | prefix.  On a fresh C3
 // slice (1.76G entries, 361M pairs) the pairs' flag pass (3.9 ms: two random
@@ -2614,11 +2611,6 @@ __global__ void k_prefix_merge(const uint32_t* __restrict__ marks, uint32_t* __r
   }
 }
 
-static bool prefix_keep_mode() {  // read at each begin (tests switch it)
-  const char* e = getenv("SG_PREFIX_PAIRS");
-  return !(e && atoi(e) != 0);
-}
-
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec, int form, uint64_t* d_ncand) {
   if (slot >= kPrefixSlots) {
@@ -2632,7 +2624,7 @@ int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_
   PrefixSlot& S = ctx->prefix[slot];
   S.slices.clear();
   S.open = false;
-  S.keep = form < 0 ? prefix_keep_mode() : form != 1;
+  S.keep = form < 0 ? ctx->opt[kOptPrefixPairs] == 0 : form != 1;
   const bool mark = form != 2;  // form 2: the partitions alone (a plain triage split in two)
   if (d_ncand) SG_HIP(hipMemsetAsync(d_ncand, 0, 8, ctx->stream));
   S.marks = marks_words;

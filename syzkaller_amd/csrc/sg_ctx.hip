@@ -495,17 +495,13 @@ int sg_ctx_create(int device, sg_ctx** out) {
   }
   sg_ctx* c = new sg_ctx();
   c->device = device;
-  // environment switches, read once here (not on the hot path)
   c->max_launch_recs = kMaxLaunchRecords;
-  if (const char* e = getenv("SG_TRIAGE_MAX_RECS")) {
-    const unsigned long long v = strtoull(e, nullptr, 10);
-    if (v > 0 && v < c->max_launch_recs) c->max_launch_recs = v;
-  }
-  if (const char* e = getenv("SG_OWNER_KEY_SPACE")) {
-    const unsigned long long v = strtoull(e, nullptr, 10);
-    if (v > 0 && v < c->owner_key_space) c->owner_key_space = v;
-  }
+  // the diagnostics switches of the GPU scripts, read once here (every other
+  // option is set by sg_ctx_set_option; nothing reads the environment later)
   c->debug_part = getenv("SG_DEBUG_PART") != nullptr;
+  if (const char* e = getenv("SG_BUCKET_BLOCKS")) c->opt[kOptBucketBlocks] = strtoll(e, nullptr, 10);
+  if (const char* e = getenv("SG_PREFIX_PAIRS")) c->opt[kOptPrefixPairs] = strtoll(e, nullptr, 10) != 0;
+  c->cpu_quota = host_cpu_quota();
   int rc = ensure_device(c);
   if (rc) {
     delete c;
@@ -628,6 +624,71 @@ int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag) {
   return SG_OK;
 }
 
+static const char* const kOptNames[kOptCount] = {
+    "bucket_blocks",      "prefix_pairs",       "fold_map",         "minimize_filter",   "minimize_filter_ranks",
+    "report_direct",      "rpc_encode_elems",   "rpc_decode_blocks", "host_slice",       "host_copy_threads"};
+
+int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value) {
+  if (!ctx || !key) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!strcmp(key, "max_launch_records")) {  // records per partitioned launch (lowered for slicing tests)
+    if (value < 0 || (uint64_t)value > kMaxLaunchRecords) {
+      set_error("sg_ctx_set_option: max_launch_records in 1..%llu (0: the default)",
+                (unsigned long long)kMaxLaunchRecords);
+      return SG_EINVAL;
+    }
+    ctx->max_launch_recs = value ? (uint64_t)value : kMaxLaunchRecords;
+    return SG_OK;
+  }
+  if (!strcmp(key, "owner_key_space")) {  // Minimize's key space (lowered to reach the generation reset)
+    if (ctx->owner) {
+      set_error("sg_ctx_set_option: owner_key_space is set before the first-owner table exists");
+      return SG_EINVAL;
+    }
+    if (value < 0 || (uint64_t)value > 0xFFFFFFFFull) {
+      set_error("sg_ctx_set_option: owner_key_space in 1..2^32-1 (0: the default)");
+      return SG_EINVAL;
+    }
+    ctx->owner_key_space = value ? (uint64_t)value : 0xFFFFFFFFull;
+    return SG_OK;
+  }
+  if (!strcmp(key, "debug_part")) {
+    ctx->debug_part = value != 0;
+    return SG_OK;
+  }
+  for (int i = 0; i < kOptCount; i++)
+    if (!strcmp(key, kOptNames[i])) {
+      ctx->opt[i] = value;
+      return SG_OK;
+    }
+  set_error("sg_ctx_set_option: unknown option '%s'", key);
+  return SG_EINVAL;
+}
+
+int sg_ctx_get_option(sg_ctx* ctx, const char* key, int64_t* out) {
+  if (!ctx || !key || !out) return SG_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!strcmp(key, "max_launch_records")) {
+    *out = (int64_t)ctx->max_launch_recs;
+    return SG_OK;
+  }
+  if (!strcmp(key, "owner_key_space")) {
+    *out = (int64_t)ctx->owner_key_space;
+    return SG_OK;
+  }
+  if (!strcmp(key, "debug_part")) {
+    *out = ctx->debug_part;
+    return SG_OK;
+  }
+  for (int i = 0; i < kOptCount; i++)
+    if (!strcmp(key, kOptNames[i])) {
+      *out = ctx->opt[i];
+      return SG_OK;
+    }
+  set_error("sg_ctx_get_option: unknown option '%s'", key);
+  return SG_EINVAL;
+}
+
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
   if (!ctx || !name || !out) return SG_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
@@ -639,6 +700,16 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
     *out = ctx->owner_key_space;
   else if (!strcmp(name, "max_launch_records"))
     *out = ctx->max_launch_recs;
+  else if (!strcmp(name, "host_copy_bytes"))  // the host ingest's last call (sg_host.hip)
+    *out = ctx->host_copy_bytes;
+  else if (!strcmp(name, "host_copy_ns"))
+    *out = ctx->host_copy_ns;
+  else if (!strcmp(name, "host_wait_ns"))
+    *out = ctx->host_wait_ns;
+  else if (!strcmp(name, "host_copy_threads"))
+    *out = ctx->host_threads;
+  else if (!strcmp(name, "cpu_quota_milli"))
+    *out = (uint64_t)(ctx->cpu_quota * 1000.0 + 0.5);
   else {
     set_error("sg_ctx_counter: unknown counter '%s'", name);
     return SG_EINVAL;

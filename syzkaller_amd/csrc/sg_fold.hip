@@ -271,13 +271,16 @@ __device__ __forceinline__ uint64_t fg_peers(uint32_t d, bool live) {  // lanes 
 template <int kT, int kS>
 __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ packed, const uint64_t* __restrict__ gstart,
                                                  const uint32_t* __restrict__ glist, uint32_t* __restrict__ out,
-                                                 uint32_t* __restrict__ gcnt) {
+                                                 uint32_t* __restrict__ gcnt, const uint32_t* __restrict__ rep) {
   constexpr int kW = kT / 64;
   constexpr uint32_t kCap = kT * kS;
   __shared__ uint32_t stage[kCap];
   __shared__ uint32_t cnt[kW][256];  // per-wave digit counts, then the waves' offsets in the digit
   __shared__ uint32_t dstart[256];
   __shared__ uint32_t red[2][kW];
+  // a list repeats a value (k_fold_pack_chk, stream-ordered before): the host
+  // redoes the fold through the multiset key path, so this one does nothing
+  if (__builtin_amdgcn_readfirstlane(*rep)) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint32_t g = glist[blockIdx.x];
   const uint64_t b0 = gstart[g];
@@ -419,7 +422,8 @@ __global__ __launch_bounds__(kT) void k_fold_lds(const uint32_t* __restrict__ pa
 // dst[doff[g] ..] = src[sbeg[g] .. + len[g]) for u32 lengths, one wave per group
 __global__ void k_fold_move(const uint32_t* __restrict__ src, const uint64_t* __restrict__ sbeg,
                             const uint32_t* __restrict__ len, const uint64_t* __restrict__ doff, uint64_t n,
-                            uint32_t* __restrict__ dst) {
+                            uint32_t* __restrict__ dst, const uint32_t* __restrict__ rep) {
+  if (__builtin_amdgcn_readfirstlane(*rep)) return;  // (the LDS folds were skipped: the lengths are stale)
   const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (g >= n) return;
   const uint64_t s = sbeg[g], d = doff[g], L = len[g];
@@ -532,15 +536,15 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
       ScopedTimer tk(ctx, "fold_lds");
       if (nform[0])
         hipLaunchKernelGGL((k_fold_lds<512, kFgSteps>), dim3(nform[0]), dim3(512), 0, ctx->stream,
-                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq, folded, gcnt);
+                           (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq, folded, gcnt, (const uint32_t*)rep);
       if (nform[1] > nform[0])
         hipLaunchKernelGGL((k_fold_lds<1024, kFgSteps>), dim3(nform[1] - nform[0]), dim3(1024), 0, ctx->stream,
                            (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nform[0], folded,
-                           gcnt);
+                           gcnt, (const uint32_t*)rep);
       if (nform[2] > nform[1])
         hipLaunchKernelGGL((k_fold_lds<1024, 2 * kFgSteps>), dim3(nform[2] - nform[1]), dim3(1024), 0, ctx->stream,
                            (const uint32_t*)packed, (const uint64_t*)dgs, (const uint32_t*)dq + nform[1], folded,
-                           gcnt);
+                           gcnt, (const uint32_t*)rep);
     }
     if (nbig) {
       ScopedTimer tk(ctx, "fold_big");
@@ -575,7 +579,8 @@ static int fold_groups_lds(sg_ctx* ctx, const uint32_t* dv, const uint64_t* off,
     {
       ScopedTimer tk(ctx, "fold_move");
       hipLaunchKernelGGL(k_fold_move, dim3(div_up(ngroups, 4)), dim3(256), 0, ctx->stream, (const uint32_t*)folded,
-                         (const uint64_t*)dgs, (const uint32_t*)gcnt, (const uint64_t*)fo, (uint64_t)ngroups, packed);
+                         (const uint64_t*)dgs, (const uint32_t*)gcnt, (const uint64_t*)fo, (uint64_t)ngroups, packed,
+                         (const uint32_t*)rep);
     }
     SG_HIP(hipGetLastError());
   }
@@ -658,14 +663,13 @@ static int fold_sorted(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, s
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint32_t jb = bits_for(st[0]);
   if (gb + 32 + jb > 64) return SG_EOVERFLOW_FOLD;
-  const char* map_env = getenv("SG_FOLD_MAP");  // (SG_FOLD_MAP=0: always the sort -- a test hook)
   const uint64_t range = st[2] - st[1] + 1;     // values lie in [AND, OR]
   // the map's passes cost ~3 bytes of traffic per value of the range, the
   // sort ~48 per key: the map only for a range dense enough (a few thousand
   // PCs spread over 2^28 would memset and scan 256 MiB -- and keep it in the
   // grow-only workspace -- to fold what the sort folds in microseconds)
   const bool dense = range <= kFoldMapMax && range <= std::max<uint64_t>(1ull << 20, 16 * N);
-  if (ngroups == 1 && jb == 0 && dense && !(map_env && !atoi(map_env))) {
+  if (ngroups == 1 && jb == 0 && dense && ctx->opt[kOptFoldMap] != 0) {  // (option fold_map 0: always the sort, a test hook)
     const uint64_t nt = div_up(range, (uint64_t)kFmTile);
     WsPlan q;
     const size_t qM = q.add(nt * kFmTile), qC = q.add(nt * 4), qP = q.add((nt + 1) * 8), qO = q.add(N * 4);

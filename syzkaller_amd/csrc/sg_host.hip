@@ -10,8 +10,9 @@
 // GB/s on the MI355X box, profiles/r04_micro_h2d.txt) and leaves the GPU idle
 // meanwhile.  Here the batch goes through in record slices:
 //
-//   host    slice i's values copied by kCopyThreads threads into pinned
-//           buffer i % 2 (pageable -> pinned at 72-88 GB/s with 4 threads),
+//   host    slice i's values copied by host_copy_threads() threads into
+//           pinned buffer i % 2 (pageable -> pinned at 72-88 GB/s with 4
+//           threads on an idle box; half the cgroup CPU share by default),
 //           its record offsets rebased to the slice;
 //   copy    DMA of pinned buffer i % 2 into device buffer i % 2 on the
 //           context's copy stream (57.5 GB/s from pinned memory);
@@ -23,20 +24,48 @@
 // whether or not the batch is cut there.
 #include "sg_internal.h"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 
 namespace sg {
 
 constexpr uint64_t kHostSliceDefault = 64ull << 20;  // entries per slice (256 MB of values)
-constexpr int kCopyThreadsDefault = 4;
+constexpr int kCopyThreadsMax = 16;
 
-static uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* e = getenv(name);
-  if (!e || !*e) return dflt;
-  const unsigned long long v = strtoull(e, nullptr, 0);
-  return v ? (uint64_t)v : dflt;
+// CPUs this process may use: the cgroup v2 quota (cpu.max), else the
+// affinity mask (read once, at context creation)
+double host_cpu_quota() {
+  double q = 0;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char a[32] = {0};
+    unsigned long long per = 0;
+    if (fscanf(f, "%31s %llu", a, &per) == 2 && strcmp(a, "max") != 0 && per) q = strtod(a, nullptr) / (double)per;
+    fclose(f);
+  }
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) {
+    const double n = (double)CPU_COUNT(&cs);
+    if (q <= 0 || n < q) q = n;
+  }
+  return q > 0 ? q : 1;
+}
+
+// pageable -> pinned copy threads: the option, else half the CPU share (the
+// other half stays with the caller's own threads), 2..16
+int host_copy_threads(const sg_ctx* ctx) {
+  if (ctx->opt[kOptHostCopyThreads] > 0) return (int)std::min<int64_t>(64, ctx->opt[kOptHostCopyThreads]);
+  return std::max(2, std::min(kCopyThreadsMax, (int)(ctx->cpu_quota / 2)));
+}
+
+static uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
 
 // memcpy by up to `threads` host threads (the calling one included)
@@ -65,8 +94,8 @@ struct HostSlice {
 
 int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* vals, const uint64_t* rec_off,
                   uint64_t nrec, uint8_t* rec_new, bool trace) {
-  const uint64_t S = env_u64("SG_HOST_SLICE", kHostSliceDefault);
-  const int threads = (int)std::min<uint64_t>(64, env_u64("SG_HOST_COPY_THREADS", kCopyThreadsDefault));
+  const uint64_t S = ctx->opt[kOptHostSlice] > 0 ? (uint64_t)ctx->opt[kOptHostSlice] : kHostSliceDefault;
+  const int threads = host_copy_threads(ctx);
   // record slices of <= S entries (or one record, when it alone holds more)
   std::vector<HostSlice> sl;
   uint64_t max_n = 1, max_r = 1;
@@ -96,6 +125,8 @@ int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     SG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     for (auto& e : ctx->pipe_ev) SG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  ctx->host_copy_bytes = ctx->host_copy_ns = ctx->host_wait_ns = 0;
+  ctx->host_threads = (uint64_t)threads;
   char* pin = (char*)ctx->pin;
   char* dst = (char*)ctx->dstage;
   uint8_t* dflag = (uint8_t*)(dst + 2 * b_slot);
@@ -109,9 +140,15 @@ int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_
     char* dv = dst + k * b_slot;
     uint64_t* dof = (uint64_t*)(dv + b_vals);
     const uint64_t n = s.e1 - s.e0, nr = s.r1 - s.r0;
+    const uint64_t t0 = now_ns();
     if (i >= 2) SG_HIP(hipEventSynchronize(ev_dma[k]));  // slice i-2's DMA has read pinned k
+    const uint64_t t1 = now_ns();
     par_copy(pv, vals + s.e0, n * 4, threads);
     for (uint64_t r = 0; r <= nr; r++) po[r] = rec_off[s.r0 + r] - s.e0;
+    const uint64_t t2 = now_ns();
+    ctx->host_wait_ns += t1 - t0;
+    ctx->host_copy_ns += t2 - t1;
+    ctx->host_copy_bytes += n * 4 + (nr + 1) * 8;
     if (i >= 2) SG_HIP(hipStreamWaitEvent(ctx->copy_stream, ev_tri[k], 0));  // slice i-2's triage has read device k
     if (n) SG_HIP(hipMemcpyAsync(dv, pv, n * 4, hipMemcpyHostToDevice, ctx->copy_stream));
     SG_HIP(hipMemcpyAsync(dof, po, (nr + 1) * 8, hipMemcpyHostToDevice, ctx->copy_stream));

@@ -61,7 +61,7 @@ struct PrefixSlice {
 };
 
 // One kept batch of the two-phase triage: its record slices and their
-// partitions (or, with SG_PREFIX_PAIRS, its first-owner pairs), in a workspace of
+// partitions (or, with option prefix_pairs, its first-owner pairs), in a workspace of
 // its own (two slots, so one batch's exchange can run while the next one is
 // partitioned)
 struct PrefixSlot {
@@ -76,8 +76,35 @@ struct PrefixSlot {
 };
 constexpr uint32_t kPrefixSlots = 2;
 
+// Context options (sg_ctx_set_option): each regime selects its own path, and
+// an option only forces one, for a test or a measurement.  -1 = the regime's
+// choice.  No option is read from the environment on a call; sg_ctx_create
+// seeds the diagnostics ones (debug_part, bucket_blocks, prefix_pairs) from
+// SG_DEBUG_PART / SG_BUCKET_BLOCKS / SG_PREFIX_PAIRS for the GPU scripts.
+enum SgOpt : int {
+  kOptBucketBlocks = 0,     // cap of the persistent bucket grid (0: none)
+  kOptPrefixPairs,          // prefix_begin's form when the caller passes -1 (0 kept partitions, 1 pairs)
+  kOptFoldMap,              // one-group fold: -1 by range, 0 never the byte map
+  kOptMinimizeFilter,       // Minimize's value filter: 1 on, 0 off
+  kOptMinimizeFilterRanks,  // Minimize phase A length (0: the default)
+  kOptReportDirect,         // cover report: 1 the global-search form at any size
+  kOptRpcEncodeElems,       // delta encode: -1 by shape, 0 per-list, 1 per-element
+  kOptRpcDecodeBlocks,      // delta decode: -1 by shape, 0 per-list, 1 per-block
+  kOptHostSlice,            // host ingest: entries per record slice (0: the default)
+  kOptHostCopyThreads,      // host ingest: pageable -> pinned copy threads (0: from the CPU quota)
+  kOptCount
+};
+
 struct sg_ctx {
   int device = 0;
+  int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0};
+  // host CPUs this process may use (cgroup cpu.max quota, else the affinity
+  // mask), read at creation: sizes the host ingest's copy threads
+  double cpu_quota = 0;
+  // the host ingest's last call (sg_host.hip): bytes copied pageable -> pinned,
+  // the wall time of those copies and of its waits for the staging slots'
+  // DMA, and the copy threads used
+  uint64_t host_copy_bytes = 0, host_copy_ns = 0, host_wait_ns = 0, host_threads = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   // grow-only device workspace and pinned host staging
@@ -93,14 +120,13 @@ struct sg_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t pipe_ev[4] = {};
   // first-owner table and its decreasing key floor; the key space is 2^32 - 1
-  // (SG_OWNER_KEY_SPACE lowers it, so tests reach the generation reset)
+  // (option owner_key_space lowers it, so tests reach the generation reset)
   uint32_t* owner = nullptr;
   uint64_t owner_floor = 0;
   uint64_t owner_key_space = 0xFFFFFFFFull;
   uint64_t owner_resets = 0;
-  // partitioned triage: records per launch (SG_TRIAGE_MAX_RECS lowers it, for
-  // tests of the record slicing) and diagnostics (SG_DEBUG_PART); the
-  // environment is read once, at context creation
+  // partitioned triage: records per launch (option max_launch_records lowers
+  // it, for tests of the record slicing) and diagnostics (option debug_part)
   uint64_t max_launch_recs = 0;
   // two-phase triage state (prefix_begin / prefix_end, sg_bucket.hip)
   PrefixSlot prefix[kPrefixSlots];
@@ -185,6 +211,8 @@ int set_add_dev_locked(sg_set* set, const uint32_t* d_vals, uint64_t n);
 // A batch in host memory through pinned double-buffered staging, record
 // slice by record slice, each slice's copies overlapping the previous one's
 // partitioned triage (sg_host.hip); takes the ctx lock.
+double host_cpu_quota();
+int host_copy_threads(const sg_ctx* ctx);
 int host_pipeline(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* vals, const uint64_t* rec_off,
                   uint64_t nrec, uint8_t* rec_new, bool trace);
 // Partitioned flags-only triage (sg_bucket.hip); ctx lock held.  trace:
@@ -219,7 +247,7 @@ int record_slice_cuts(sg_ctx* ctx, const uint64_t* d_off, uint64_t nrec, uint64_
 // signal not in base_words and keeps the batch's partitions (or each such
 // signal's first record) in the slot; end flags the records against
 // mwords | owords and, with `update`, updates mwords / nwords.
-// form: 0 kept partitions, 1 first-owner pairs, -1 from SG_PREFIX_PAIRS; d_ncand
+// form: 0 kept partitions, 1 first-owner pairs, -1 from option prefix_pairs; d_ncand
 // (nullable, device): the batch's distinct signals not in base_words.
 int prefix_begin(sg_ctx* ctx, uint32_t slot, const uint32_t* base_words, uint32_t* marks_words, const uint32_t* d_vals,
                  const uint64_t* d_off, uint64_t n, uint64_t nrec, int form = -1, uint64_t* d_ncand = nullptr);

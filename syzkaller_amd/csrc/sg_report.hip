@@ -838,10 +838,9 @@ int sg_cover_uncovered(sg_ctx* ctx, const uint32_t* cov, size_t ncov, uint32_t b
                o_is = p.add(((uint64_t)istart.nb + 1) * 4), o_ld2 = p.add(nsym * 4);
   // chunked query path (k_q_*) up to kMaxChunks chunks of call sites, the
   // per-query search passes (k_rep_first / k_rep_del) past them;
-  // SG_REPORT_DIRECT=1 takes the latter at any size (a test hook for the
+  // option report_direct 1 takes the latter at any size (a test hook for the
   // > 16M-site regime)
-  const char* direct_env = getenv("SG_REPORT_DIRECT");
-  const bool chunked = nall <= (uint64_t)kSites * kMaxChunks && !(direct_env && atoi(direct_env));
+  const bool chunked = nall <= (uint64_t)kSites * kMaxChunks && ctx->opt[kOptReportDirect] <= 0;
   const uint32_t nch = div_up(nall, kSites);
   // query tiles: 64K queries per count / scatter workgroup
   const uint32_t ntq = div_up(ncov, (uint64_t)kQT * kSQPer * kSQSub);

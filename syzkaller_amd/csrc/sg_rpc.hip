@@ -487,15 +487,13 @@ __global__ void k_sancov(const uint32_t* __restrict__ cov, const uint64_t* __res
 // fewer than 256 lists or more than 64 Ki values (bytes) per list on average.
 constexpr uint64_t kWaveListsMin = 256, kWaveListAvg = 65536;
 
-static bool enc_elems(uint64_t n, uint64_t N) {  // read at each call (tests switch it)
-  const char* e = getenv("SG_RPC_ENCODE_ELEMS");
-  if (e) return atoi(e) != 0;
+static bool enc_elems(const sg_ctx* ctx, uint64_t n, uint64_t N) {  // (option rpc_encode_elems forces a form)
+  if (ctx->opt[kOptRpcEncodeElems] >= 0) return ctx->opt[kOptRpcEncodeElems] != 0;
   return n < kWaveListsMin || N / n > kWaveListAvg;
 }
 
-static bool dec_blocks(uint64_t n, uint64_t nb) {  // read at each call (tests switch it)
-  const char* e = getenv("SG_RPC_DECODE_BLOCKS");
-  if (e) return atoi(e) != 0;
+static bool dec_blocks(const sg_ctx* ctx, uint64_t n, uint64_t nb) {  // (option rpc_decode_blocks forces a form)
+  if (ctx->opt[kOptRpcDecodeBlocks] >= 0) return ctx->opt[kOptRpcDecodeBlocks] != 0;
   return n < kWaveListsMin || nb / n > kWaveListAvg;
 }
 
@@ -528,7 +526,7 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
   uint64_t* kw = (uint64_t*)ws_at(ctx, o_kw);
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   // (a list's byte count is a u32: the per-list form when 5 N cannot overflow it)
-  if (!enc_elems(n, N) && N * 5 < (1ull << 32)) {
+  if (!enc_elems(ctx, n, N) && N * 5 < (1ull << 32)) {
     ScopedTimer tm(ctx, "rpc_encode");
     uint32_t* lbytes = (uint32_t*)ws_at(ctx, o_lb);
     hipLaunchKernelGGL(k_enc_list_len, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_v, d_off, n, lbytes,
@@ -538,7 +536,7 @@ int encode_dev(sg_ctx* ctx, const uint32_t* d_v, const uint64_t* d_off, uint64_t
     hipLaunchKernelGGL(k_enc_list_write, dim3((uint32_t)div_up(n, 4)), dim3(256), 0, ctx->stream, d_v, d_off, n,
                        (const uint64_t*)lo, out);
   } else {
-    // (SG_RPC_ENCODE_ELEMS=1: the per-element form)
+    // (option rpc_encode_elems 1: the per-element form)
     ScopedTimer tm(ctx, "rpc_encode");
     if (N) {
       hipLaunchKernelGGL(k_word_lists, dim3(grid_for((N + 31) / 32)), dim3(256), 0, ctx->stream, d_off, n, N, kw);
@@ -587,7 +585,7 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
   SG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
   ScopedTimer tm(ctx, "rpc_decode");
   // (a list's value count is a u32: the per-list form when nb cannot overflow it)
-  const bool lists = nb && nb < (1ull << 32) && !dec_blocks(n, nb);
+  const bool lists = nb && nb < (1ull << 32) && !dec_blocks(ctx, n, nb);
   if (lists) {
     // the lists' value counts, their scan; no host wait between the passes:
     // the decode checks the capacity itself (error bit 2: nothing written)
@@ -611,7 +609,7 @@ int decode_dev(sg_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off, uint6
       set_error("sg_delta_decode: %llu values, capacity %llu", (unsigned long long)N, (unsigned long long)cap);
       return SG_EINVAL;
     }
-    // (SG_RPC_DECODE_BLOCKS=1: the per-block form -- runs per 32-byte block,
+    // (option rpc_decode_blocks 1: the per-block form -- runs per 32-byte block,
     // then a scan of the deltas)
     if (nb) {
       SG_HIP(hipMemsetAsync(heads, 0, nblk * 4 + 4, ctx->stream));

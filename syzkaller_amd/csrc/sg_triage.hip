@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kOwnWaves * 64) __attribute__((amdgpu_waves_per_eu(
       ghi = a.e0 + a.roff[R0 + lane + 1];
     }
     const uint32_t gnp = gq.y - gq.x;
-    if ((uint32_t)lane < nb) a.rec_new[R0 + lane] = gnp ? 1 : 0;  // queued iff it owns a signal (fuzzer.go:678-690)
+    if (a.rec_new && (uint32_t)lane < nb) a.rec_new[R0 + lane] = gnp ? 1 : 0;  // queued iff it owns a signal (fuzzer.go:678-690)
     const uint64_t gc0 = glo / kChunk, gc1 = gnp ? (ghi - 1) / kChunk : gc0;
     const bool mine = gnp && gnp <= kOwnWave && gc1 - gc0 < (uint64_t)kOwnCB && gc1 < nfull;
     if (gnp && !mine) a.big[1 + atomicAdd(a.big, 1u)] = R0 + lane;
@@ -1432,14 +1432,11 @@ int sg_minimize(sg_ctx* ctx, const uint32_t* vals, const uint64_t* off, size_t n
   // phase A: ranks < R (the first ~kFiltElems elements in processing order)
   // claim one workgroup per input and fill the filter set; phase B: the rest
   // through the persistent filtered claim (k_min_claim_f)
-  const char* filt_env = getenv("SG_MINIMIZE_FILTER");
-  const bool use_filt = !filt_env || atoi(filt_env);
-  // phase A: the first kFiltRanks inputs (SG_MINIMIZE_FILTER_RANKS: tests
+  const bool use_filt = ctx->opt[kOptMinimizeFilter] != 0;
+  // phase A: the first kFiltRanks inputs (option minimize_filter_ranks: tests
   // raise it past the filter's values' inputs)
-  const char* fr_env = getenv("SG_MINIMIZE_FILTER_RANKS");
-  const uint64_t R = use_filt && n > kFiltRanks ? std::min<uint64_t>(n - 1, std::max<uint64_t>(
-                                                       kFiltRanks, fr_env ? (uint64_t)atoll(fr_env) : 0))
-                                                 : n;
+  const uint64_t fr = ctx->opt[kOptMinimizeFilterRanks] > 0 ? (uint64_t)ctx->opt[kOptMinimizeFilterRanks] : 0;
+  const uint64_t R = use_filt && n > kFiltRanks ? std::min<uint64_t>(n - 1, std::max<uint64_t>(kFiltRanks, fr)) : n;
   {
     ScopedTimer tm(ctx, "min_claim");
     SG_HIP(hipMemsetAsync(dtouch, 0, kSetBytes, ctx->stream));

@@ -486,6 +486,8 @@ class PrefixTriage:
         if ev is not None:
             ev.synchronize()
         c = self.slots[slot]["cnts_h"].view(-1, 2).tolist()
+        if any(n < 0 for n, _ in c):  # a rank ran a form that does not count: no data, stay dense
+            return "dense"
         frac = max(n / max(e, 1) for n, e in c)
         return "sparse" if frac < self.sparse_below else "dense"
 
@@ -498,7 +500,7 @@ class PrefixTriage:
         None when the batch ran without the counts (one rank without
         collectives, or a form that does not count)."""
         last, G = self.last, self.comm.world
-        if "slot" not in last or last.get("form") == "default":
+        if "slot" not in last or last.get("form") == "default" or self.exchange == "dense":
             return None
         counts = self.slots[last["slot"]]["cnts_h"].view(-1, 2)[:, 0].tolist()
         m = max(counts)
@@ -550,20 +552,22 @@ class PrefixTriage:
                     b["ncand_h"].copy_(b["ncand"])
                 self._nov = (slot, nvals, ev)
         # every rank's (candidates, entries): the sparse form's counts now, the
-        # agreed form two batches on
-        if form is None:
-            b["ncand"].zero_()
-        b["cnt"][:1].copy_(b["ncand"])
-        b["cnt"][1] = nvals
-        c.all_gather_equal(b["cnts"], b["cnt"])
-        if b["cnts"].is_cuda:
-            b["cnts_h"].copy_(b["cnts"], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-        else:
-            b["cnts_h"].copy_(b["cnts"])
-            ev = None
-        self.counted = (self.counted + [(slot, ev)])[-2:]
+        # agreed form two batches on (not gathered when the exchange is forced
+        # dense: nothing reads them then, and the gather would wait on step 1)
+        if self.exchange != "dense":
+            if form is None:  # (the library's default form counts nothing: unknown, not 0)
+                b["ncand"].fill_(-1)
+            b["cnt"][:1].copy_(b["ncand"])
+            b["cnt"][1] = nvals
+            c.all_gather_equal(b["cnts"], b["cnt"])
+            if b["cnts"].is_cuda:
+                b["cnts_h"].copy_(b["cnts"], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                b["cnts_h"].copy_(b["cnts"])
+                ev = None
+            self.counted = (self.counted + [(slot, ev)])[-2:]
         pend["slot"] = slot
         if xform == "sparse":
             # 2. the candidate lists of every rank (padded to the longest)

@@ -44,6 +44,22 @@ def ctx():
     yield c
 
 
+@pytest.fixture
+def ctx_option():
+    """set(context, key, value): a context option (sg_ctx_set_option) for one
+    test, restored after it."""
+    saved = []
+
+    def set_(c, key, value):
+        saved.append((c, key, c.get_option(key)))
+        c.set_option(key, value)
+
+    yield set_
+    for c, key, v in reversed(saved):
+        if c.h:
+            c.set_option(key, v)
+
+
 @pytest.fixture(scope="session")
 def kats():
     import json

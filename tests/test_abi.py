@@ -89,3 +89,34 @@ def test_minimize_order_matches_oracle_go_sort():
             lens = rng.integers(0, lenhi, size=n)
             off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
             assert np.array_equal(minimize_order(off), O.minimize_order(off)), (n, lenhi)
+
+
+def test_no_environment_reads_on_calls():
+    """Production behaviour does not depend on the process environment: the
+    only getenv calls are sg_ctx_create's seeding of the diagnostics options
+    (sg_ctx_set_option sets the rest)."""
+    csrc = os.path.join(ROOT, "syzkaller_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        src = open(os.path.join(csrc, f)).read()
+        if f != "sg_ctx.hip":
+            assert "getenv" not in src, f
+            continue
+        body = src[src.index("int sg_ctx_create("):]
+        body = body[: body.index("\n}\n")]
+        assert src.count("getenv") == body.count("getenv") == 3
+
+
+@pytest.mark.gpu
+def test_context_options(ctx):
+    from syzkaller_amd._lib import SG_EINVAL, SyzSigError
+
+    assert ctx.get_option("fold_map") == -1 and ctx.get_option("minimize_filter") == 1
+    assert ctx.get_option("max_launch_records") == 1 << 24
+    ctx.set_option("rpc_decode_blocks", 1)
+    assert ctx.get_option("rpc_decode_blocks") == 1
+    ctx.set_option("rpc_decode_blocks", -1)
+    for bad in (("no_such_option", 1), ("max_launch_records", (1 << 24) + 1), ("max_launch_records", -2)):
+        with pytest.raises(SyzSigError) as e:
+            ctx.set_option(*bad)
+        assert e.value.rc == SG_EINVAL
+    assert ctx.counter("cpu_quota_milli") >= 1000

@@ -113,12 +113,12 @@ def test_union_fold_zipf_corpus(ctx):
 
 
 @pytest.mark.gpu
-def test_union_fold_byte_map_edges(ctx, monkeypatch):
+def test_union_fold_byte_map_edges(ctx, ctx_option):
     """One group of canonical lists takes the byte map over [AND, OR] of the
     values: value 0, spans just under and over 2^28 (the latter sorts), the
     sentinel (dropped; its presence widens the span, so the fold sorts), lists
     sharing most values, a wide span over few values (too sparse for the map:
-    sorts); each equal to the oracle and to the sort (SG_FOLD_MAP=0)."""
+    sorts); each equal to the oracle and to the sort (option fold_map 0)."""
     from syzkaller_amd import cover as C
 
     rng = np.random.default_rng(57)
@@ -138,9 +138,9 @@ def test_union_fold_byte_map_edges(ctx, monkeypatch):
         ev, eo = O.union_fold(vals, off)
         gv, go = C.union_fold(vals, off, ctx=ctx)
         assert np.array_equal(go, eo) and np.array_equal(gv, ev), span
-        monkeypatch.setenv("SG_FOLD_MAP", "0")
+        ctx_option(ctx, "fold_map", 0)
         sv, so = C.union_fold(vals, off, ctx=ctx)
-        monkeypatch.delenv("SG_FOLD_MAP")
+        ctx.set_option("fold_map", -1)
         assert np.array_equal(so, eo) and np.array_equal(sv, ev), span
 
 

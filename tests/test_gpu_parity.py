@@ -258,14 +258,14 @@ def test_minimize_vs_oracle(C):
         assert np.array_equal(C.minimize_csr(rv, ro, order), O.minimize(rv, ro, order)), n
 
 
-def test_minimize_filtered_claim(C, monkeypatch):
+def test_minimize_filtered_claim(C, ctx_option):
     """Minimize's filtered claim (sg_triage.hip k_min_claim_f): the values
     common to the first inputs in processing order fill an LDS set, and later
     elements found in it skip the owner table.  Phase A (the inputs claimed
     one workgroup each) is the first 4 inputs, or more
-    (SG_MINIMIZE_FILTER_RANKS); Zipf values (most later elements held),
+    (option minimize_filter_ranks); Zipf values (most later elements held),
     sentinels, empty inputs, inputs longer than a claim window, any
-    processing order, and the unfiltered path (SG_MINIMIZE_FILTER=0)."""
+    processing order, and the unfiltered path (option minimize_filter 0)."""
     rng = np.random.default_rng(108)
 
     def corpus(n, med, hi, s=1.1):
@@ -282,15 +282,16 @@ def test_minimize_filtered_claim(C, monkeypatch):
 
     for n, med, hi, budget in [(3000, 40, 5000, "4"), (5000, 300, 1 << 20, "60"), (2500, 3000, 1 << 16, "1")]:
         vals, off = corpus(n, med, hi)
-        monkeypatch.setenv("SG_MINIMIZE_FILTER_RANKS", budget)
+        dc = C.default_context()
+        ctx_option(dc, "minimize_filter_ranks", int(budget))
         order = C.minimize_order(off)
         got = C.minimize_csr(vals, off, order)
-        monkeypatch.delenv("SG_MINIMIZE_FILTER_RANKS")
+        dc.set_option("minimize_filter_ranks", 0)
         assert np.array_equal(got, O.minimize(vals, off, order)), (n, budget)
         perm = rng.permutation(n).astype(np.uint32)
-        monkeypatch.setenv("SG_MINIMIZE_FILTER_RANKS", budget)
+        dc.set_option("minimize_filter_ranks", int(budget))
         got = C.minimize_csr(vals, off, perm)
-        monkeypatch.delenv("SG_MINIMIZE_FILTER_RANKS")
+        dc.set_option("minimize_filter_ranks", 0)
         assert np.array_equal(got, O.minimize(vals, off, perm)), (n, budget)
     # just past phase A: one or two inputs left, empty inputs, all-sentinel inputs
     for covs in ([[1, 2, 3], [2, 3], [3], [3, 4], [4, 5]], [[7, 8], [], [8], [], [SENT], [8, 9], []],
@@ -301,7 +302,7 @@ def test_minimize_filtered_claim(C, monkeypatch):
     vals, off = corpus(12000, 200, 1 << 22)  # the default phase A
     order = C.minimize_order(off)
     assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order))
-    monkeypatch.setenv("SG_MINIMIZE_FILTER", "0")
+    ctx_option(C.default_context(), "minimize_filter", 0)
     assert np.array_equal(C.minimize_csr(vals, off, order), O.minimize(vals, off, order))
 
 
@@ -721,7 +722,7 @@ def test_triage_dev_unaligned_input(C):
         assert np.array_equal(ns.export(), on.export())
 
 
-def test_triage_record_slices(C, monkeypatch):
+def test_triage_record_slices(C):
     """Batches above the per-launch record limit run as consecutive record
     slices (sg_bucket.hip bucket_triage); the limit is lowered here so that
     slices start mid-batch, at empty records and at group boundaries.  The
@@ -730,8 +731,8 @@ def test_triage_record_slices(C, monkeypatch):
     (1, 5000)."""
     rng = np.random.default_rng(131)
     for limit, nrec in ((1000, 4321), (100000, 240000), (7, 50), (3, 300), (1, 5000)):
-        monkeypatch.setenv("SG_TRIAGE_MAX_RECS", str(limit))
-        ctx = C.Context(0)  # the switch is read at context creation
+        ctx = C.Context(0)
+        ctx.set_option("max_launch_records", limit)
         assert ctx.counter("max_launch_records") == limit
         P = TwoPaths(C, ctx)
         om, on = O.OSet(), O.OSet()
@@ -747,18 +748,17 @@ def test_triage_record_slices(C, monkeypatch):
         assert np.array_equal(m, om.export()) and np.array_equal(n, on.export())
         del P
         ctx.close()
-    monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
 
 
-def test_owner_key_generation_reset(C, monkeypatch):
+def test_owner_key_generation_reset(C):
     """The first-owner table (sg_ctx.hip owner_keys) hands out decreasing keys
     and starts a fresh generation (a full reset of the table) when the key
     space runs out.  The key space is lowered here so that rank-keyed
     Minimize crosses several resets, between triage batches and Poll merges
     (which take their owners from the bucket stage, not the table); every
     result still equals the oracle's."""
-    monkeypatch.setenv("SG_OWNER_KEY_SPACE", "1500")
     ctx = C.Context(0)
+    ctx.set_option("owner_key_space", 1500)
     assert ctx.counter("owner_key_space") == 1500
     rng = np.random.default_rng(151)
     ms, ns, mm = C.SignalSet(ctx), C.SignalSet(ctx), C.SignalSet(ctx)
@@ -819,13 +819,13 @@ def test_cover_uncovered_radix_edges(C):
     assert np.array_equal(got, exp)
 
 
-def test_cover_uncovered_chunk_edges(C, monkeypatch):
+def test_cover_uncovered_chunk_edges(C, ctx_option):
     """The chunked query path (sg_report.hip k_q_*): a chunk whose PC range
     spans more symbols than it holds in LDS (many site-less symbols: global
     symbol search), queries below the first and above the last call site,
     site counts at and around the 4096-site chunk size; the same queries in
     PC order (no regrouping), and through the direct per-query passes of the
-    > 16M-site regime (SG_REPORT_DIRECT=1)."""
+    > 16M-site regime (option report_direct 1)."""
     rng = np.random.default_rng(143)
     hi32 = np.uint64(0xffffffff) << np.uint64(32)
     base = np.uint64(0xffffffff81000000)
@@ -850,9 +850,9 @@ def test_cover_uncovered_chunk_edges(C, monkeypatch):
         qs = np.sort(q)
         assert np.array_equal(C.cover_uncovered(qs, 0xffffffff, starts, ends, sites),
                               O.cover_uncovered(qs, 0xffffffff, starts, ends, sites)), sites.size
-        monkeypatch.setenv("SG_REPORT_DIRECT", "1")
+        ctx_option(C.default_context(), "report_direct", 1)
         got = C.cover_uncovered(q, 0xffffffff, starts, ends, sites)
-        monkeypatch.delenv("SG_REPORT_DIRECT")
+        C.default_context().set_option("report_direct", 0)
         assert np.array_equal(got, exp), sites.size
 
 

@@ -65,7 +65,7 @@ def _dev_reference(ctx, m0, d_vals, d_off, trace):
 
 
 @pytest.mark.parametrize("trace", [False, True])
-def test_host_pipeline_slices_equal_device_path(ctx, monkeypatch, trace):
+def test_host_pipeline_slices_equal_device_path(ctx, ctx_option, trace):
     from syzkaller_amd import cover as C
 
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -81,10 +81,7 @@ def test_host_pipeline_slices_equal_device_path(ctx, monkeypatch, trace):
     # default slices (one slice here), many slices, slices of about one record,
     # and slices smaller than a record (each record then is a slice of its own)
     for slice_entries in (None, 1 << 19, 1000, 300):
-        if slice_entries is None:
-            monkeypatch.delenv("SG_HOST_SLICE", raising=False)
-        else:
-            monkeypatch.setenv("SG_HOST_SLICE", str(slice_entries))
+        ctx_option(ctx, "host_slice", slice_entries or 0)
         ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
         C.SignalAdd(ms, m0)
         if trace:
@@ -98,7 +95,7 @@ def test_host_pipeline_slices_equal_device_path(ctx, monkeypatch, trace):
         ns.close()
 
 
-def test_host_pipeline_copy_threads_and_empty_records(ctx, monkeypatch):
+def test_host_pipeline_copy_threads_and_empty_records(ctx, ctx_option):
     """Empty records at slice edges, one copy thread or many, and a batch of
     only empty records."""
     from syzkaller_amd import cover as C
@@ -113,8 +110,8 @@ def test_host_pipeline_copy_threads_and_empty_records(ctx, monkeypatch):
     m0 = np.unique(vals[: vals.size // 3])
     exp = _dev_reference(ctx, m0, d_vals, d_off, False)
     for thr, sl in ((1, 777), (16, 5000), (3, 1 << 26)):
-        monkeypatch.setenv("SG_HOST_COPY_THREADS", str(thr))
-        monkeypatch.setenv("SG_HOST_SLICE", str(sl))
+        ctx_option(ctx, "host_copy_threads", thr)
+        ctx_option(ctx, "host_slice", sl)
         ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
         C.SignalAdd(ms, m0)
         got, _, _ = C.triage_batch(ms, ns, vals, off, want_diff=False, ctx=ctx)

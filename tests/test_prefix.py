@@ -207,8 +207,11 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
                 xbytes.append(tri.last["exchange_bytes"])
                 # the batch's exchange in both forms: the one it took is what it sent
                 model = tri.exchange_model()
-                models.append(model is not None and model[tri.last["exchange"]] == tri.last["exchange_bytes"]
-                              and model["sparse"] == (4 * model["candidates_max"] + 16) * (world - 1))
+                if exchange == "dense":  # (forced dense: no counts are gathered, no model)
+                    models.append(model is None)
+                else:
+                    models.append(model is not None and model[tri.last["exchange"]] == tri.last["exchange_bytes"]
+                                  and model["sparse"] == (4 * model["candidates_max"] + 16) * (world - 1))
                 continue
             # the next batch started (marked against the maxSignal that still
             # lacks this batch's total) before the previous one is finished
@@ -231,7 +234,11 @@ def _worker(rank, world, port, q, pipelined, gather, drain=False, pairs_below=0.
                           (2, True, True, False, 0.05), (4, False, True, False, 0.05),
                           (2, True, False, True, 0.05), (4, True, True, True, 0.05),
                           (2, False, False, False, 2.0), (4, True, False, True, 2.0),
-                          (2, True, True, False, -1.0)])
+                          (2, True, True, False, -1.0),
+                          # G = 8, the C3 node: the prefix-OR over 7 predecessors,
+                          # gather mode's 8 bitmaps per rank
+                          (8, False, False, False, 0.05), (8, True, True, True, 0.05),
+                          (8, True, False, False, 2.0)])
 def test_prefix_triage_equals_sequential_loop(world, pipelined, gather, drain, pairs_below):
     _run_and_check(world, pipelined, gather, drain, pairs_below, "auto", None, None)
 
@@ -310,7 +317,13 @@ def _run_and_check(world, pipelined, gather, drain, pairs_below, exchange, spars
                           (4, True, False, True, "auto", 2.0, ["dense", "dense", "sparse", "sparse", "sparse"]),
                           (4, False, False, False, "sparse", None, ["sparse"] * 5),
                           (2, True, True, True, "sparse", None, ["sparse"] * 5),
-                          (4, True, True, False, "auto", 0.2, None)])
+                          (4, True, True, False, "auto", 0.2, None),
+                          # G = 8: the count agreement over 8 ranks, dense / sparse / auto,
+                          # gather and all-to-all modes
+                          (8, True, False, True, "auto", 2.0, ["dense", "dense", "sparse", "sparse", "sparse"]),
+                          (8, False, True, False, "sparse", None, ["sparse"] * 5),
+                          (8, True, False, False, "auto", 0.2, None),
+                          (8, True, True, False, "dense", None, ["dense"] * 5)])
 def test_prefix_sparse_exchange_equals_sequential_loop(world, pipelined, gather, drain, exchange, sparse_below, expect):
     """The candidate-list exchange: forced from the first
     batch, and mixed with the bitmap exchange within one run (the form agreed

@@ -65,11 +65,11 @@ def _lists(rng, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("blocks", ["0", "1"])  # the wave-per-list codec / the per-block and per-element forms
-def test_delta_batch_vs_oracle(ctx, monkeypatch, blocks):
+def test_delta_batch_vs_oracle(ctx, ctx_option, blocks):
     from syzkaller_amd import cover as C
 
-    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
-    monkeypatch.setenv("SG_RPC_ENCODE_ELEMS", blocks)
+    ctx_option(ctx, "rpc_decode_blocks", int(blocks))
+    ctx_option(ctx, "rpc_encode_elems", int(blocks))
 
     rng = np.random.default_rng(42)
     lists = _lists(rng, 200)
@@ -102,7 +102,7 @@ def test_delta_batch_vs_oracle(ctx, monkeypatch, blocks):
 
 
 @pytest.mark.gpu
-def test_delta_codec_list_edges(ctx, monkeypatch):
+def test_delta_codec_list_edges(ctx, ctx_option):
     """The per-list codec at every 16-byte / 4-value alignment: lists of 0-9
     and 255-257 values (steps of 256 values and 1 KiB, loads aligned down to
     the list's first value / byte), values 0 and 0xFFFFFFFF, long zero runs
@@ -110,8 +110,7 @@ def test_delta_codec_list_edges(ctx, monkeypatch):
     default routing takes the per-list kernels."""
     from syzkaller_amd import cover as C
 
-    monkeypatch.delenv("SG_RPC_DECODE_BLOCKS", raising=False)
-    monkeypatch.delenv("SG_RPC_ENCODE_ELEMS", raising=False)
+    assert ctx.get_option("rpc_decode_blocks") == -1 and ctx.get_option("rpc_encode_elems") == -1
     rng = np.random.default_rng(48)
     lists = []
     for k in range(300):
@@ -175,7 +174,7 @@ def test_sancov_batch_vs_oracle(ctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("blocks", ["0", "1"])
-def test_delta_decode_corrupted_payloads_vs_oracle(ctx, monkeypatch, blocks):
+def test_delta_decode_corrupted_payloads_vs_oracle(ctx, ctx_option, blocks):
     """Decode accepts / rejects exactly what binary.Uvarint + a running sum do
     (oracle), on payloads with flipped high bits and cut ends, including runs
     that cross the decoder's 32-byte blocks, its 1 KiB wave steps and list
@@ -183,7 +182,7 @@ def test_delta_decode_corrupted_payloads_vs_oracle(ctx, monkeypatch, blocks):
     from syzkaller_amd import cover as C
     from syzkaller_amd._lib import SyzSigError
 
-    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
+    ctx_option(ctx, "rpc_decode_blocks", int(blocks))
     rng = np.random.default_rng(7)
     for t in range(160):
         parts = []
@@ -215,7 +214,7 @@ def test_delta_decode_corrupted_payloads_vs_oracle(ctx, monkeypatch, blocks):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("blocks", ["0", "1"])
-def test_delta_decode_sum_past_32_bits(ctx, monkeypatch, blocks):
+def test_delta_decode_sum_past_32_bits(ctx, ctx_option, blocks):
     """A running sum that passes 2^32 - 1 at a chosen value, deep in a long
     list (across the decoder's lanes, rows and steps): rejected exactly when
     binary.Uvarint + the sum would overflow the uint32 (oracle), accepted when
@@ -223,7 +222,7 @@ def test_delta_decode_sum_past_32_bits(ctx, monkeypatch, blocks):
     from syzkaller_amd import cover as C
     from syzkaller_amd._lib import SyzSigError
 
-    monkeypatch.setenv("SG_RPC_DECODE_BLOCKS", blocks)
+    ctx_option(ctx, "rpc_decode_blocks", int(blocks))
     step = (1 << 24) + 1
     for m, last in ((300, None), (255, None), (256, None), (257, None), (1000, None), (255, 0xFFFFFFFF)):
         d = [step] * m

@@ -152,7 +152,7 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])  # 8: the C3 node (manager.go:957-962 fans out to every fuzzer)
 def test_sharded_triage_equals_sequential_loop(world):
     from oracle import pyoracle as O
 

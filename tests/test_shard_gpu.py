@@ -66,13 +66,13 @@ def test_shard_candidates_vs_numpy(ctx, g):
     assert np.array_equal(snap.export(), m0)
 
 
-def test_shard_candidates_record_slices(C, monkeypatch):
+def test_shard_candidates_record_slices(C):
     """Record slices of the local stage (a lowered per-launch record limit):
     a signal may come once per slice; its smallest record is the first one."""
     from syzkaller_amd.shard import HipStages
 
-    monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
     ctx2 = C.Context(0)
+    ctx2.set_option("max_launch_records", 777)
     vals, off = _batch(301, 5000, hi=1 << 16)
     snap = C.SignalSet(ctx2)
     st = HipStages(ctx2)
@@ -104,9 +104,9 @@ class _Words:
 
 @pytest.mark.parametrize("pairs", [False, True])
 @pytest.mark.parametrize("as_prefix", [False, True])
-def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, pairs):
+def test_prefix_begin_end_equals_triage(C, as_prefix, pairs):
     """sg_prefix_begin_dev / sg_prefix_end_dev (the partitions kept between
-    the two calls, or with SG_PREFIX_PAIRS the first-owner pairs; several
+    the two calls, or with option prefix_pairs the first-owner pairs; several
     record slices via a lowered per-launch record limit) against the oracle: the
     marks are the batch's signal not in the base set, and the flags after end
     are the sequential loop's against maxsig | prefix.  Without a prefix
@@ -114,10 +114,10 @@ def test_prefix_begin_end_equals_triage(C, monkeypatch, as_prefix, pairs):
     and M0 ∪ prefix ∪ new, and is the loop's after the prefix is ORed in."""
     from syzkaller_amd.shard import HipStages
 
-    monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "777")
-    if pairs:
-        monkeypatch.setenv("SG_PREFIX_PAIRS", "1")
     ctx2 = C.Context(0)
+    ctx2.set_option("max_launch_records", 777)
+    if pairs:
+        ctx2.set_option("prefix_pairs", 1)
     st = HipStages(ctx2)
     vals, off = _batch(305, 5000, hi=1 << 18)
     m0 = np.unique(np.random.default_rng(306).integers(0, 1 << 18, size=20000)).astype(np.uint32)

@@ -157,12 +157,12 @@ def test_traces_equal_exec_then_triage_on_gpu(C):
         ctx.reset_stream()
 
 
-def test_traces_record_slices(C, monkeypatch):
+def test_traces_record_slices(C):
     """Trace batches above the per-launch record limit (lowered here) run as
     record slices; each slice starts at a call start."""
     rng = np.random.default_rng(704)
-    monkeypatch.setenv("SG_TRIAGE_MAX_RECS", "500")
     ctx = C.Context(0)
+    ctx.set_option("max_launch_records", 500)
     try:
         lens = rng.integers(0, 60, size=3000)
         lens[rng.integers(0, lens.size, size=600)] = 0
@@ -177,7 +177,6 @@ def test_traces_record_slices(C, monkeypatch):
         ns.close()
     finally:
         ctx.close()
-        monkeypatch.delenv("SG_TRIAGE_MAX_RECS")
 
 
 def test_exec_signal_queued_lists(C, ctx):
