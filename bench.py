@@ -626,29 +626,51 @@ def run_host_api(ctx, b, maxsig, newsig, m0set, gpu_flags, reps=3):
     """The drop-in host entry point (sg_triage_batch, flags + set updates) on
     one C2 batch handed over in pageable host memory, as the Go adapter hands
     it (the signal is born in host shm, pkg/ipc/ipc_linux.go:247): the
-    pipelined ingest of sg_host.hip.  End to end, PCIe included; never `value`."""
+    pipelined ingest of sg_host.hip.  End to end, PCIe included; never `value`.
+    The call's own stage rates come from the context's counters: the
+    pageable -> pinned copies (GB/s over the copy threads' wall time) and the
+    time the host waited for a staging slot's DMA; the default thread count
+    (half the CPU quota) is timed beside 4 and 16 threads."""
     vals = b.vals.cpu().numpy().view(np.uint32).copy()
     off = b.off.cpu().numpy().view(np.uint64).copy()
     flags = np.zeros(b.nrec, dtype=np.uint8)
     nbytes = vals.nbytes + off.nbytes
     pinned = pinned_h2d_gbs()
-    times, ok = [], True
-    for _ in range(reps):
-        call("sg_set_copy", maxsig.h, m0set.h)
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        call("sg_triage_batch", ctx.h, maxsig.h, newsig.h, vals.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-             off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), b.nrec,
-             flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None, None, None)
-        times.append(time.perf_counter() - t)
-        ok &= bool(np.array_equal(flags, gpu_flags))
-    t = min(times)
-    return {"workload": f"C2 batch in pageable host memory ({b.nvals} signal entries, {nbytes / 1e9:.2f} GB with the "
-                        "record offsets) through sg_triage_batch: record slices through pinned double-buffered "
-                        "staging, each slice's copies overlapping the previous slice's triage (sg_host.hip)",
-            "value": b.nvals / t, "unit": "PCs/s (PCIe-inclusive)", "ms_per_batch": t * 1e3,
-            "h2d_gbs": nbytes / t / 1e9, "pinned_h2d_gbs": pinned, "frac_of_pinned_h2d": nbytes / t / 1e9 / pinned,
-            "flags_equal_device_path": ok, "reps": reps}
+    ok = True
+
+    def leg(threads):
+        nonlocal ok
+        ctx.set_option("host_copy_threads", threads)
+        best = None
+        for _ in range(reps):
+            call("sg_set_copy", maxsig.h, m0set.h)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            call("sg_triage_batch", ctx.h, maxsig.h, newsig.h, vals.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                 off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), b.nrec,
+                 flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None, None, None)
+            t = time.perf_counter() - t
+            ok &= bool(np.array_equal(flags, gpu_flags))
+            c = {k: ctx.counter(k) for k in ("host_copy_bytes", "host_copy_ns", "host_wait_ns", "host_copy_threads")}
+            if best is None or t < best[0]:
+                best = (t, c)
+        t, c = best
+        return {"ms_per_batch": t * 1e3, "h2d_gbs": nbytes / t / 1e9, "frac_of_pinned_h2d": nbytes / t / 1e9 / pinned,
+                "copy_threads": c["host_copy_threads"],
+                "pageable_to_pinned_gbs": c["host_copy_bytes"] / max(c["host_copy_ns"], 1),
+                "host_copy_ms": c["host_copy_ns"] / 1e6, "host_wait_dma_ms": c["host_wait_ns"] / 1e6}
+
+    dflt = leg(0)
+    sweep = {str(k): leg(k) for k in (4, 16) if k != dflt["copy_threads"]}
+    ctx.set_option("host_copy_threads", 0)
+    out = {"workload": f"C2 batch in pageable host memory ({b.nvals} signal entries, {nbytes / 1e9:.2f} GB with the "
+                       "record offsets) through sg_triage_batch: record slices through pinned double-buffered "
+                       "staging, each slice's copies overlapping the previous slice's triage (sg_host.hip)",
+           "value": b.nvals / (dflt["ms_per_batch"] / 1e3), "unit": "PCs/s (PCIe-inclusive)"}
+    out.update(dflt)
+    out.update({"pinned_h2d_gbs": pinned, "cpu_quota": ctx.counter("cpu_quota_milli") / 1000.0,
+                "flags_equal_device_path": ok, "reps": reps, "threads_sweep": sweep})
+    return out
 
 
 def run_from_traces(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new, steps):

@@ -19,7 +19,7 @@ import torch.distributed as dist
 
 from bench import (METRIC, STEP_KERNELS, Gen, build_m0, call, cpu_baseline, kernel_table, n_uniq, pmc_bytes_per_step,
                    step_bytes, triage, HBM_PEAK_GBS, Context, SignalSet, U32_WORDS, StepTimer)
-from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage
+from syzkaller_amd.shard import Comm, HipStages, PrefixTriage, ShardedTriage, exchange_time_model
 
 SHARD_KERNELS = STEP_KERNELS + ["shard_local", "shard_route", "shard_owner", "shard_resolve", "shard_flags",
                                 "set_add", "prefix_or", "bucket_mark", "prefix_flags", "prefix_merge", "set_or", "set_or_new_or",
@@ -260,6 +260,11 @@ def run_c3(ctx, args, cfg, rank, world):
         "accounting": acct,
         "exchange_bytes_per_rank_per_step": xgmi,
         "exchange_bytes_by_form_first_batch": xmodel,
+        # the exchange time model of DESIGN.md §5 at this world size and at G = 8
+        # (the node the driver's scaling run uses), for checking measured N > 1 steps
+        "predicted_exchange_ms": ({str(g): exchange_time_model(g, gather=tri.gather if g == world else None,
+                                                               cand_max=(xmodel or {}).get("candidates_max"))
+                                   for g in sorted({world, 8})} if prefix else None),
         "prefix_forms": forms[-args.steps:] if prefix and forms else None,
         "exchange_forms": [f for f, _ in xchg[-args.steps:]] if prefix else None,
         "path": ("prefix (syzkaller_amd/shard.py PrefixTriage)" if prefix else

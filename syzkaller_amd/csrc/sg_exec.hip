@@ -66,12 +66,17 @@ constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int K>
+// kDbg (option debug_part): per program, as its waves see them, dbg[8 p + j]:
+// 0 deciding-wave cycles in its steps, 1 its cycles at the window barrier,
+// 2 steps, 3 windows, 4 producer cycles compacting, 5 building, 6 at the
+// barrier, 7 the block's cycles in the window loop
+template <int K, bool kDbg>
 __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict__ pcs,
                                                       const uint64_t* __restrict__ call_off,
                                                       const uint64_t* __restrict__ prog_off, uint32_t* __restrict__ tmp,
                                                       uint32_t* __restrict__ cnt, const uint64_t* __restrict__ pstop,
-                                                      const uint8_t* __restrict__ emit) {
+                                                      const uint8_t* __restrict__ emit,
+                                                      unsigned long long* __restrict__ dbg) {
   constexpr int W = 64 * K;
   __shared__ uint32_t table[kDedupSize + 8];        // + mirror of slots 0..2, dummy slot 8196
   __shared__ unsigned long long wlist[2][W];        // position << 32 | signal, region-major
@@ -228,12 +233,16 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
     }
     if (lq && lane == 0) cnt[cq] = (uint32_t)(outpos - bq);
   };
+  unsigned long long dc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_loop = kDbg ? clock64() : 0, tk = t_loop;
   if (prod) build(0, sd, nd, cd, bd, ld, fd, ed);
   lds_sync();
   for (uint32_t it = 0;; it++) {
     const uint32_t buf = it & 1;
     const bool live = __hip_atomic_load(&wlive[buf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+    if (kDbg) tk = clock64();
     if (!prod) {
+      if (kDbg && live) dc[3]++;
       if (live) {
         const uint32_t bcw = wbc[buf][lane];
         const uint32_t base = bcw >> 16, iend = base + (bcw & 0xFFFFu);
@@ -248,6 +257,7 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
         uint32_t pos = i < iend ? (uint32_t)(cur >> 32) : kNoPos, pos2 = i + 1 < iend ? (uint32_t)(cu2 >> 32) : kNoPos;
         uint32_t s = (uint32_t)cur, s2 = (uint32_t)cu2;
         while (__ballot(pos != kNoPos)) {
+          if (kDbg) dc[2]++;
           const uint32_t left = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
           const uint32_t right = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
           const uint32_t hr = s & 127u, hr2 = s2 & 127u;
@@ -283,13 +293,30 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
           s2 = (uint32_t)nx2;
         }
       }
+      if (kDbg) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long t = clock64();
+        dc[0] += t - tk;
+        tk = t;
+      }
     } else {
       if (nq) compact(buf ^ 1);  // the window decided in the last iteration
+      if (kDbg) {
+        const unsigned long long t = clock64();
+        dc[4] += t - tk;
+        tk = t;
+      }
       uint32_t sb[K];
       int nb_ = 0;
       uint64_t cb = 0, bb = 0;
       bool lb = false, fb = false, eb = false;
       if (live) build(buf ^ 1, sb, nb_, cb, bb, lb, fb, eb);
+      if (kDbg) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long t = clock64();
+        dc[5] += t - tk;
+        tk = t;
+      }
       // shift: decided -> to compact, being decided -> decided next, built -> being decided
 #pragma unroll
       for (int k = 0; k < K; k++) {
@@ -310,9 +337,20 @@ __global__ __launch_bounds__(128) void k_exec_region2(const uint32_t* __restrict
       ed = eb;
     }
     lds_sync();
+    if (kDbg) {
+      const unsigned long long t = clock64();
+      dc[prod ? 6 : 1] += t - tk;
+    }
     if (!live) break;
   }
   // (the last decided window: compacted in the iteration that found no window to decide)
+  if (kDbg) {
+    dc[7] = clock64() - t_loop;
+    if (!prod && lane == 0)
+      for (int j : {0, 1, 2, 3, 7}) dbg[8 * p + j] = dc[j];
+    if (prod && lane == 0)
+      for (int j : {4, 5, 6}) dbg[8 * p + j] = dc[j];
+  }
 }
 
 // the calls each program has to run for its queued calls' lists: up to and
@@ -477,10 +515,39 @@ static int exec_signal(sg_ctx* ctx, const uint32_t* d_pcs, const uint64_t* d_cal
   if (pstop && nprog)
     hipLaunchKernelGGL(k_prog_stop, dim3(div_up(nprog, 256)), dim3(256), 0, ctx->stream, d_prog_off, d_rec_new, nprog,
                        pstop);
+  unsigned long long* ddbg = nullptr;
+  if (ctx->debug_part && nprog) {  // diagnostics: the per-program cycle breakdown (stderr)
+    SG_HIP(hipMalloc(&ddbg, nprog * 64));
+    SG_HIP(hipMemsetAsync(ddbg, 0, nprog * 64, ctx->stream));
+  }
   if (nprog) {
     ScopedTimer tm(ctx, "exec_signal");
-    hipLaunchKernelGGL((k_exec_region2<4>), dim3((uint32_t)nprog), dim3(128), 0, ctx->stream, d_pcs, d_call_off,
-                       d_prog_off, tmp, cnt, (const uint64_t*)pstop, d_rec_new);
+    if (ddbg)
+      hipLaunchKernelGGL((k_exec_region2<4, true>), dim3((uint32_t)nprog), dim3(128), 0, ctx->stream, d_pcs,
+                         d_call_off, d_prog_off, tmp, cnt, (const uint64_t*)pstop, d_rec_new, ddbg);
+    else
+      hipLaunchKernelGGL((k_exec_region2<4, false>), dim3((uint32_t)nprog), dim3(128), 0, ctx->stream, d_pcs,
+                         d_call_off, d_prog_off, tmp, cnt, (const uint64_t*)pstop, d_rec_new, nullptr);
+  }
+  if (ddbg) {
+    std::vector<unsigned long long> h(nprog * 8);
+    SG_HIP(hipMemcpyAsync(h.data(), ddbg, nprog * 64, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    hipFree(ddbg);
+    double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t nrun = 0;
+    for (uint64_t q = 0; q < nprog; q++) {
+      if (!h[8 * q + 3]) continue;
+      nrun++;
+      for (int j = 0; j < 8; j++) t[j] += (double)h[8 * q + j];
+    }
+    const double W = t[3] ? t[3] : 1;
+    fprintf(stderr,
+            "[exec dbg] programs run %llu of %llu, windows %.0f (%.1f per program), steps %.2f per window; cycles "
+            "per window: decide %.0f (%.1f per step), decider at barrier %.0f, producer compact %.0f, build %.0f, "
+            "producer at barrier %.0f; block loop %.0f per window\n",
+            (unsigned long long)nrun, (unsigned long long)nprog, t[3], t[3] / (nrun ? nrun : 1), t[2] / W, t[0] / W,
+            t[2] ? t[0] / t[2] : 0.0, t[1] / W, t[4] / W, t[5] / W, t[6] / W, t[7] / W);
   }
   SG_HIP(hipGetLastError());
   rc = scan_counts(ctx, cnt, d_sig_off, ncalls, scan_off);

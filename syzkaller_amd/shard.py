@@ -345,6 +345,35 @@ class ShardedTriage:
 
 
 
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (7 per MI355X, one to each peer of an 8-GPU node)
+COLLECTIVE_ALPHA_MS = 0.05  # fixed cost per RCCL collective (launch + handshake), an assumption
+PREFIX_OR_GBS = 5500.0  # the prefix-OR / set passes stream at about this rate
+
+
+def exchange_time_model(world, words=1 << 27, gather=None, cand_max=None, link_gbs=XGMI_LINK_GBS,
+                        alpha_ms=COLLECTIVE_ALPHA_MS):
+    """Predicted time of one batch's exchange per rank (ms), per form, on a
+    fully connected node (one xGMI link to each peer, used in parallel):
+    dense all-to-all form (G >= 3): all_to_all of C, all_to_all of P, all_gather
+    of T -- each link carries one 1/G slice of the 512 MiB bitmap per
+    collective -- plus the prefix-OR over G slices; dense gather form (G <= 2):
+    all_gather of the whole C (each link the whole bitmap); sparse: all_gather
+    of the (count, entries) words and of the candidate lists padded to the
+    longest (cand_max entries).  Bytes over links, not measured (no N > 1
+    node was available to the builder): a check for the driver's 8-GPU run."""
+    G = world
+    if G <= 1:
+        return {"dense": 0.0, "sparse": 0.0 if cand_max is not None else None}
+    gather = (G <= 2) if gather is None else gather
+    bmp = 4 * words
+    if gather:
+        dense = bmp / (link_gbs * 1e6) + alpha_ms + (G * bmp) / (PREFIX_OR_GBS * 1e6)
+    else:
+        dense = 3 * ((bmp / G) / (link_gbs * 1e6) + alpha_ms) + (2 * bmp) / (PREFIX_OR_GBS * 1e6)
+    sparse = None if cand_max is None else 2 * alpha_ms + (4 * cand_max + 16) / (link_gbs * 1e6)
+    return {"dense": dense, "sparse": sparse}
+
+
 class PrefixTriage:
     """fuzzer.go:645-693 over one batch whose call records are split
     contiguously across the ranks of `comm` (rank order = record order), by

@@ -335,3 +335,20 @@ def test_prefix_sparse_exchange_equals_sequential_loop(world, pipelined, gather,
         _run_and_check(world, pipelined, gather, drain, 0.05, exchange, sparse_below, "any")
     else:
         _run_and_check(world, pipelined, gather, drain, 0.05, exchange, sparse_below, expect)
+
+
+def test_exchange_time_model():
+    """The per-rank exchange time model that the C3 line
+    reports as predicted_exchange_ms: no exchange at one rank; the dense
+    all-to-all form moves 3 slices of 512 MiB / G per link (G = 8: ~1.3 ms of
+    link time at 153 GB/s per direction); the gather form the whole bitmap per
+    link; the sparse form only the candidate lists."""
+    from syzkaller_amd.shard import XGMI_LINK_GBS, exchange_time_model
+
+    assert exchange_time_model(1) == {"dense": 0.0, "sparse": None}
+    m8 = exchange_time_model(8, cand_max=100_000)
+    link8 = 3 * (512 << 20) / 8 / (XGMI_LINK_GBS * 1e6)
+    assert link8 < m8["dense"] < link8 + 0.5
+    assert exchange_time_model(2)["dense"] > exchange_time_model(4)["dense"] > m8["dense"]
+    assert exchange_time_model(8, gather=True)["dense"] > m8["dense"]
+    assert m8["sparse"] < 0.2 and exchange_time_model(8, cand_max=10 ** 8)["sparse"] > m8["sparse"]
