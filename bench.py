@@ -125,7 +125,8 @@ UNIVERSE_SEED = 0x5A17C0DE
 POP_SEED = 0x9091A7E5
 
 # kernels of one partitioned triage step (sg_bucket.hip), for the per-kernel table
-STEP_KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan"]
+STEP_KERNELS = ["p1_hist", "p1_scatter", "p2_hist", "p2_scatter", "bucket_triage", "bucket_spill", "scan",
+                "m0_index", "m0_filter", "m0_tail"]
 ORDERED_KERNELS = ["owned_sort", "owned_sweep", "emit"]
 OTHER_KERNELS = ["emit", "shard_local", "shard_route", "shard_owner",
                  "shard_resolve", "shard_flags", "set_add"]
@@ -237,12 +238,14 @@ def step_bytes(a):
     return 4 * a["n_in"] + 4 * a["n_uniq"] + 12 * a["n_cand"] + 4 * a["n_diff"] + a["n_rec"] / 8
 
 
-def pmc_bytes_per_step(kernels, workload):
+def pmc_bytes_per_step(kernels, workload, minor=()):
     """HBM bytes per step of `workload` ("c2", "steady", "from_traces") from the
     PMC summary committed under profiles/ (separate FETCH_SIZE / WRITE_SIZE
     passes over that workload's own timed launches, gfx950-corrected), summed
     over the step's kernels, or None when the summary holds no measurement of
-    this workload or of another kernel set."""
+    this workload or of another kernel set.  `minor`: kernels that ran in the
+    timed steps but under 5 % of their time (the M0 filter's probe of a fresh
+    batch, one record slice in 16), skipped when the summary lacks them."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             d = json.load(f)
@@ -257,7 +260,7 @@ def pmc_bytes_per_step(kernels, workload):
         if k in per and per[k].get("hbm_bytes_per_launch") is not None:
             tot += per[k]["hbm_bytes_per_launch"] * per[k].get("launches_per_step", 1)
             seen.append(k)
-        elif k not in ("scan", "bucket_spill"):  # a summary of another kernel set: stale
+        elif k not in ("scan", "bucket_spill") and k not in minor:  # a summary of another kernel set: stale
             return None, None
     return (tot if seen else None), f"{w.get('tag', d.get('tag'))}/{workload}"
 
@@ -538,7 +541,9 @@ def kernel_table(ctx, names, steps):
 def roofline(acct, step_ms, kernels, workload="c2"):
     b = step_bytes(acct)
     ach = b / (step_ms / 1e3) / 1e9
-    traffic, tag = pmc_bytes_per_step(STEP_KERNELS, workload)
+    ran = [k for k in kernels if k in STEP_KERNELS] or STEP_KERNELS
+    minor = [k for k in ran if kernels.get(k, {}).get("ms_per_step", 0) < 0.05 * step_ms]
+    traffic, tag = pmc_bytes_per_step(ran, workload, minor)
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "scope": "whole triage step (all its kernels, HIP events on the launch stream)",

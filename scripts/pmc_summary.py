@@ -23,7 +23,8 @@ KERNELS = {"p1_hist": ("k_hist_rep<false>", "k_hist_trace", "k_p1_hist"), "p1_sc
            "bucket_spill": ("k_bucket_direct<false>",),
            "count_missing": ("k_count_missing",), "emit_scatter": ("k_scatter(",),
            "bucket_mark": ("k_bucket_mark",), "prefix_or": ("k_prefix_or",), "prefix_flags": ("k_prefix_flags",),
-           "prefix_merge": ("k_prefix_merge",), "set_or": ("k_set_or(",), "set_or_new": ("k_set_or_new(",), "set_or_new_or": ("k_set_or_new_or",)}
+           "prefix_merge": ("k_prefix_merge",), "set_or": ("k_set_or(",), "set_or_new": ("k_set_or_new(",), "set_or_new_or": ("k_set_or_new_or",),
+           "m0_index": ("k_m0_index",), "m0_filter": ("k_m0_filter",), "m0_tail": ("k_m0_tail_insert", "k_m0_tail_flush")}
 
 
 def load(path, counter, nregions):

@@ -1867,6 +1867,289 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
   return SG_OK;
 }
 
+// ------------------------------------------------------------- M0 filter ---
+// The fuzzer's steady state (r06): nearly every entry of a batch is already
+// in maxSignal (fuzzer.go:666 ends most records at the SignalNew test; the
+// bench's steady batch: 139K candidates among 880M entries), yet pass 2 and
+// the bucket stage move every entry.  A random probe of any exact table of
+// maxSignal costs each CU ~10 cycles wherever the table lives (L2, Infinity
+// Cache or HBM; scripts/micro/m0_filter.hip: 55-91 G probes/s), so the test
+// has to be in LDS -- and pass 1 already groups the entries by slice (b2: 2^24
+// signals).  A slice's part of maxSignal is ~50K signals (12.8M / 256): too
+// many for its 2 MiB of bitmap, few enough for a packed index in LDS:
+//   k_m0_index  per slice, one 16-B header per 2^11-signal filter bucket
+//               (8192: 128 KiB): the bucket's count and its first 10 set
+//               positions as 12-bit fields (ascending), or, past 10, a marker,
+//               the first 8 and where the rest start in a small overflow list
+//               (kFOv values per slice; past it, signals are not proven, only
+//               re-checked by the tail); one read of the slice's bitmap;
+//   k_m0_filter per slice part, the slice's index in LDS (136 KiB); every
+//               pass-1 entry reads its bucket's header (one ds_read_b128) and
+//               compares; an entry not found survives, as (position, slice);
+//   tail        if the survivors fit (kFSurvCap): each survivor still outside
+//               maxSignal (the exact bitmap test) gets its record (its pass-1
+//               tile by a search over the slice's run starts) and takes
+//               min(record) per signal in a hash table; then every distinct
+//               signal sets its first owner's flag and its bits in maxSignal
+//               and newSignal -- the bucket stage's results (fuzzer.go:669-690)
+//               over the candidates.
+// When the survivors overflow, pass 2 and the bucket stage run on the same
+// pass-1 output: the filter costs its index and a short pass, and the regime
+// is not tried again for 15 record slices (option m0_filter: -1 auto).
+constexpr uint32_t kFRemBits = 11;                      // positions per filter bucket: 2^11
+constexpr uint32_t kFBuckets = 1u << (24 - kFRemBits);  // 8192 per slice
+constexpr uint32_t kFOv = 4096;                         // overflow values per slice (8 KiB of u16)
+constexpr uint32_t kFSurvCap = 1u << 20;                // survivors per launch
+constexpr uint32_t kFTableBits = 21;                    // the tail's table: 2^21 u64 slots
+constexpr int kFThreads = 1024;
+constexpr uint32_t kFParts = 2;                         // filter workgroups per slice
+constexpr unsigned long long kFEmpty = ~0ull;
+
+struct M0F {
+  uint4* tab;                 // [slice][bucket] headers
+  uint16_t* ovals;            // [slice][kFOv] overflow values
+  uint32_t* cursor;           // [slice] overflow values placed (may pass kFOv)
+  uint32_t* nsurv;            // survivors (may pass kFSurvCap)
+  uint2* surv;                // (position, slice)
+  unsigned long long* table;  // signal << 32 | min record; kFEmpty between launches
+};
+static size_t m0f_bytes() {
+  return 256ull * kFBuckets * 16 + 256ull * kFOv * 2 + 256 * 4 + 256 + (uint64_t)kFSurvCap * 8 +
+         (8ull << kFTableBits);
+}
+static M0F m0f_bind(sg_ctx* ctx) {
+  char* b = (char*)ctx->m0f;
+  M0F f;
+  f.tab = (uint4*)b;
+  b += 256ull * kFBuckets * 16;
+  f.ovals = (uint16_t*)b;
+  b += 256ull * kFOv * 2;
+  f.cursor = (uint32_t*)b;
+  f.nsurv = f.cursor + 256;
+  b += 256 * 4 + 256;
+  f.surv = (uint2*)b;
+  b += (uint64_t)kFSurvCap * 8;
+  f.table = (unsigned long long*)b;
+  return f;
+}
+
+// Header of a filter bucket, as two 64-bit halves: lo bits 0..3 the count n
+// (15: more than 10), fields k = 0..4 at 4 + 12 k; hi fields k = 5..9 at
+// 12 (k - 5).  Past 10 values: fields 0..7, hi bits 36..51 the overflow start,
+// 52..63 how many follow there.
+__device__ __forceinline__ uint32_t m0f_field_bit(uint32_t k) { return k < 5 ? 4 + 12 * k : 64 + 12 * (k - 5); }
+
+// grid (kFBuckets / 256, 256): wave w of block (e, d) indexes filter buckets
+// 256 e + 64 w .. + 63 of slice d; lane l holds word l of each (64 words =
+// 2^11 positions), so a bucket's word loads are one coalesced 256 B.  The
+// wave's 64 headers are assembled in LDS (each set position ORs its field in)
+// and stored as one coalesced 1 KiB.
+__global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ mwords, uint4* __restrict__ tab,
+                                                   uint16_t* __restrict__ ovals, uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t hdr[4][64][4];
+  const uint32_t d = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t j0 = blockIdx.x * 256 + w * 64;
+  const uint32_t* src = mwords + ((uint64_t)d << 19) + ((uint64_t)j0 << 6) + lane;
+  uint32_t wd[64];
+#pragma unroll
+  for (int i = 0; i < 64; i++) wd[i] = src[(uint64_t)i << 6];
+#pragma unroll
+  for (int q = 0; q < 4; q++) hdr[w][lane][q] = 0;
+  uint32_t cl = 0;  // lane i: bucket j0 + i's count
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const uint32_t incl = sgd::wave_incl_add((uint32_t)__popc(wd[i]));
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    cl = lane == (uint32_t)i ? c : cl;
+  }
+  // the overflow lists of the wave's buckets with more than 10 values
+  const uint32_t ov = cl > 10 ? cl - 8 : 0u;
+  const uint32_t oi = sgd::wave_incl_add(ov);
+  const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane((int)oi, 63);
+  uint32_t obase = 0;
+  if (lane == 0 && otot) obase = atomicAdd(&cursor[d], otot);
+  obase = (uint32_t)__builtin_amdgcn_readfirstlane((int)obase);
+  const uint32_t ost = obase + oi - ov;  // lane i: bucket j0 + i's first overflow value
+  __builtin_amdgcn_wave_barrier();
+  uint16_t* out = ovals + (uint64_t)d * kFOv;
+#pragma unroll 4
+  for (int i = 0; i < 64; i++) {
+    uint32_t m = wd[i];
+    const uint32_t p = (uint32_t)__popc(m);
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)cl, i);
+    const uint32_t os = (uint32_t)__builtin_amdgcn_readlane((int)ost, i);
+    const uint32_t kin = n > 10 ? 8u : n;  // values in the header
+    uint32_t k = sgd::wave_incl_add(p) - p;
+    while (m) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t v = (lane << 5) | b;  // the position in the bucket (ascending in k)
+      if (k < kin) {
+        const uint32_t at = m0f_field_bit(k), wi = at >> 5, sh = at & 31;
+        atomicOr(&hdr[w][i][wi], v << sh);
+        if (sh > 20) atomicOr(&hdr[w][i][wi + 1], v >> (32 - sh));
+      } else if (os + (k - 8) < kFOv) {
+        out[os + (k - 8)] = (uint16_t)v;
+      }
+      k++;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  {
+    uint4 h = make_uint4(hdr[w][lane][0], hdr[w][lane][1], hdr[w][lane][2], hdr[w][lane][3]);
+    if (cl > 10) {
+      const uint32_t rem = ost >= kFOv ? 0u : min(cl - 8, kFOv - ost);  // (past kFOv: re-checked by the tail)
+      h.x |= 15u;
+      h.w |= ((ost & 0xFFFFu) << 4) | (rem << 20);  // hi bits 36..51, 52..63
+    } else {
+      h.x |= cl;
+    }
+    tab[(uint64_t)d * kFBuckets + j0 + lane] = h;
+  }
+}
+
+// grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step 8
+// entries, a step's loads in flight while the one before is tested; each entry
+// one header read.  A survivor is written as (position, slice).
+__global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restrict__ v1,
+                                                          const uint32_t* __restrict__ goff1, uint32_t T,
+                                                          const uint4* __restrict__ tab,
+                                                          const uint16_t* __restrict__ ovals,
+                                                          const uint32_t* __restrict__ cursor,
+                                                          uint2* __restrict__ surv, uint32_t* __restrict__ nsurv) {
+  __shared__ uint4 lhdr[kFBuckets];
+  __shared__ uint16_t lov[kFOv];
+  __shared__ uint32_t full;  // some wave saw the survivors overflow (no global polling: one
+                             // counter read by every wave each step measured 12 ms per C2 step)
+  const uint32_t d = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t R0 = goff1[(uint64_t)d * T], R1 = goff1[(uint64_t)(d + 1) * T];
+  const uint64_t len = R1 - R0;
+  const uint32_t a = R0 + (uint32_t)(len * blockIdx.x / gridDim.x), b = R0 + (uint32_t)(len * (blockIdx.x + 1) / gridDim.x);
+  if (a >= b) return;
+  const uint32_t nov = min(cursor[d], kFOv);
+  if (tid == 0) full = 0;
+  for (uint32_t i = tid; i < kFBuckets; i += kFThreads) lhdr[i] = tab[(uint64_t)d * kFBuckets + i];
+  for (uint32_t i = tid; i < nov; i += kFThreads) lov[i] = ovals[(uint64_t)d * kFOv + i];
+  __syncthreads();
+  constexpr int U = 2;  // quads per thread per step
+  constexpr int E = 4 * U;
+  const uint32_t qa = a & ~3u;
+  constexpr uint32_t kStep = 4 * kFThreads * U;
+  uint32_t en[E];
+  auto load = [&](uint32_t q0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t q = q0 + 4 * kFThreads * u;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (q < b) {
+        const v4u32 t = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(v1 + q));
+        x = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      en[4 * u] = x.x;
+      en[4 * u + 1] = x.y;
+      en[4 * u + 2] = x.z;
+      en[4 * u + 3] = x.w;
+    }
+  };
+  load(qa + 4 * tid);
+  for (uint32_t q0 = qa + 4 * tid; q0 < b; q0 += kStep) {
+    uint32_t e[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) e[k] = en[k];
+    load(q0 + kStep);
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+      break;
+    uint4 h[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) h[k] = lhdr[(e[k] >> 8) >> kFRemBits];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const uint32_t p = q0 + 4 * kFThreads * (k >> 2) + (k & 3);
+      const bool live = p >= a && p < b;
+      const uint32_t r = (e[k] >> 8) & ((1u << kFRemBits) - 1);
+      const uint64_t lo = ((uint64_t)h[k].y << 32) | h[k].x, hi = ((uint64_t)h[k].w << 32) | h[k].z;
+      const uint32_t n4 = h[k].x & 15u, nh = n4 == 15u ? 8u : n4;
+      bool hit = false;
+#pragma unroll
+      for (uint32_t f = 0; f < 10; f++) {
+        const uint32_t v = (uint32_t)((f < 5 ? lo >> (4 + 12 * f) : hi >> (12 * (f - 5))) & 0xFFFu);
+        hit |= v == r && f < nh;
+      }
+      if (!hit && n4 == 15u) {  // the rest, in the overflow list (sorted)
+        uint32_t o = (uint32_t)(hi >> 36) & 0xFFFFu, m = (uint32_t)(hi >> 52);
+        const uint32_t end = o + m;
+        while (m) {
+          const uint32_t hf = m >> 1;
+          if (lov[o + hf] < r) {
+            o += hf + 1;
+            m -= hf + 1;
+          } else {
+            m = hf;
+          }
+        }
+        hit = o < end && lov[o] == r;
+      }
+      const bool sv = live && !hit;
+      const uint64_t bal = __ballot(sv);
+      if (!bal) continue;
+      const int first = __builtin_ctzll(bal);
+      uint32_t at = 0;
+      if (lane == (uint32_t)first) at = atomicAdd(nsurv, (uint32_t)__popcll(bal));
+      at = (uint32_t)__shfl((int)at, first);
+      if (at >= kFSurvCap && lane == (uint32_t)first)
+        __hip_atomic_store(&full, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      at += (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+      if (sv && at < kFSurvCap) surv[at] = make_uint2(p, d);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t m0f_hash(uint32_t s) {
+  s ^= s >> 16;
+  s *= 0x7FEB352Du;
+  s ^= s >> 15;
+  return s;
+}
+
+// the survivors still outside maxSignal (a value past an index cap is only
+// re-checked here): each one's record (its pass-1 tile by a search over the
+// slice's run starts), then min(record) per signal
+__global__ void k_m0_tail_insert(const uint2* __restrict__ surv, uint32_t n, const uint32_t* __restrict__ v1,
+                                 const uint32_t* __restrict__ goff1, uint32_t T, const uint32_t* __restrict__ trec,
+                                 const uint32_t* __restrict__ mwords, unsigned long long* __restrict__ table) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint2 q = surv[i];  // (position, slice)
+  const uint32_t e = v1[q.x], t = (q.y << 24) | (e >> 8);
+  if ((mwords[t >> 5] >> (t & 31)) & 1u) return;
+  const uint32_t s = part_sig(t);
+  const uint32_t rec = trec[last_le(goff1 + (uint64_t)q.y * T, 0, T, q.x)] + (e & 0xFFu);
+  const unsigned long long key = ((unsigned long long)s << 32) | rec;
+  constexpr uint32_t mask = (1u << kFTableBits) - 1;
+  for (uint32_t h = m0f_hash(s) & mask;; h = (h + 1) & mask) {
+    const unsigned long long old = atomicCAS(&table[h], kFEmpty, key);
+    if (old == kFEmpty) return;
+    if ((uint32_t)(old >> 32) == s) {
+      if (old > key) atomicMin(&table[h], key);
+      return;
+    }
+  }
+}
+
+// every distinct new signal: its first owner queued, its bits set (and the
+// slot emptied for the next launch)
+__global__ void k_m0_tail_flush(unsigned long long* __restrict__ table, uint32_t* __restrict__ mwords,
+                                uint32_t* __restrict__ nwords, uint8_t* __restrict__ rec_new) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long v = table[i];
+  if (v == kFEmpty) return;
+  table[i] = kFEmpty;
+  rec_new[(uint32_t)v] = 1;
+  const uint32_t t = part_key((uint32_t)(v >> 32)), bit = 1u << (t & 31);
+  atomicOr(&mwords[t >> 5], bit);
+  if (nwords) atomicOr(&nwords[t >> 5], bit);
+}
+
 // ------------------------------------------------------------------ host ---
 struct BucketPlan {
   uint64_t n, nrec, nA, nB, T, NG, ng, gmax;
@@ -1941,19 +2224,24 @@ uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
 // Stage A of one partitioned launch: tiles, both partition passes, the
 // bucket descriptors and the list of non-empty buckets, in the workspace from
 // ws_base (reserved by the caller when `reserved`).  n > 0, nrec > 0.
+// stages: 1 the tiles and pass 1 (then bp is rebased), 2 the rest (after a
+// stage-1 call with the same bp), 3 both.
 static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n, uint64_t nrec,
-                         size_t ws_base, bool reserved, BucketPlan& bp, bool trace = false) {
-  if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
-    set_error("bucket triage: batch too large");
-    return SG_EINVAL;
+                         size_t ws_base, bool reserved, BucketPlan& bp, bool trace = false, int stages = 3) {
+  int rc = SG_OK;
+  if (stages & 1) {
+    if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
+      set_error("bucket triage: batch too large");
+      return SG_EINVAL;
+    }
+    rc = reserved ? SG_OK : ws_reserve(ctx, ws_base + bp.p.total);
+    if (rc) return rc;
+    if (ctx->ws_cap < ws_base + bp.p.total) {
+      set_error("bucket triage: workspace not reserved");
+      return SG_EINVAL;
+    }
+    bp.rebase(ws_base);
   }
-  int rc = reserved ? SG_OK : ws_reserve(ctx, ws_base + bp.p.total);
-  if (rc) return rc;
-  if (ctx->ws_cap < ws_base + bp.p.total) {
-    set_error("bucket triage: workspace not reserved");
-    return SG_EINVAL;
-  }
-  bp.rebase(ws_base);
   uint32_t* tstart = (uint32_t*)ws_at(ctx, bp.oTS);
   uint32_t* trec = (uint32_t*)ws_at(ctx, bp.oTR);
   uint32_t* gt = (uint32_t*)ws_at(ctx, bp.oGT);
@@ -1976,7 +2264,8 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
     uint32_t* scr = (uint32_t*)ws_at(ctx, bp.oSC);
   const uint32_t T = (uint32_t)bp.T, G = (uint32_t)bp.gmax, NG = (uint32_t)bp.NG;
   const uint32_t* gcount = cbase + bp.ng;  // device: number of pass-2 chunks
-
+  const bool dbg = ctx->debug_part;
+  if (stages & 1) {
   // pass-1 tiles
   Cuts c1{};
   c1.nA = bp.nA;
@@ -2005,7 +2294,6 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
   P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, b1, nullptr, (const uint64_t*)ws_at(ctx, bp.oKM)};
-  const bool dbg = ctx->debug_part;
   unsigned long long* p1dbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&p1dbg, 64));
@@ -2031,6 +2319,8 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
             "write %.0f (tiles %llu)\n", (double)h[0] / h[5], (double)h[1] / h[5], (double)h[2] / h[5],
             (double)h[3] / h[5], (double)h[4] / h[5], h[5]);
   }
+  }
+  if (!(stages & 2)) return SG_OK;
   // pass-2 chunks
   hipLaunchKernelGGL(k_group_chunks, dim3(div_up(bp.ng, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)goff1,
                      T, NG, (const uint32_t*)gt, bp.ng, nch);
@@ -2194,6 +2484,69 @@ static int buckets_one(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint
 // flagging records and updating the sets (mwords is then only read).  The
 // launch's scratch starts at workspace offset ws_base (reserved by the caller
 // when ws_base != 0).
+// The M0 filter on stage 1's output (bp rebased): *done when its tail has
+// produced the flags and set updates; otherwise the survivors overflowed and
+// the caller goes on with stage 2 and the bucket stage (nothing written yet).
+static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32_t* nwords, uint8_t* d_rec_new,
+                     bool* done) {
+  *done = false;
+  if (!ctx->m0f) {
+    SG_HIP(hipMalloc(&ctx->m0f, m0f_bytes()));
+    const M0F f0 = m0f_bind(ctx);
+    SG_HIP(hipMemsetAsync(f0.table, 0xFF, 8ull << kFTableBits, ctx->stream));
+  }
+  const M0F f = m0f_bind(ctx);
+  const uint32_t T = (uint32_t)bp.T;
+  SG_HIP(hipMemsetAsync(f.cursor, 0, 256 * 4 + 4, ctx->stream));  // cursors and the survivor count
+  {
+    ScopedTimer tm(ctx, "m0_index");
+    hipLaunchKernelGGL(k_m0_index, dim3(kFBuckets / 256, 256), dim3(256), 0, ctx->stream, (const uint32_t*)mwords,
+                       f.tab, f.ovals, f.cursor);
+  }
+  {
+    ScopedTimer tm(ctx, "m0_filter");
+    hipLaunchKernelGGL(k_m0_filter, dim3(kFParts, 256), dim3(kFThreads), 0, ctx->stream,
+                       (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
+                       (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor, f.surv, f.nsurv);
+  }
+  SG_HIP(hipGetLastError());
+  // (the host ingest's pinned staging may be in a DMA now: a pageable read)
+  uint32_t ns = 0;
+  SG_HIP(hipMemcpyAsync(&ns, f.nsurv, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->m0f_survivors = ns;
+  if (ns > kFSurvCap) {
+    ctx->m0f_fallback++;
+    if (ctx->opt[kOptM0Filter] < 0) ctx->m0f_skip = 15;
+    return SG_OK;
+  }
+  if (ns) {
+    ScopedTimer tm(ctx, "m0_tail");
+    hipLaunchKernelGGL(k_m0_tail_insert, dim3(div_up(ns, 256)), dim3(256), 0, ctx->stream, (const uint2*)f.surv, ns,
+                       (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
+                       (const uint32_t*)ws_at(ctx, bp.oTR), (const uint32_t*)mwords, f.table);
+    hipLaunchKernelGGL(k_m0_tail_flush, dim3((1u << kFTableBits) / 256), dim3(256), 0, ctx->stream, f.table, mwords,
+                       nwords, d_rec_new);
+  }
+  SG_HIP(hipGetLastError());
+  ctx->m0f_used++;
+  *done = true;
+  return SG_OK;
+}
+
+// The M0 filter's regime: option m0_filter 1 always tries it, 0 never; auto
+// tries it unless a recent record slice overflowed it (15 slices are skipped
+// then, so a run of fresh batches pays it on one slice in 16).
+static bool m0f_try(sg_ctx* ctx) {
+  const int64_t o = ctx->opt[kOptM0Filter];
+  if (o >= 0) return o != 0;
+  if (ctx->m0f_skip) {
+    ctx->m0f_skip--;
+    return false;
+  }
+  return true;
+}
+
 static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
                              const uint64_t* d_off, uint64_t n, uint64_t nrec, uint8_t* d_rec_new,
                              const EmitArgs* emit = nullptr, size_t ws_base = 0, bool trace = false) {
@@ -2203,9 +2556,20 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
     return SG_EINVAL;
   }
   BucketPlan bp(n, nrec);
-  int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp, trace);
+  if (emit || ws_base || !m0f_try(ctx)) {
+    int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp, trace);
+    if (rc) return rc;
+    return buckets_one(ctx, bp, mwords, nwords, d_rec_new, emit, n, nrec);
+  }
+  // the flags path with the M0 filter between the two partition passes
+  int rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 1);
   if (rc) return rc;
-  return buckets_one(ctx, bp, mwords, nwords, d_rec_new, emit, n, nrec);
+  bool done = false;
+  rc = m0_filter(ctx, bp, mwords, nwords, d_rec_new, &done);
+  if (rc || done) return rc;
+  rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 2);
+  if (rc) return rc;
+  return buckets_one(ctx, bp, mwords, nwords, d_rec_new, nullptr, n, nrec);
 }
 
 // Marks: nwords |= every signal of stage A's buckets that is not in mwords

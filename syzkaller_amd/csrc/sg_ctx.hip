@@ -539,6 +539,7 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);
+  if (ctx->m0f) hipFree(ctx->m0f);
   if (ctx->slice_off) hipFree(ctx->slice_off);
   if (ctx->slice_cuts) hipFree(ctx->slice_cuts);
   if (ctx->dscal) hipFree(ctx->dscal);
@@ -626,7 +627,8 @@ int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag) {
 
 static const char* const kOptNames[kOptCount] = {
     "bucket_blocks",      "prefix_pairs",       "fold_map",         "minimize_filter",   "minimize_filter_ranks",
-    "report_direct",      "rpc_encode_elems",   "rpc_decode_blocks", "host_slice",       "host_copy_threads"};
+    "report_direct",      "rpc_encode_elems",   "rpc_decode_blocks", "host_slice",       "host_copy_threads",
+    "m0_filter"};
 
 int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return SG_EINVAL;
@@ -708,6 +710,12 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
     *out = ctx->host_wait_ns;
   else if (!strcmp(name, "host_copy_threads"))
     *out = ctx->host_threads;
+  else if (!strcmp(name, "m0_filter_used"))  // record slices the M0 filter finished (sg_bucket.hip)
+    *out = ctx->m0f_used;
+  else if (!strcmp(name, "m0_filter_fallback"))  // ... and those whose survivors overflowed (the partition went on)
+    *out = ctx->m0f_fallback;
+  else if (!strcmp(name, "m0_filter_survivors"))  // survivors of the last filtered slice
+    *out = ctx->m0f_survivors;
   else if (!strcmp(name, "cpu_quota_milli"))
     *out = (uint64_t)(ctx->cpu_quota * 1000.0 + 0.5);
   else {

@@ -92,12 +92,19 @@ enum SgOpt : int {
   kOptRpcDecodeBlocks,      // delta decode: -1 by shape, 0 per-list, 1 per-block
   kOptHostSlice,            // host ingest: entries per record slice (0: the default)
   kOptHostCopyThreads,      // host ingest: pageable -> pinned copy threads (0: from the CPU quota)
+  kOptM0Filter,             // flags path: the M0 filter (sg_bucket.hip): -1 by the last batches, 0 never, 1 always tried
   kOptCount
 };
 
 struct sg_ctx {
   int device = 0;
-  int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0};
+  int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0, -1};
+  // the M0 filter's buffers (lazy, sg_bucket.hip) and its regime state: the
+  // batches left to skip after a batch whose survivors overflowed; batches
+  // it filtered and fell back on (counters)
+  void* m0f = nullptr;
+  uint32_t m0f_skip = 0;
+  uint64_t m0f_used = 0, m0f_fallback = 0, m0f_survivors = 0;
   // host CPUs this process may use (cgroup cpu.max quota, else the affinity
   // mask), read at creation: sizes the host ingest's copy threads
   double cpu_quota = 0;

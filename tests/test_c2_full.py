@@ -87,26 +87,33 @@ def test_c2_full_batch_steady_state_vs_oracle(ctx):
     del trace
     nvals, nrec = sig.numel(), off.numel() - 1
     assert nrec == nprog * calls and nvals > 800_000_000  # the C2 shape
-    ms, ns = SignalSet(ctx), SignalSet(ctx)
-    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernel has read it)
-    call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
-    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
-    call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
-         None, None)
-    torch.cuda.synchronize()
-    got = rec_new.cpu().numpy()
     # the oracle's sequential loop over the same batch
     om, on = O.OSet(m0), O.OSet()
     exp, ev, eo = O.triage_batch(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))
     frac = float(exp.mean())
     assert 0.05 < frac < 0.95, frac  # mixed flags: the attribution is really tested
-    assert np.array_equal(got, exp)
     em, en = om.export(), on.export()
     del om, on
-    assert np.array_equal(ns.export(), en)
-    assert np.array_equal(ms.export(), em)
-    ns.close()
-    ms.close()
+    # the flags path with the M0 filter forced (its tail makes the results:
+    # ~139K survivors), in its auto regime (which takes it here), and without it
+    dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernels have read it)
+    rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    for mode in (1, -1, 0):
+        ctx.set_option("m0_filter", mode)
+        used = ctx.counter("m0_filter_used")
+        ms, ns = SignalSet(ctx), SignalSet(ctx)
+        call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
+        call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
+             None, None)
+        torch.cuda.synchronize()
+        assert (ctx.counter("m0_filter_used") > used) == (mode != 0), mode
+        assert np.array_equal(rec_new.cpu().numpy(), exp), mode
+        assert np.array_equal(ns.export(), en), mode
+        assert np.array_equal(ms.export(), em), mode
+        ns.close()
+        ms.close()
+    ctx.set_option("m0_filter", -1)
+    del dm0
     _diff_path(call, ctx, m0, sig, off, exp, ev, eo, em, en)
     call("sg_ctx_reset_stream", ctx.h)
 
@@ -142,9 +149,15 @@ def test_c2_full_fresh_batch_sets_vs_oracle(ctx):
     dm0 = torch.from_numpy(m0.view(np.int32)).cuda()  # (held until the kernel has read it)
     call("sg_set_add_dev", ms.h, dm0.data_ptr(), m0.size)
     rec_new = torch.zeros(nrec, dtype=torch.uint8, device="cuda")
+    # the M0 filter forced: its survivors (~326M) overflow, and pass 2 and the
+    # bucket stage go on from the same pass-1 output
+    ctx.set_option("m0_filter", 1)
+    fb = ctx.counter("m0_filter_fallback")
     call("sg_triage_batch_dev", ctx.h, ms.h, ns.h, sig.data_ptr(), off.data_ptr(), nvals, nrec, rec_new.data_ptr(),
          None, None)
     torch.cuda.synchronize()
+    ctx.set_option("m0_filter", -1)
+    assert ctx.counter("m0_filter_fallback") == fb + 1
     got = rec_new.cpu().numpy()
     om, on = O.OSet(m0), O.OSet()
     exp, ev, eo = O.triage_batch(om, on, sig.cpu().numpy().view(np.uint32), off.cpu().numpy().view(np.uint64))

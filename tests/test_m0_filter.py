@@ -1,0 +1,159 @@
+"""The M0 filter (sg_bucket.hip k_m0_index / k_m0_filter and the tail): the
+flags path's regime for low-novelty batches, between the two partition
+passes.  Forced on (context option m0_filter 1) every batch must give the
+sequential loop's flags, maxSignal and newSignal (syz-fuzzer/fuzzer.go:645-693,
+oracle/sigoracle.c) -- through the filter's own tail when the survivors fit,
+through pass 2 and the bucket stage when they overflow -- and auto must pick
+the regime from the last slices.  The edge cases are the filter's own: no
+survivors, every entry a survivor, a slice holding more maxSignal signals than
+its LDS index (kFCap: the rest are re-checked against the bitmap), signals 0
+and 0xFFFFFFFF, repeats of a new signal across records (first owner), record
+slices, and raw traces (the set-exact trace path runs the same filter)."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+SENT = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def C(ctx):
+    from syzkaller_amd import cover
+
+    return cover
+
+
+def _batch(rng, nrec, m0, novelty, maxlen=60, hi=1 << 32):
+    lens = rng.integers(0, maxlen, size=nrec)
+    lens[rng.integers(0, nrec, size=nrec // 6)] = 0
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    n = int(off[-1])
+    vals = m0[rng.integers(0, m0.size, size=n)] if m0.size else np.zeros(n, np.uint32)
+    fresh = rng.random(n) < novelty
+    vals[fresh] = rng.integers(0, hi, size=int(fresh.sum()), dtype=np.uint64).astype(np.uint32)
+    return vals.astype(np.uint32), off
+
+
+def _check(C, ctx, m0, vals, off, mode, expect):
+    """One batch through sg_triage_batch with option m0_filter = mode against
+    the oracle; expect: "used" (the filter's tail produced the results),
+    "fallback" (its survivors overflowed), "skip" (not tried), None (any)."""
+    ctx.set_option("m0_filter", mode)
+    u0, f0 = ctx.counter("m0_filter_used"), ctx.counter("m0_filter_fallback")
+    ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
+    if m0.size:
+        C.SignalAdd(ms, m0)
+    got, _, _ = C.triage_batch(ms, ns, vals, off, want_diff=False, ctx=ctx)
+    du, df = ctx.counter("m0_filter_used") - u0, ctx.counter("m0_filter_fallback") - f0
+    om, on = O.OSet(m0), O.OSet()
+    exp = O.triage_flags_only(om, on, vals, off)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(ms.export(), om.export())
+    assert np.array_equal(ns.export(), on.export())
+    ms.close()
+    ns.close()
+    if expect == "used":
+        assert du >= 1 and df == 0, (du, df)
+    elif expect == "fallback":
+        assert df >= 1 and du == 0, (du, df)
+    elif expect == "skip":
+        assert du == 0 and df == 0, (du, df)
+    return exp
+
+
+def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option):
+    ctx_option(ctx, "m0_filter", 1)
+    rng = np.random.default_rng(6001)
+    m0 = np.unique(rng.integers(0, 1 << 32, size=300_000, dtype=np.uint64).astype(np.uint32))
+    m0 = np.unique(np.concatenate([m0, np.array([0, SENT], np.uint32)]))
+    for nov in (1e-3, 0.0, 0.02):  # low novelty, no survivor at all, more of them
+        vals, off = _batch(rng, 20_000, m0, nov)
+        vals[:5] = [0, SENT, 0, SENT, m0[7]]
+        exp = _check(C, ctx, m0, vals, off, 1, "used")
+        assert (exp.sum() == 0) == (nov == 0.0)
+    # a new signal repeated over many records: its first owner only
+    vals, off = _batch(rng, 5_000, m0, 0.0)
+    rep = np.uint32(0x12345679)
+    assert rep not in set(m0.tolist())
+    vals[rng.integers(0, vals.size, size=200)] = rep
+    _check(C, ctx, m0, vals, off, 1, "used")
+    # empty maxSignal: every entry survives (fewer than the cap)
+    vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0, hi=1 << 20)
+    _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "used")
+    # empty records only / a batch without entries
+    _check(C, ctx, m0, np.zeros(0, np.uint32), np.zeros(9, np.uint64), 1, None)
+
+
+def test_m0_filter_index_cap_and_overflow(C, ctx, ctx_option):
+    """A pass-1 slice holding 100K maxSignal signals (past the index's 61,440):
+    the bucket prefixes past the cap leave signals unproven, which the tail
+    re-checks against the bitmap; and a fresh batch whose survivors overflow
+    the 2^20 cap goes on through pass 2 and the bucket stage."""
+    ctx_option(ctx, "m0_filter", 1)
+    rng = np.random.default_rng(6002)
+    # signals of pass-1 slice 5: b2 (bits 16..23) = 5
+    low = rng.choice(1 << 24, size=100_000, replace=False).astype(np.uint64)
+    dense = np.unique(((low >> np.uint64(16)) << np.uint64(24)) | (np.uint64(5) << np.uint64(16))
+                      | (low & np.uint64(0xFFFF))).astype(np.uint32)
+    other = np.unique(rng.integers(0, 1 << 32, size=50_000, dtype=np.uint64).astype(np.uint32))
+    m0 = np.unique(np.concatenate([dense, other]))
+    vals, off = _batch(rng, 30_000, m0, 1e-3)
+    _check(C, ctx, m0, vals, off, 1, "used")
+    # fresh: ~1.6M survivors > the cap
+    vals, off = _batch(rng, 50_000, m0, 1.0, maxlen=80)
+    assert vals.size > (1 << 20) + 200_000
+    _check(C, ctx, m0, vals, off, 1, "fallback")
+
+
+def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
+    """auto: a batch whose survivors overflow turns the filter off for the
+    next 15 record slices, then it is tried again; record slices (a lowered
+    per-launch record limit) are filtered one by one, each against the
+    maxSignal the slices before it left."""
+    ctx = C.Context(0)
+    try:
+        rng = np.random.default_rng(6003)
+        m0 = np.unique(rng.integers(0, 1 << 32, size=200_000, dtype=np.uint64).astype(np.uint32))
+        vals, off = _batch(rng, 12_000, m0, 2e-3)
+        ctx.set_option("max_launch_records", 1000)  # 12 slices
+        _check(C, ctx, m0, vals, off, 1, "used")
+        assert ctx.counter("m0_filter_used") >= 12
+        ctx.set_option("max_launch_records", 0)
+        fresh, foff = _batch(rng, 50_000, m0, 1.0, maxlen=80)
+        _check(C, ctx, m0, fresh, foff, -1, "fallback")
+        for _ in range(15):  # skipped while the regime says fresh
+            _check(C, ctx, m0, vals, off, -1, "skip")
+        _check(C, ctx, m0, vals, off, -1, "used")
+        _check(C, ctx, m0, vals, off, 0, "skip")  # never
+    finally:
+        ctx.close()
+
+
+def test_m0_filter_traces(C, ctx, ctx_option):
+    """The set-exact trace path (sg_triage_traces: the edge signal computed in
+    pass 1's loads) through the filter, against the oracle's executor signal
+    and loop."""
+    ctx_option(ctx, "m0_filter", 1)
+    rng = np.random.default_rng(6004)
+    ncalls = 6000
+    lens = rng.integers(0, 200, size=ncalls)
+    call_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    pcs = (0x81000000 + 16 * (np.minimum(rng.zipf(1.1, size=int(call_off[-1])), 1 << 14) - 1)).astype(np.uint32)
+    prog_off = np.arange(ncalls + 1, dtype=np.uint64)
+    sig, soff = O.exec_signal(pcs, call_off, prog_off)
+    m0 = np.unique(sig[: int(soff[ncalls * 9 // 10])])  # most of the batch's edges already known
+    om, on = O.OSet(m0), O.OSet()
+    exp = O.triage_flags_only(om, on, sig, soff)
+    u0 = ctx.counter("m0_filter_used")
+    ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
+    C.SignalAdd(ms, m0)
+    got = C.triage_traces(ms, ns, pcs, call_off, ctx=ctx)
+    assert ctx.counter("m0_filter_used") > u0
+    assert 0 < exp.sum() < ncalls
+    assert np.array_equal(got, exp)
+    assert np.array_equal(ms.export(), om.export()) and np.array_equal(ns.export(), on.export())
+    ms.close()
+    ns.close()
