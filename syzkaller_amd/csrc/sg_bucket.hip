@@ -1898,24 +1898,33 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 // is not tried again for 15 record slices (option m0_filter: -1 auto).
 constexpr uint32_t kFRemBits = 11;                      // positions per filter bucket: 2^11
 constexpr uint32_t kFBuckets = 1u << (24 - kFRemBits);  // 8192 per slice
-constexpr uint32_t kFOv = 4096;                         // overflow values per slice (8 KiB of u16)
+constexpr uint32_t kFOv = 8192;                         // overflow values per slice (16 KiB of u16, 8-value blocks)
 constexpr uint32_t kFSurvCap = 1u << 20;                // survivors per launch
 constexpr uint32_t kFTableBits = 21;                    // the tail's table: 2^21 u64 slots
 constexpr int kFThreads = 1024;
-constexpr uint32_t kFParts = 2;                         // filter workgroups per slice
+#ifndef SG_FPARTS
+#define SG_FPARTS 2
+#endif
+#ifndef SG_FABL
+#define SG_FABL 0  // diagnostics builds: 1 the entry stream only, 2 and the header reads (wrong results)
+#endif
+constexpr uint32_t kFParts = SG_FPARTS;                 // filter workgroups per slice
+constexpr uint32_t kFWgCap = 4 * kFSurvCap / (256 * kFParts);  // survivors per filter workgroup (its own region:
+                                                              // 4x the mean share at the cap, 32 MiB in all)
 constexpr unsigned long long kFEmpty = ~0ull;
 
 struct M0F {
   uint4* tab;                 // [slice][bucket] headers
   uint16_t* ovals;            // [slice][kFOv] overflow values
   uint32_t* cursor;           // [slice] overflow values placed (may pass kFOv)
-  uint32_t* nsurv;            // survivors (may pass kFSurvCap)
-  uint2* surv;                // (position, slice)
+  uint32_t* nsurv;            // survivors; kFSurvCap + 1 when a workgroup's region overflowed
+  uint2* surv;                // (position, slice), kFWgCap per filter workgroup
+  uint32_t* wgcnt;            // [filter workgroup] survivors in its region
   unsigned long long* table;  // signal << 32 | min record; kFEmpty between launches
 };
 static size_t m0f_bytes() {
-  return 256ull * kFBuckets * 16 + 256ull * kFOv * 2 + 256 * 4 + 256 + (uint64_t)kFSurvCap * 8 +
-         (8ull << kFTableBits);
+  return 256ull * kFBuckets * 16 + 256ull * kFOv * 2 + 256 * 4 + 256 + 256ull * kFParts * kFWgCap * 8 +
+         256ull * kFParts * 4 + (8ull << kFTableBits);
 }
 static M0F m0f_bind(sg_ctx* ctx) {
   char* b = (char*)ctx->m0f;
@@ -1928,179 +1937,244 @@ static M0F m0f_bind(sg_ctx* ctx) {
   f.nsurv = f.cursor + 256;
   b += 256 * 4 + 256;
   f.surv = (uint2*)b;
-  b += (uint64_t)kFSurvCap * 8;
+  b += 256ull * kFParts * kFWgCap * 8;
+  f.wgcnt = (uint32_t*)b;
+  b += 256ull * kFParts * 4;
   f.table = (unsigned long long*)b;
   return f;
 }
 
 // Header of a filter bucket, as two 64-bit halves: lo bits 0..3 the count n
 // (15: more than 10), fields k = 0..4 at 4 + 12 k; hi fields k = 5..9 at
-// 12 (k - 5).  Past 10 values: fields 0..7, hi bits 36..51 the overflow start,
-// 52..63 how many follow there.
+// 12 (k - 5); unused fields hold 0xFFF (no position is), so a lookup compares
+// all ten at once.  Past 10 values: fields 0..7, hi bits 36..51 the overflow
+// list's first 8-value block, 52..63 how many values follow there; the list
+// is whole 16-B blocks of u16, padded with 0xFFFF.
 __device__ __forceinline__ uint32_t m0f_field_bit(uint32_t k) { return k < 5 ? 4 + 12 * k : 64 + 12 * (k - 5); }
 
-// grid (kFBuckets / 256, 256): wave w of block (e, d) indexes filter buckets
-// 256 e + 64 w .. + 63 of slice d; lane l holds word l of each (64 words =
-// 2^11 positions), so a bucket's word loads are one coalesced 256 B.  The
-// wave's 64 headers are assembled in LDS (each set position ORs its field in)
-// and stored as one coalesced 1 KiB.
+// does one of the 12-bit fields in bits 0..59 of t equal r?  (SWAR: a field
+// of t ^ r...r is zero exactly where it matches; the borrow trick finds one)
+__device__ __forceinline__ uint64_t m0f_has12(uint64_t t, uint64_t rep) {  // rep = r in each 12-bit field
+  constexpr uint64_t kOnes = 0x001001001001001ull, kHigh = 0x800800800800800ull;
+  const uint64_t x = t ^ rep;
+  return (x - kOnes) & ~x & kHigh;  // non-zero iff some field equals r
+}
+__device__ __forceinline__ uint64_t m0f_has16(uint64_t t, uint64_t rep) {  // four 16-bit fields
+  constexpr uint64_t kOnes = 0x0001000100010001ull, kHigh = 0x8000800080008000ull;
+  const uint64_t x = t ^ rep;
+  return (x - kOnes) & ~x & kHigh;
+}
+
+// grid (kFBuckets / 256, 256): thread t of block (e, d) indexes filter
+// bucket 256 e + t of slice d, its 64 bitmap words (256 B) read as 16 quads;
+// it walks their set bits in order into its header's fields and its overflow
+// list, whose blocks one cursor add per wave places.  (A wave per 64 buckets,
+// lane l holding word l of each, measured 0.40-0.45 ms per steady step: 128
+// wave scans per 64 buckets.)
 __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ mwords, uint4* __restrict__ tab,
                                                    uint16_t* __restrict__ ovals, uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t hdr[4][64][4];
-  const uint32_t d = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t j0 = blockIdx.x * 256 + w * 64;
-  const uint32_t* src = mwords + ((uint64_t)d << 19) + ((uint64_t)j0 << 6) + lane;
-  uint32_t wd[64];
+  const uint32_t d = blockIdx.y, lane = threadIdx.x & 63;
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(mwords + ((uint64_t)d << 19) + ((uint64_t)j << 6));
+  uint4 q[16];
 #pragma unroll
-  for (int i = 0; i < 64; i++) wd[i] = src[(uint64_t)i << 6];
+  for (int i = 0; i < 16; i++) q[i] = src[i];
+  uint32_t n = 0;
 #pragma unroll
-  for (int q = 0; q < 4; q++) hdr[w][lane][q] = 0;
-  uint32_t cl = 0;  // lane i: bucket j0 + i's count
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    const uint32_t incl = sgd::wave_incl_add((uint32_t)__popc(wd[i]));
-    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    cl = lane == (uint32_t)i ? c : cl;
-  }
-  // the overflow lists of the wave's buckets with more than 10 values
-  const uint32_t ov = cl > 10 ? cl - 8 : 0u;
-  const uint32_t oi = sgd::wave_incl_add(ov);
+  for (int i = 0; i < 16; i++) n += __popc(q[i].x) + __popc(q[i].y) + __popc(q[i].z) + __popc(q[i].w);
+  // the overflow list (whole 8-value blocks) of a bucket past 10 values
+  const uint32_t ob = n > 10 ? (n - 8 + 7) >> 3 : 0u;
+  const uint32_t oi = sgd::wave_incl_add(ob);
   const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane((int)oi, 63);
   uint32_t obase = 0;
   if (lane == 0 && otot) obase = atomicAdd(&cursor[d], otot);
   obase = (uint32_t)__builtin_amdgcn_readfirstlane((int)obase);
-  const uint32_t ost = obase + oi - ov;  // lane i: bucket j0 + i's first overflow value
-  __builtin_amdgcn_wave_barrier();
-  uint16_t* out = ovals + (uint64_t)d * kFOv;
-#pragma unroll 4
-  for (int i = 0; i < 64; i++) {
-    uint32_t m = wd[i];
-    const uint32_t p = (uint32_t)__popc(m);
-    const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)cl, i);
-    const uint32_t os = (uint32_t)__builtin_amdgcn_readlane((int)ost, i);
-    const uint32_t kin = n > 10 ? 8u : n;  // values in the header
-    uint32_t k = sgd::wave_incl_add(p) - p;
-    while (m) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m);
-      m &= m - 1;
-      const uint32_t v = (lane << 5) | b;  // the position in the bucket (ascending in k)
-      if (k < kin) {
-        const uint32_t at = m0f_field_bit(k), wi = at >> 5, sh = at & 31;
-        atomicOr(&hdr[w][i][wi], v << sh);
-        if (sh > 20) atomicOr(&hdr[w][i][wi + 1], v >> (32 - sh));
-      } else if (os + (k - 8) < kFOv) {
-        out[os + (k - 8)] = (uint16_t)v;
+  const uint32_t ost = 1 + obase + oi - ob;  // first block (block 0: none, the filter's dummy)
+  constexpr uint32_t kOvBlocks = kFOv / 8;
+  const bool ok = ob && ost + ob <= kOvBlocks;  // (else the list is dropped: the tail re-checks)
+  uint16_t* out = ovals + (uint64_t)d * kFOv + 8 * (uint64_t)ost;
+  const uint32_t kin = n > 10 ? 8u : n;  // values in the header
+  uint64_t lo = 0, hi = 0;
+  uint32_t k = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t wq[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      uint32_t m = wq[c];
+      while (m) {
+        const uint32_t v = (uint32_t)(32 * (4 * i + c)) + (uint32_t)__builtin_ctz(m);  // ascending in k
+        m &= m - 1;
+        if (k < kin) {
+          const uint32_t at = m0f_field_bit(k);
+          if (at < 64)
+            lo |= (uint64_t)v << at;
+          else
+            hi |= (uint64_t)v << (at - 64);
+        } else if (ok) {
+          out[k - 8] = (uint16_t)v;
+        }
+        k++;
       }
-      k++;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  {
-    uint4 h = make_uint4(hdr[w][lane][0], hdr[w][lane][1], hdr[w][lane][2], hdr[w][lane][3]);
-    if (cl > 10) {
-      const uint32_t rem = ost >= kFOv ? 0u : min(cl - 8, kFOv - ost);  // (past kFOv: re-checked by the tail)
-      h.x |= 15u;
-      h.w |= ((ost & 0xFFFFu) << 4) | (rem << 20);  // hi bits 36..51, 52..63
-    } else {
-      h.x |= cl;
-    }
-    tab[(uint64_t)d * kFBuckets + j0 + lane] = h;
+  for (uint32_t f = kin; f < (n > 10 ? 8u : 10u); f++) {  // unused fields: 0xFFF
+    const uint32_t at = m0f_field_bit(f);
+    if (at < 64)
+      lo |= 0xFFFull << at;
+    else
+      hi |= 0xFFFull << (at - 64);
   }
+  if (n > 10) {
+    if (ok)
+      for (uint32_t t = n - 8; t < 8 * ob; t++) out[t] = 0xFFFFu;  // the last block's padding
+    lo |= 15u;
+    hi |= ((uint64_t)(ok ? ost : 0u) << 36) | ((uint64_t)(ok ? n - 8 : 0u) << 52);
+  } else {
+    lo |= n;
+  }
+  tab[(uint64_t)d * kFBuckets + j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step 8
-// entries, a step's loads in flight while the one before is tested; each entry
-// one header read.  A survivor is written as (position, slice).
+// grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step 16
+// entries, the next two steps' loads in flight while one is tested; each entry
+// one 16-B header read and two SWAR compares (an overflow block read for the
+// few buckets past 10 values).  A survivor is written as (position, slice).
 __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restrict__ v1,
                                                           const uint32_t* __restrict__ goff1, uint32_t T,
                                                           const uint4* __restrict__ tab,
                                                           const uint16_t* __restrict__ ovals,
                                                           const uint32_t* __restrict__ cursor,
-                                                          uint2* __restrict__ surv, uint32_t* __restrict__ nsurv) {
+                                                          uint2* __restrict__ surv, uint32_t* __restrict__ nsurv,
+                                                          uint32_t* __restrict__ wgcnt) {
   __shared__ uint4 lhdr[kFBuckets];
-  __shared__ uint16_t lov[kFOv];
-  __shared__ uint32_t full;  // some wave saw the survivors overflow (no global polling: one
-                             // counter read by every wave each step measured 12 ms per C2 step)
+  __shared__ uint4 lov[kFOv / 8];
+  // the workgroup's survivors so far, in its own region of surv (an LDS
+  // cursor: a returning global atomic per survivor wave makes the compiler
+  // wait for every load in flight, the next step's entries included; one
+  // counter read by every wave each step measured 12 ms per C2 step)
+  __shared__ uint32_t wsurv;
   const uint32_t d = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const uint32_t R0 = goff1[(uint64_t)d * T], R1 = goff1[(uint64_t)(d + 1) * T];
   const uint64_t len = R1 - R0;
   const uint32_t a = R0 + (uint32_t)(len * blockIdx.x / gridDim.x), b = R0 + (uint32_t)(len * (blockIdx.x + 1) / gridDim.x);
-  if (a >= b) return;
-  const uint32_t nov = min(cursor[d], kFOv);
-  if (tid == 0) full = 0;
+  if (a >= b) {
+    if (tid == 0) wgcnt[d * gridDim.x + blockIdx.x] = 0;
+    return;
+  }
+  const uint32_t nob = min(cursor[d] + 1, kFOv / 8);
+  const uint32_t wg = d * gridDim.x + blockIdx.x;
+  uint2* wsv = surv + (uint64_t)wg * kFWgCap;
+  if (tid == 0) wsurv = 0;
   for (uint32_t i = tid; i < kFBuckets; i += kFThreads) lhdr[i] = tab[(uint64_t)d * kFBuckets + i];
-  for (uint32_t i = tid; i < nov; i += kFThreads) lov[i] = ovals[(uint64_t)d * kFOv + i];
+  const uint4* osrc = reinterpret_cast<const uint4*>(ovals + (uint64_t)d * kFOv);
+  for (uint32_t i = tid; i < nob; i += kFThreads) lov[i] = osrc[i];
+  if (tid == 0) lov[0] = make_uint4(~0u, ~0u, ~0u, ~0u);  // the dummy block: matches no position
   __syncthreads();
-  constexpr int U = 2;  // quads per thread per step
+  // 16 entries per thread per step, two more steps in flight (128 KiB per CU:
+  // one 16-wave workgroup holds the LDS index, so the stream's depth is per
+  // thread)
+  constexpr int U = 4;  // quads per thread per step
   constexpr int E = 4 * U;
+  constexpr int EH = 4;  // entries tested together (their LDS reads in flight)
   const uint32_t qa = a & ~3u;
   constexpr uint32_t kStep = 4 * kFThreads * U;
-  uint32_t en[E];
-  auto load = [&](uint32_t q0) {
+  // (unpredicated loads, clamped to the run's last quad: a load under a
+  // branch makes the compiler wait for every load in flight at the join, the
+  // next steps' included -- the step then paid a whole memory latency)
+  const uint32_t qlast = (b - 1) & ~3u;
+  auto load = [&](uint32_t q0, uint32_t(&en)[E]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t q = q0 + 4 * kFThreads * u;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (q < b) {
-        const v4u32 t = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(v1 + q));
-        x = make_uint4(t[0], t[1], t[2], t[3]);
-      }
-      en[4 * u] = x.x;
-      en[4 * u + 1] = x.y;
-      en[4 * u + 2] = x.z;
-      en[4 * u + 3] = x.w;
+      const uint32_t q = min(q0 + 4 * kFThreads * u, qlast);
+      const v4u32 t = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(v1 + q));
+      en[4 * u] = t[0];
+      en[4 * u + 1] = t[1];
+      en[4 * u + 2] = t[2];
+      en[4 * u + 3] = t[3];
     }
   };
-  load(qa + 4 * tid);
-  for (uint32_t q0 = qa + 4 * tid; q0 < b; q0 += kStep) {
-    uint32_t e[E];
+  // Three entry buffers in rotation (a register copy from a buffer whose
+  // loads are in flight would wait for them): step i tests one while the
+  // next two steps' loads land in the others.
+  uint32_t bA[E], bB[E], bC[E];
+  auto step = [&](uint32_t q0, const uint32_t(&e)[E]) -> bool {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&wsurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >
+        kFWgCap)
+      return false;  // (overflowing: the partition goes on)
+    // Branch-free per entry (a branch per entry cost more than the tests):
+    // the header and, for a bucket past 10 values, its overflow list's first
+    // block (else the dummy block 0) are read for every entry; a value past
+    // the first block (a bucket past 18 values) is not proven here and
+    // survives -- the tail re-checks every survivor against the bitmap.
+    uint32_t svm = 0;  // bit k: entry k survives
 #pragma unroll
-    for (int k = 0; k < E; k++) e[k] = en[k];
-    load(q0 + kStep);
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-      break;
-    uint4 h[E];
+    for (int k0 = 0; k0 < E; k0 += EH) {
+      if (SG_FABL == 1) continue;
+      uint4 h[EH];
 #pragma unroll
-    for (int k = 0; k < E; k++) h[k] = lhdr[(e[k] >> 8) >> kFRemBits];
+      for (int k = 0; k < EH; k++) h[k] = lhdr[(e[k0 + k] >> 8) >> kFRemBits];
+      if (SG_FABL == 2) {
+        uint32_t x = 0;
 #pragma unroll
-    for (int k = 0; k < E; k++) {
-      const uint32_t p = q0 + 4 * kFThreads * (k >> 2) + (k & 3);
-      const bool live = p >= a && p < b;
-      const uint32_t r = (e[k] >> 8) & ((1u << kFRemBits) - 1);
-      const uint64_t lo = ((uint64_t)h[k].y << 32) | h[k].x, hi = ((uint64_t)h[k].w << 32) | h[k].z;
-      const uint32_t n4 = h[k].x & 15u, nh = n4 == 15u ? 8u : n4;
-      bool hit = false;
-#pragma unroll
-      for (uint32_t f = 0; f < 10; f++) {
-        const uint32_t v = (uint32_t)((f < 5 ? lo >> (4 + 12 * f) : hi >> (12 * (f - 5))) & 0xFFFu);
-        hit |= v == r && f < nh;
+        for (int k = 0; k < EH; k++) x |= h[k].x ^ h[k].w;
+        if (x == 0x12345678u) wsv[0] = make_uint2(x, x);
+        continue;
       }
-      if (!hit && n4 == 15u) {  // the rest, in the overflow list (sorted)
-        uint32_t o = (uint32_t)(hi >> 36) & 0xFFFFu, m = (uint32_t)(hi >> 52);
-        const uint32_t end = o + m;
-        while (m) {
-          const uint32_t hf = m >> 1;
-          if (lov[o + hf] < r) {
-            o += hf + 1;
-            m -= hf + 1;
-          } else {
-            m = hf;
-          }
-        }
-        hit = o < end && lov[o] == r;
+      uint4 o[EH];
+#pragma unroll
+      for (int k = 0; k < EH; k++) o[k] = lov[(h[k].x & 15u) == 15u ? (h[k].w >> 4) & 0xFFFFu : 0u];
+#pragma unroll
+      for (int kk = 0; kk < EH; kk++) {
+        const int k = k0 + kk;
+        const uint32_t r = (e[k] >> 8) & ((1u << kFRemBits) - 1);
+        const uint64_t lo = ((uint64_t)h[kk].y << 32) | h[kk].x, hi = ((uint64_t)h[kk].w << 32) | h[kk].z;
+        const bool mark = (h[kk].x & 15u) == 15u;
+        const uint64_t hf = mark ? (hi & 0xFFFFFFFFFull) | 0xFFFFFF000000000ull : hi;  // fields 8, 9 unused
+        const uint64_t r12 = 0x001001001001001ull * r, r16 = 0x0001000100010001ull * r;
+        const bool hit = (m0f_has12(lo >> 4, r12) | m0f_has12(hf & 0xFFFFFFFFFFFFFFFull, r12) |
+                          m0f_has16(((uint64_t)o[kk].y << 32) | o[kk].x, r16) |
+                          m0f_has16(((uint64_t)o[kk].w << 32) | o[kk].z, r16)) != 0;
+        const uint32_t p = q0 + 4 * kFThreads * (k >> 2) + (k & 3);
+        svm |= (p >= a && p < b && !hit ? 1u : 0u) << k;
       }
-      const bool sv = live && !hit;
-      const uint64_t bal = __ballot(sv);
-      if (!bal) continue;
-      const int first = __builtin_ctzll(bal);
-      uint32_t at = 0;
-      if (lane == (uint32_t)first) at = atomicAdd(nsurv, (uint32_t)__popcll(bal));
-      at = (uint32_t)__shfl((int)at, first);
-      if (at >= kFSurvCap && lane == (uint32_t)first)
-        __hip_atomic_store(&full, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      at += (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-      if (sv && at < kFSurvCap) surv[at] = make_uint2(p, d);
     }
+    if (__ballot(svm != 0)) {  // (rare in the steady state)
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const bool sv = (svm >> k) & 1u;
+        const uint64_t bal = __ballot(sv);
+        if (!bal) continue;
+        const uint32_t p = q0 + 4 * kFThreads * (k >> 2) + (k & 3);
+        const int first = __builtin_ctzll(bal);
+        uint32_t at = 0;
+        if (lane == (uint32_t)first) at = atomicAdd(&wsurv, (uint32_t)__popcll(bal));
+        at = (uint32_t)__shfl((int)at, first) + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        if (sv && at < kFWgCap) wsv[at] = make_uint2(p, d);
+      }
+    }
+    return true;
+  };
+  uint32_t q0 = qa + 4 * tid;
+  load(q0, bA);
+  load(q0 + kStep, bB);
+  while (q0 < b) {
+    load(q0 + 2 * kStep, bC);
+    if (!step(q0, bA)) break;
+    if ((q0 += kStep) >= b) break;
+    load(q0 + 2 * kStep, bA);
+    if (!step(q0, bB)) break;
+    if ((q0 += kStep) >= b) break;
+    load(q0 + 2 * kStep, bB);
+    if (!step(q0, bC)) break;
+    q0 += kStep;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t c = wsurv;
+    wgcnt[wg] = c;
+    // the total (kFSurvCap + 1 past a region: the host then partitions)
+    atomicAdd(nsurv, c > kFWgCap ? kFSurvCap + 1 : c);
   }
 }
 
@@ -2114,25 +2188,28 @@ __device__ __forceinline__ uint32_t m0f_hash(uint32_t s) {
 // the survivors still outside maxSignal (a value past an index cap is only
 // re-checked here): each one's record (its pass-1 tile by a search over the
 // slice's run starts), then min(record) per signal
-__global__ void k_m0_tail_insert(const uint2* __restrict__ surv, uint32_t n, const uint32_t* __restrict__ v1,
+__global__ void k_m0_tail_insert(const uint2* __restrict__ surv, const uint32_t* __restrict__ wgcnt,
+                                 const uint32_t* __restrict__ v1,
                                  const uint32_t* __restrict__ goff1, uint32_t T, const uint32_t* __restrict__ trec,
                                  const uint32_t* __restrict__ mwords, unsigned long long* __restrict__ table) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint2 q = surv[i];  // (position, slice)
+  // grid (4, filter workgroups): the survivors of region y, strided
+  const uint32_t nw = min(wgcnt[blockIdx.y], kFWgCap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
+  const uint2 q = surv[(uint64_t)blockIdx.y * kFWgCap + i];  // (position, slice)
   const uint32_t e = v1[q.x], t = (q.y << 24) | (e >> 8);
-  if ((mwords[t >> 5] >> (t & 31)) & 1u) return;
+  if ((mwords[t >> 5] >> (t & 31)) & 1u) continue;
   const uint32_t s = part_sig(t);
   const uint32_t rec = trec[last_le(goff1 + (uint64_t)q.y * T, 0, T, q.x)] + (e & 0xFFu);
   const unsigned long long key = ((unsigned long long)s << 32) | rec;
   constexpr uint32_t mask = (1u << kFTableBits) - 1;
   for (uint32_t h = m0f_hash(s) & mask;; h = (h + 1) & mask) {
     const unsigned long long old = atomicCAS(&table[h], kFEmpty, key);
-    if (old == kFEmpty) return;
+    if (old == kFEmpty) break;
     if ((uint32_t)(old >> 32) == s) {
       if (old > key) atomicMin(&table[h], key);
-      return;
+      break;
     }
+  }
   }
 }
 
@@ -2507,7 +2584,8 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
     ScopedTimer tm(ctx, "m0_filter");
     hipLaunchKernelGGL(k_m0_filter, dim3(kFParts, 256), dim3(kFThreads), 0, ctx->stream,
                        (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
-                       (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor, f.surv, f.nsurv);
+                       (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor, f.surv, f.nsurv,
+                       f.wgcnt);
   }
   SG_HIP(hipGetLastError());
   // (the host ingest's pinned staging may be in a DMA now: a pageable read)
@@ -2517,12 +2595,13 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   ctx->m0f_survivors = ns;
   if (ns > kFSurvCap) {
     ctx->m0f_fallback++;
-    if (ctx->opt[kOptM0Filter] < 0) ctx->m0f_skip = 15;
+    ctx->m0f_last = 0;
     return SG_OK;
   }
   if (ns) {
     ScopedTimer tm(ctx, "m0_tail");
-    hipLaunchKernelGGL(k_m0_tail_insert, dim3(div_up(ns, 256)), dim3(256), 0, ctx->stream, (const uint2*)f.surv, ns,
+    hipLaunchKernelGGL(k_m0_tail_insert, dim3(4, 256 * kFParts), dim3(256), 0, ctx->stream,
+                       (const uint2*)f.surv, (const uint32_t*)f.wgcnt,
                        (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
                        (const uint32_t*)ws_at(ctx, bp.oTR), (const uint32_t*)mwords, f.table);
     hipLaunchKernelGGL(k_m0_tail_flush, dim3((1u << kFTableBits) / 256), dim3(256), 0, ctx->stream, f.table, mwords,
@@ -2530,21 +2609,57 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   }
   SG_HIP(hipGetLastError());
   ctx->m0f_used++;
+  ctx->m0f_last = 1;
   *done = true;
   return SG_OK;
 }
 
-// The M0 filter's regime: option m0_filter 1 always tries it, 0 never; auto
-// tries it unless a recent record slice overflowed it (15 slices are skipped
-// then, so a run of fresh batches pays it on one slice in 16).
+// queued records of a partitioned slice: one add per block
+__global__ void k_count_flags(const uint8_t* __restrict__ f, uint64_t n, uint32_t* __restrict__ out) {
+  uint32_t c = 0;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (uint64_t)gridDim.x * blockDim.x * 4)
+    for (int k = 0; k < 4; k++) c += i + k < n && f[i + k] ? 1u : 0u;
+  c = sgd::wave_incl_add(c);
+  if ((threadIdx.x & 63) == 63 && c) atomicAdd(out, c);
+}
+
+// After a partitioned slice (auto regime): its queued records counted on the
+// device and copied to pinned memory behind an event, read by a later m0f_try.
+static int m0f_note_partitioned(sg_ctx* ctx, const uint8_t* d_rec_new, uint64_t nrec) {
+  ctx->m0f_last = 0;
+  if (ctx->opt[kOptM0Filter] >= 0 || ctx->m0f_pending) return SG_OK;
+  if (!ctx->m0f_host) {
+    SG_HIP(hipHostMalloc((void**)&ctx->m0f_host, 64, hipHostMallocDefault));
+    SG_HIP(hipEventCreateWithFlags(&ctx->m0f_ev, hipEventDisableTiming));
+  }
+  uint32_t* dcnt = (uint32_t*)ctx->dscal + 32;  // (a device scalar of the context)
+  SG_HIP(hipMemsetAsync(dcnt, 0, 4, ctx->stream));
+  hipLaunchKernelGGL(k_count_flags, dim3(std::min<uint64_t>(256, div_up(nrec, 1024))), dim3(256), 0, ctx->stream,
+                     d_rec_new, nrec, dcnt);
+  SG_HIP(hipMemcpyAsync(ctx->m0f_host, dcnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipEventRecord(ctx->m0f_ev, ctx->stream));
+  ctx->m0f_pending = true;
+  ctx->m0f_nrec = nrec;
+  return SG_OK;
+}
+
+// The M0 filter's regime: option m0_filter 1 always tries it, 0 never.  auto
+// (the fuzzer's loop, batch after batch) tries it after a slice it filtered,
+// and after a partitioned slice whose queued fraction was below kFTryQueued
+// (in the steady state 9 % of the records are queued, in a fresh batch all:
+// fresh batches then never pay for it); on the context's first slice it is
+// tried.  A queued count still in flight keeps the previous choice.
+constexpr double kFTryQueued = 0.25;
 static bool m0f_try(sg_ctx* ctx) {
   const int64_t o = ctx->opt[kOptM0Filter];
   if (o >= 0) return o != 0;
-  if (ctx->m0f_skip) {
-    ctx->m0f_skip--;
-    return false;
+  if (ctx->m0f_pending && hipEventQuery(ctx->m0f_ev) == hipSuccess) {
+    ctx->m0f_pending = false;
+    ctx->m0f_queued = (double)*ctx->m0f_host / (double)(ctx->m0f_nrec ? ctx->m0f_nrec : 1);
   }
-  return true;
+  if (ctx->m0f_last < 0) return true;
+  if (ctx->m0f_last == 1) return true;
+  return ctx->m0f_queued >= 0 && ctx->m0f_queued < kFTryQueued;
 }
 
 static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, const uint32_t* d_vals,
@@ -2556,10 +2671,16 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
     return SG_EINVAL;
   }
   BucketPlan bp(n, nrec);
-  if (emit || ws_base || !m0f_try(ctx)) {
+  if (emit || ws_base) {
     int rc = partition_one(ctx, d_vals, d_off, n, nrec, ws_base, ws_base != 0, bp, trace);
     if (rc) return rc;
     return buckets_one(ctx, bp, mwords, nwords, d_rec_new, emit, n, nrec);
+  }
+  if (!m0f_try(ctx)) {
+    int rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace);
+    if (!rc) rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new, nullptr, n, nrec);
+    if (!rc) rc = m0f_note_partitioned(ctx, d_rec_new, nrec);
+    return rc;
   }
   // the flags path with the M0 filter between the two partition passes
   int rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 1);
@@ -2568,8 +2689,9 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
   rc = m0_filter(ctx, bp, mwords, nwords, d_rec_new, &done);
   if (rc || done) return rc;
   rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 2);
-  if (rc) return rc;
-  return buckets_one(ctx, bp, mwords, nwords, d_rec_new, nullptr, n, nrec);
+  if (!rc) rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new, nullptr, n, nrec);
+  if (!rc) rc = m0f_note_partitioned(ctx, d_rec_new, nrec);
+  return rc;
 }
 
 // Marks: nwords |= every signal of stage A's buckets that is not in mwords

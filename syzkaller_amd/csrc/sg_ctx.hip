@@ -540,6 +540,8 @@ void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->dstage) hipFree(ctx->dstage);
   if (ctx->owner) hipFree(ctx->owner);
   if (ctx->m0f) hipFree(ctx->m0f);
+  if (ctx->m0f_host) hipHostFree(ctx->m0f_host);
+  if (ctx->m0f_ev) hipEventDestroy(ctx->m0f_ev);
   if (ctx->slice_off) hipFree(ctx->slice_off);
   if (ctx->slice_cuts) hipFree(ctx->slice_cuts);
   if (ctx->dscal) hipFree(ctx->dscal);
@@ -716,6 +718,8 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
     *out = ctx->m0f_fallback;
   else if (!strcmp(name, "m0_filter_survivors"))  // survivors of the last filtered slice
     *out = ctx->m0f_survivors;
+  else if (!strcmp(name, "m0_filter_queued_milli"))  // queued fraction x1000 of the last partitioned slice
+    *out = ctx->m0f_queued < 0 ? ~0ull : (uint64_t)(ctx->m0f_queued * 1000.0 + 0.5);
   else if (!strcmp(name, "cpu_quota_milli"))
     *out = (uint64_t)(ctx->cpu_quota * 1000.0 + 0.5);
   else {

@@ -100,10 +100,17 @@ struct sg_ctx {
   int device = 0;
   int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0, -1};
   // the M0 filter's buffers (lazy, sg_bucket.hip) and its regime state: the
-  // batches left to skip after a batch whose survivors overflowed; batches
-  // it filtered and fell back on (counters)
+  // last record slice's outcome (1 filtered, 0 partitioned), the queued
+  // records of the last partitioned slice (counted on the device, read back
+  // through m0f_host once m0f_ev has passed: no host wait) and its record
+  // count; slices it filtered and fell back on (counters)
   void* m0f = nullptr;
-  uint32_t m0f_skip = 0;
+  uint32_t* m0f_host = nullptr;  // pinned: the queued-record count
+  hipEvent_t m0f_ev = nullptr;
+  int m0f_last = -1;             // -1 nothing yet
+  bool m0f_pending = false;
+  uint64_t m0f_nrec = 0;
+  double m0f_queued = -1;        // queued fraction of the last partitioned slice (-1 unknown)
   uint64_t m0f_used = 0, m0f_fallback = 0, m0f_survivors = 0;
   // host CPUs this process may use (cgroup cpu.max quota, else the affinity
   // mask), read at creation: sizes the host ingest's copy threads

@@ -81,8 +81,13 @@ def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option):
     vals[rng.integers(0, vals.size, size=200)] = rep
     _check(C, ctx, m0, vals, off, 1, "used")
     # empty maxSignal: every entry survives (fewer than the cap)
-    vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0, hi=1 << 20)
+    vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0)
     _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "used")
+    # ... all of them in one pass-1 slice (b2 = 0): past a filter workgroup's
+    # region (8192), so the partition goes on
+    vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0, hi=1 << 16)
+    assert vals.size > 2 * 8192 + 1000
+    _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "fallback")
     # empty records only / a batch without entries
     _check(C, ctx, m0, np.zeros(0, np.uint32), np.zeros(9, np.uint64), 1, None)
 
@@ -100,7 +105,9 @@ def test_m0_filter_index_cap_and_overflow(C, ctx, ctx_option):
                       | (low & np.uint64(0xFFFF))).astype(np.uint32)
     other = np.unique(rng.integers(0, 1 << 32, size=50_000, dtype=np.uint64).astype(np.uint32))
     m0 = np.unique(np.concatenate([dense, other]))
-    vals, off = _batch(rng, 30_000, m0, 1e-3)
+    vals, off = _batch(rng, 30_000, other, 1e-3)
+    hot = rng.random(vals.size) < 0.02  # ~15K entries in the dense slice: ~1/3 of them unproven by its index
+    vals[hot] = dense[rng.integers(0, dense.size, size=int(hot.sum()))]
     _check(C, ctx, m0, vals, off, 1, "used")
     # fresh: ~1.6M survivors > the cap
     vals, off = _batch(rng, 50_000, m0, 1.0, maxlen=80)
@@ -109,10 +116,12 @@ def test_m0_filter_index_cap_and_overflow(C, ctx, ctx_option):
 
 
 def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
-    """auto: a batch whose survivors overflow turns the filter off for the
-    next 15 record slices, then it is tried again; record slices (a lowered
-    per-launch record limit) are filtered one by one, each against the
-    maxSignal the slices before it left."""
+    """auto: tried after a slice it filtered; after a partitioned slice only
+    when that slice queued under a quarter of its records (a fresh batch queues
+    nearly all: the next one is partitioned, and its own low queued fraction
+    brings the filter back); record slices (a lowered per-launch record limit)
+    are filtered one by one, each against the maxSignal the slices before it
+    left."""
     ctx = C.Context(0)
     try:
         rng = np.random.default_rng(6003)
@@ -123,11 +132,12 @@ def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
         assert ctx.counter("m0_filter_used") >= 12
         ctx.set_option("max_launch_records", 0)
         fresh, foff = _batch(rng, 50_000, m0, 1.0, maxlen=80)
-        _check(C, ctx, m0, fresh, foff, -1, "fallback")
-        for _ in range(15):  # skipped while the regime says fresh
-            _check(C, ctx, m0, vals, off, -1, "skip")
-        _check(C, ctx, m0, vals, off, -1, "used")
+        _check(C, ctx, m0, fresh, foff, -1, "fallback")  # (tried: the last slice was filtered)
+        _check(C, ctx, m0, vals, off, -1, "skip")  # the fresh batch queued ~83 % of its records
+        _check(C, ctx, m0, vals, off, -1, "used")  # ... this one a few percent
+        assert ctx.counter("m0_filter_queued_milli") < 250
         _check(C, ctx, m0, vals, off, 0, "skip")  # never
+        _check(C, ctx, m0, fresh, foff, -1, "fallback")
     finally:
         ctx.close()
 
