@@ -584,12 +584,13 @@ template <bool kTop>
 __device__ __forceinline__ void tile_write(const uint32_t* stage, const uint32_t* cnt, const uint32_t* gbase,
                                            uint32_t* __restrict__ out, uint8_t* __restrict__ top, int tid) {
   const int hw = tid >> 5, hl = tid & 31;
+  const bool wtop = kTop && top;  // (none when the M0 filter may end the partition after pass 1)
   for (int d = hw; d < 256; d += kPThreads / 32) {
     const uint32_t e = cnt[d], gb = gbase[d];
     for (uint32_t p = (d ? cnt[d - 1] : 0u) + hl; p < e; p += 32) {
       const uint32_t v = stage[p];
       out[gb + p] = v;
-      if (kTop) top[gb + p] = (uint8_t)(v >> 24);
+      if (wtop) top[gb + p] = (uint8_t)(v >> 24);
     }
   }
 }
@@ -1878,14 +1879,23 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 // signals).  A slice's part of maxSignal is ~50K signals (12.8M / 256): too
 // many for its 2 MiB of bitmap, few enough for a packed index in LDS:
 //   k_m0_index  per slice, one 16-B header per 2^11-signal filter bucket
-//               (8192: 128 KiB): the bucket's count and its first 10 set
-//               positions as 12-bit fields (ascending), or, past 10, a marker,
-//               the first 8 and where the rest start in a small overflow list
-//               (kFOv values per slice; past it, signals are not proven, only
-//               re-checked by the tail); one read of the slice's bitmap;
-//   k_m0_filter per slice part, the slice's index in LDS (136 KiB); every
-//               pass-1 entry reads its bucket's header (one ds_read_b128) and
-//               compares; an entry not found survives, as (position, slice);
+//               (8192: 128 KiB): up to 8 of the bucket's set positions as
+//               16-bit fields (ascending, 0x8000 in the unused ones), or,
+//               past 8, the first 7 and in field 7 0x8000 | the block of the
+//               next 8 in a small per-slice pool (kFOvBlocks 8-value blocks);
+//               the rest (past 15, or past 7 when the pool is full) in the
+//               slice's spill list (kFSpill positions; past it, signals are
+//               not proven, only re-checked by the tail); one read of the
+//               slice's bitmap;
+//   k_m0_filter per slice part, the slice's index in LDS (159 KiB); every
+//               pass-1 entry reads its bucket's header and the first block of
+//               its overflow list (the pool's dummy block 0 for a bucket
+//               without one) -- two ds_read_b128, the second one's address
+//               from the first -- and compares its position with the 16
+//               fields by packed 16-bit xor / min; an entry not found is
+//               looked up in the spill list (held in registers, 8 per lane,
+//               a wave-wide compare per such entry) and, not there either,
+//               survives, as (position, slice);
 //   tail        if the survivors fit (kFSurvCap): each survivor still outside
 //               maxSignal (the exact bitmap test) gets its record (its pass-1
 //               tile by a search over the slice's run starts) and takes
@@ -1894,19 +1904,26 @@ static int scan32(sg_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, ui
 //               and newSignal -- the bucket stage's results (fuzzer.go:669-690)
 //               over the candidates.
 // When the survivors overflow, pass 2 and the bucket stage run on the same
-// pass-1 output: the filter costs its index and a short pass, and the regime
-// is not tried again for 15 record slices (option m0_filter: -1 auto).
+// pass-1 output.  Option m0_filter -1 (auto, m0f_try) tries the filter after a
+// slice it filtered and after a partitioned slice that queued under a quarter
+// of its records.
 constexpr uint32_t kFRemBits = 11;                      // positions per filter bucket: 2^11
 constexpr uint32_t kFBuckets = 1u << (24 - kFRemBits);  // 8192 per slice
-constexpr uint32_t kFOv = 8192;                         // overflow values per slice (16 KiB of u16, 8-value blocks)
+constexpr uint32_t kFOvBlocks = 1984;                   // overflow pool per slice: 8-value u16 blocks (31 KiB);
+                                                        // block 0 the dummy
+constexpr uint32_t kFPad = 0x8000u;                     // an unused field (no position; >= it: a block link)
+constexpr uint32_t kFSpill = 512;                       // spill list per slice (8 registers per lane)
 constexpr uint32_t kFSurvCap = 1u << 20;                // survivors per launch
 constexpr uint32_t kFTableBits = 21;                    // the tail's table: 2^21 u64 slots
 constexpr int kFThreads = 1024;
 #ifndef SG_FPARTS
 #define SG_FPARTS 2
 #endif
-#ifndef SG_FABL
-#define SG_FABL 0  // diagnostics builds: 1 the entry stream only, 2 and the header reads (wrong results)
+#ifndef SG_FU
+#define SG_FU 4  // 16-B entry loads per thread per step
+#endif
+#ifndef SG_FEH
+#define SG_FEH 4  // entries whose LDS reads are in flight together
 #endif
 constexpr uint32_t kFParts = SG_FPARTS;                 // filter workgroups per slice
 constexpr uint32_t kFWgCap = 4 * kFSurvCap / (256 * kFParts);  // survivors per filter workgroup (its own region:
@@ -1915,15 +1932,18 @@ constexpr unsigned long long kFEmpty = ~0ull;
 
 struct M0F {
   uint4* tab;                 // [slice][bucket] headers
-  uint16_t* ovals;            // [slice][kFOv] overflow values
-  uint32_t* cursor;           // [slice] overflow values placed (may pass kFOv)
+  uint16_t* ovals;            // [slice][8 kFOvBlocks] overflow pool
+  uint32_t* cursor;           // [slice] overflow blocks placed (may pass the pool)
+  uint32_t* nspill;           // [slice] spilled positions (may pass kFSpill)
+  uint32_t* spill;            // [slice][kFSpill] positions
   uint32_t* nsurv;            // survivors; kFSurvCap + 1 when a workgroup's region overflowed
   uint2* surv;                // (position, slice), kFWgCap per filter workgroup
   uint32_t* wgcnt;            // [filter workgroup] survivors in its region
   unsigned long long* table;  // signal << 32 | min record; kFEmpty between launches
 };
 static size_t m0f_bytes() {
-  return 256ull * kFBuckets * 16 + 256ull * kFOv * 2 + 256 * 4 + 256 + 256ull * kFParts * kFWgCap * 8 +
+  return 256ull * kFBuckets * 16 + 256ull * kFOvBlocks * 16 + 256 * 4 + 256 + 256 * 4 + 256ull * kFSpill * 4 +
+         256ull * kFParts * kFWgCap * 8 +
          256ull * kFParts * 4 + (8ull << kFTableBits);
 }
 static M0F m0f_bind(sg_ctx* ctx) {
@@ -1932,10 +1952,13 @@ static M0F m0f_bind(sg_ctx* ctx) {
   f.tab = (uint4*)b;
   b += 256ull * kFBuckets * 16;
   f.ovals = (uint16_t*)b;
-  b += 256ull * kFOv * 2;
+  b += 256ull * kFOvBlocks * 16;
   f.cursor = (uint32_t*)b;
   f.nsurv = f.cursor + 256;
-  b += 256 * 4 + 256;
+  f.nspill = f.cursor + 256 + 64;
+  b += 256 * 4 + 256 + 256 * 4;
+  f.spill = (uint32_t*)b;
+  b += 256ull * kFSpill * 4;
   f.surv = (uint2*)b;
   b += 256ull * kFParts * kFWgCap * 8;
   f.wgcnt = (uint32_t*)b;
@@ -1944,35 +1967,15 @@ static M0F m0f_bind(sg_ctx* ctx) {
   return f;
 }
 
-// Header of a filter bucket, as two 64-bit halves: lo bits 0..3 the count n
-// (15: more than 10), fields k = 0..4 at 4 + 12 k; hi fields k = 5..9 at
-// 12 (k - 5); unused fields hold 0xFFF (no position is), so a lookup compares
-// all ten at once.  Past 10 values: fields 0..7, hi bits 36..51 the overflow
-// list's first 8-value block, 52..63 how many values follow there; the list
-// is whole 16-B blocks of u16, padded with 0xFFFF.
-__device__ __forceinline__ uint32_t m0f_field_bit(uint32_t k) { return k < 5 ? 4 + 12 * k : 64 + 12 * (k - 5); }
-
-// does one of the 12-bit fields in bits 0..59 of t equal r?  (SWAR: a field
-// of t ^ r...r is zero exactly where it matches; the borrow trick finds one)
-__device__ __forceinline__ uint64_t m0f_has12(uint64_t t, uint64_t rep) {  // rep = r in each 12-bit field
-  constexpr uint64_t kOnes = 0x001001001001001ull, kHigh = 0x800800800800800ull;
-  const uint64_t x = t ^ rep;
-  return (x - kOnes) & ~x & kHigh;  // non-zero iff some field equals r
-}
-__device__ __forceinline__ uint64_t m0f_has16(uint64_t t, uint64_t rep) {  // four 16-bit fields
-  constexpr uint64_t kOnes = 0x0001000100010001ull, kHigh = 0x8000800080008000ull;
-  const uint64_t x = t ^ rep;
-  return (x - kOnes) & ~x & kHigh;
-}
-
 // grid (kFBuckets / 256, 256): thread t of block (e, d) indexes filter
 // bucket 256 e + t of slice d, its 64 bitmap words (256 B) read as 16 quads;
 // it walks their set bits in order into its header's fields and its overflow
 // list, whose blocks one cursor add per wave places.  (A wave per 64 buckets,
 // lane l holding word l of each, measured 0.40-0.45 ms per steady step: 128
-// wave scans per 64 buckets.)
+// wave scans per 64 buckets; this form 0.24 ms.)
 __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ mwords, uint4* __restrict__ tab,
-                                                   uint16_t* __restrict__ ovals, uint32_t* __restrict__ cursor) {
+                                                   uint16_t* __restrict__ ovals, uint32_t* __restrict__ cursor,
+                                                   uint32_t* __restrict__ nspill, uint32_t* __restrict__ spill) {
   const uint32_t d = blockIdx.y, lane = threadIdx.x & 63;
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   const uint4* src = reinterpret_cast<const uint4*>(mwords + ((uint64_t)d << 19) + ((uint64_t)j << 6));
@@ -1982,19 +1985,18 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
   uint32_t n = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) n += __popc(q[i].x) + __popc(q[i].y) + __popc(q[i].z) + __popc(q[i].w);
-  // the overflow list (whole 8-value blocks) of a bucket past 10 values
-  const uint32_t ob = n > 10 ? (n - 8 + 7) >> 3 : 0u;
+  // the overflow block of a bucket past 8 values
+  const uint32_t ob = n > 8 ? 1u : 0u;
   const uint32_t oi = sgd::wave_incl_add(ob);
   const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane((int)oi, 63);
   uint32_t obase = 0;
   if (lane == 0 && otot) obase = atomicAdd(&cursor[d], otot);
   obase = (uint32_t)__builtin_amdgcn_readfirstlane((int)obase);
   const uint32_t ost = 1 + obase + oi - ob;  // first block (block 0: none, the filter's dummy)
-  constexpr uint32_t kOvBlocks = kFOv / 8;
-  const bool ok = ob && ost + ob <= kOvBlocks;  // (else the list is dropped: the tail re-checks)
-  uint16_t* out = ovals + (uint64_t)d * kFOv + 8 * (uint64_t)ost;
-  const uint32_t kin = n > 10 ? 8u : n;  // values in the header
-  uint64_t lo = 0, hi = 0;
+  const bool ok = ob && ost + ob <= kFOvBlocks;  // (else the rest is spilled)
+  uint16_t* out = ovals + ((uint64_t)d * kFOvBlocks + ost) * 8;
+  const uint32_t kin = n > 8 ? 7u : 8u;  // values in the header
+  uint64_t lo = 0, hi = 0;               // fields 0..3, 4..7
   uint32_t k = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
@@ -2006,49 +2008,53 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
         const uint32_t v = (uint32_t)(32 * (4 * i + c)) + (uint32_t)__builtin_ctz(m);  // ascending in k
         m &= m - 1;
         if (k < kin) {
-          const uint32_t at = m0f_field_bit(k);
-          if (at < 64)
-            lo |= (uint64_t)v << at;
+          if (k < 4)
+            lo |= (uint64_t)v << (16 * k);
           else
-            hi |= (uint64_t)v << (at - 64);
-        } else if (ok) {
-          out[k - 8] = (uint16_t)v;
+            hi |= (uint64_t)v << (16 * (k - 4));
+        } else if (ok && k < 15) {
+          out[k - 7] = (uint16_t)v;
+        } else {  // (rare: past 15 values, or the pool full)
+          const uint32_t at = atomicAdd(&nspill[d], 1u);
+          if (at < kFSpill) spill[(uint64_t)d * kFSpill + at] = (j << kFRemBits) | v;
         }
         k++;
       }
     }
   }
-  for (uint32_t f = kin; f < (n > 10 ? 8u : 10u); f++) {  // unused fields: 0xFFF
-    const uint32_t at = m0f_field_bit(f);
-    if (at < 64)
-      lo |= 0xFFFull << at;
+  for (uint32_t f = min(n, kin); f < 8; f++) {  // unused fields, and field 7 past 8 values
+    const uint64_t v = f == 7 && n > 8 && ok ? kFPad | ost : kFPad;
+    if (f < 4)
+      lo |= v << (16 * f);
     else
-      hi |= 0xFFFull << (at - 64);
+      hi |= v << (16 * (f - 4));
   }
-  if (n > 10) {
-    if (ok)
-      for (uint32_t t = n - 8; t < 8 * ob; t++) out[t] = 0xFFFFu;  // the last block's padding
-    lo |= 15u;
-    hi |= ((uint64_t)(ok ? ost : 0u) << 36) | ((uint64_t)(ok ? n - 8 : 0u) << 52);
-  } else {
-    lo |= n;
-  }
+  if (ok)
+    for (uint32_t t = n - 7; t < 8; t++) out[t] = (uint16_t)kFPad;  // the block's padding
   tab[(uint64_t)d * kFBuckets + j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step 16
-// entries, the next two steps' loads in flight while one is tested; each entry
-// one 16-B header read and two SWAR compares (an overflow block read for the
-// few buckets past 10 values).  A survivor is written as (position, slice).
+typedef unsigned short m0f_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t m0f_min16(uint32_t a, uint32_t b) {  // v_pk_min_u16
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(m0f_u16x2, a),
+                                                               __builtin_bit_cast(m0f_u16x2, b)));
+}
+
+// grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step
+// 4 SG_FU entries, the next two steps' loads in flight while one is tested.
+// A survivor is written as (position, slice).
 __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restrict__ v1,
                                                           const uint32_t* __restrict__ goff1, uint32_t T,
                                                           const uint4* __restrict__ tab,
                                                           const uint16_t* __restrict__ ovals,
                                                           const uint32_t* __restrict__ cursor,
+                                                          const uint32_t* __restrict__ nspill,
+                                                          const uint32_t* __restrict__ spill,
                                                           uint2* __restrict__ surv, uint32_t* __restrict__ nsurv,
                                                           uint32_t* __restrict__ wgcnt) {
-  __shared__ uint4 lhdr[kFBuckets];
-  __shared__ uint4 lov[kFOv / 8];
+  // the overflow pool, then the headers (one array: both bases fit the
+  // ds_read offset field)
+  __shared__ v4u32 lds[kFOvBlocks + kFBuckets];
   // the workgroup's survivors so far, in its own region of surv (an LDS
   // cursor: a returning global atomic per survivor wave makes the compiler
   // wait for every load in flight, the next step's entries included; one
@@ -2062,21 +2068,28 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
     if (tid == 0) wgcnt[d * gridDim.x + blockIdx.x] = 0;
     return;
   }
-  const uint32_t nob = min(cursor[d] + 1, kFOv / 8);
+  const uint32_t nob = min(cursor[d] + 1, kFOvBlocks);
   const uint32_t wg = d * gridDim.x + blockIdx.x;
   uint2* wsv = surv + (uint64_t)wg * kFWgCap;
   if (tid == 0) wsurv = 0;
-  for (uint32_t i = tid; i < kFBuckets; i += kFThreads) lhdr[i] = tab[(uint64_t)d * kFBuckets + i];
-  const uint4* osrc = reinterpret_cast<const uint4*>(ovals + (uint64_t)d * kFOv);
-  for (uint32_t i = tid; i < nob; i += kFThreads) lov[i] = osrc[i];
-  if (tid == 0) lov[0] = make_uint4(~0u, ~0u, ~0u, ~0u);  // the dummy block: matches no position
+  const v4u32* hsrc = reinterpret_cast<const v4u32*>(tab + (uint64_t)d * kFBuckets);
+  for (uint32_t i = tid; i < kFBuckets; i += kFThreads) lds[kFOvBlocks + i] = hsrc[i];
+  const v4u32* osrc = reinterpret_cast<const v4u32*>(ovals + (uint64_t)d * kFOvBlocks * 8);
+  for (uint32_t i = 1 + tid; i < nob; i += kFThreads) lds[i] = osrc[i];
+  if (tid == 0) lds[0] = v4u32{kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u};  // dummy
+  // the spill list, entry 64 i + lane in sp[i] (~0u: none)
+  const uint32_t nsp = min(nspill[d], kFSpill);
+  uint32_t sp[kFSpill / 64];
+#pragma unroll
+  for (int i = 0; i < (int)(kFSpill / 64); i++)
+    sp[i] = 64 * i + lane < nsp ? spill[(uint64_t)d * kFSpill + 64 * i + lane] : ~0u;
   __syncthreads();
-  // 16 entries per thread per step, two more steps in flight (128 KiB per CU:
-  // one 16-wave workgroup holds the LDS index, so the stream's depth is per
-  // thread)
-  constexpr int U = 4;  // quads per thread per step
+  // 4 SG_FU entries per thread per step, two more steps in flight (one
+  // 16-wave workgroup per CU holds the LDS index, so the stream's depth is
+  // per thread)
+  constexpr int U = SG_FU;
   constexpr int E = 4 * U;
-  constexpr int EH = 4;  // entries tested together (their LDS reads in flight)
+  constexpr int EH = SG_FEH;
   const uint32_t qa = a & ~3u;
   constexpr uint32_t kStep = 4 * kFThreads * U;
   // (unpredicated loads, clamped to the run's last quad: a load under a
@@ -2102,44 +2115,58 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&wsurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >
         kFWgCap)
       return false;  // (overflowing: the partition goes on)
-    // Branch-free per entry (a branch per entry cost more than the tests):
-    // the header and, for a bucket past 10 values, its overflow list's first
-    // block (else the dummy block 0) are read for every entry; a value past
-    // the first block (a bucket past 18 values) is not proven here and
-    // survives -- the tail re-checks every survivor against the bitmap.
-    uint32_t svm = 0;  // bit k: entry k survives
+    // the entries inside [a, b): all of them unless the wave's step crosses
+    // an end of the part (a uniform test)
+    const uint32_t qw = (uint32_t)__builtin_amdgcn_readfirstlane((int)q0);  // lane 0's
+    uint32_t vm = (1u << E) - 1;
+    if (!(qw >= a && qw + 4 * 63 + 3 + 4 * kFThreads * (U - 1) < b)) {
+      vm = 0;
+#pragma unroll
+      for (int k = 0; k < E; k++)
+        vm |= (q0 + 4 * kFThreads * (k >> 2) + (k & 3) - a < b - a ? 1u : 0u) << k;
+    }
+    // Branch-free per entry: the header and its overflow list's first block
+    // (else the dummy block 0) are read for every entry; a position past the
+    // first block (a bucket past 15 values) is not proven here and survives
+    // -- the tail re-checks every survivor against the bitmap.
+    uint32_t hm = 0;  // bit k: entry k found
 #pragma unroll
     for (int k0 = 0; k0 < E; k0 += EH) {
-      if (SG_FABL == 1) continue;
-      uint4 h[EH];
+      v4u32 h[EH];
 #pragma unroll
-      for (int k = 0; k < EH; k++) h[k] = lhdr[(e[k0 + k] >> 8) >> kFRemBits];
-      if (SG_FABL == 2) {
-        uint32_t x = 0;
+      for (int k = 0; k < EH; k++) h[k] = lds[kFOvBlocks + (e[k0 + k] >> (8 + kFRemBits))];
+      v4u32 o[EH];
 #pragma unroll
-        for (int k = 0; k < EH; k++) x |= h[k].x ^ h[k].w;
-        if (x == 0x12345678u) wsv[0] = make_uint2(x, x);
-        continue;
-      }
-      uint4 o[EH];
-#pragma unroll
-      for (int k = 0; k < EH; k++) o[k] = lov[(h[k].x & 15u) == 15u ? (h[k].w >> 4) & 0xFFFFu : 0u];
+      for (int k = 0; k < EH; k++) o[k] = lds[__builtin_elementwise_sub_sat(h[k][3] >> 16, kFPad)];
 #pragma unroll
       for (int kk = 0; kk < EH; kk++) {
-        const int k = k0 + kk;
-        const uint32_t r = (e[k] >> 8) & ((1u << kFRemBits) - 1);
-        const uint64_t lo = ((uint64_t)h[kk].y << 32) | h[kk].x, hi = ((uint64_t)h[kk].w << 32) | h[kk].z;
-        const bool mark = (h[kk].x & 15u) == 15u;
-        const uint64_t hf = mark ? (hi & 0xFFFFFFFFFull) | 0xFFFFFF000000000ull : hi;  // fields 8, 9 unused
-        const uint64_t r12 = 0x001001001001001ull * r, r16 = 0x0001000100010001ull * r;
-        const bool hit = (m0f_has12(lo >> 4, r12) | m0f_has12(hf & 0xFFFFFFFFFFFFFFFull, r12) |
-                          m0f_has16(((uint64_t)o[kk].y << 32) | o[kk].x, r16) |
-                          m0f_has16(((uint64_t)o[kk].w << 32) | o[kk].z, r16)) != 0;
-        const uint32_t p = q0 + 4 * kFThreads * (k >> 2) + (k & 3);
-        svm |= (p >= a && p < b && !hit ? 1u : 0u) << k;
+        const uint32_t rep = ((e[k0 + kk] >> 8) & ((1u << kFRemBits) - 1)) * 0x10001u;
+        const uint32_t m = m0f_min16(m0f_min16(m0f_min16(h[kk][0] ^ rep, h[kk][1] ^ rep),
+                                               m0f_min16(h[kk][2] ^ rep, h[kk][3] ^ rep)),
+                                     m0f_min16(m0f_min16(o[kk][0] ^ rep, o[kk][1] ^ rep),
+                                               m0f_min16(o[kk][2] ^ rep, o[kk][3] ^ rep)));
+        hm |= (min(m & 0xFFFFu, m >> 16) == 0 ? 1u : 0u) << (k0 + kk);
       }
     }
+    uint32_t svm = vm & ~hm;  // bit k: entry k survives
     if (__ballot(svm != 0)) {  // (rare in the steady state)
+      if (nsp) {
+        // each entry not found so far: its position against the spill list,
+        // all lanes comparing their part of it
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+          uint64_t bal = __ballot((svm >> k) & 1u);
+          while (bal) {
+            const int l = __builtin_ctzll(bal);
+            bal &= bal - 1;
+            const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)(e[k] >> 8), l) & 0xFFFFFFu;
+            bool f = false;
+#pragma unroll
+            for (int i = 0; i < (int)(kFSpill / 64); i++) f |= sp[i] == key;
+            if (__ballot(f) && lane == (uint32_t)l) svm &= ~(1u << k);
+          }
+        }
+      }
 #pragma unroll
       for (int k = 0; k < E; k++) {
         const bool sv = (svm >> k) & 1u;
@@ -2302,9 +2329,11 @@ uint32_t persistent_grid(sg_ctx* ctx, const void* kernel, int threads) {
 // bucket descriptors and the list of non-empty buckets, in the workspace from
 // ws_base (reserved by the caller when `reserved`).  n > 0, nrec > 0.
 // stages: 1 the tiles and pass 1 (then bp is rebased), 2 the rest (after a
-// stage-1 call with the same bp), 3 both.
+// stage-1 call with the same bp), 3 both.  plane: pass 1 writes the pass-2
+// digit plane (else stage 2 needs k_top_plane first).
 static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_off, uint64_t n, uint64_t nrec,
-                         size_t ws_base, bool reserved, BucketPlan& bp, bool trace = false, int stages = 3) {
+                         size_t ws_base, bool reserved, BucketPlan& bp, bool trace = false, int stages = 3,
+                         bool plane = true) {
   int rc = SG_OK;
   if (stages & 1) {
     if (256 * bp.gmax >= 0xFFFFFFFFull || bp.NG > kMaxGroups) {
@@ -2370,7 +2399,8 @@ static int partition_one(sg_ctx* ctx, const uint32_t* d_vals, const uint64_t* d_
   }
   rc = scan32(ctx, hist1, goff1, 256 * bp.T, scr);
   if (rc) return rc;
-  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, b1, nullptr, (const uint64_t*)ws_at(ctx, bp.oKM)};
+  P1Args a1{d_vals, d_off, nrec, tstart, trec, T, goff1, hist1, v1, plane ? b1 : nullptr, nullptr,
+            (const uint64_t*)ws_at(ctx, bp.oKM)};
   unsigned long long* p1dbg = nullptr;
   if (dbg) {
     SG_HIP(hipMalloc(&p1dbg, 64));
@@ -2574,17 +2604,18 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   }
   const M0F f = m0f_bind(ctx);
   const uint32_t T = (uint32_t)bp.T;
-  SG_HIP(hipMemsetAsync(f.cursor, 0, 256 * 4 + 4, ctx->stream));  // cursors and the survivor count
+  SG_HIP(hipMemsetAsync(f.cursor, 0, 256 * 4 + 256 + 256 * 4, ctx->stream));  // cursors, survivor and spill counts
   {
     ScopedTimer tm(ctx, "m0_index");
     hipLaunchKernelGGL(k_m0_index, dim3(kFBuckets / 256, 256), dim3(256), 0, ctx->stream, (const uint32_t*)mwords,
-                       f.tab, f.ovals, f.cursor);
+                       f.tab, f.ovals, f.cursor, f.nspill, f.spill);
   }
   {
     ScopedTimer tm(ctx, "m0_filter");
     hipLaunchKernelGGL(k_m0_filter, dim3(kFParts, 256), dim3(kFThreads), 0, ctx->stream,
                        (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
-                       (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor, f.surv, f.nsurv,
+                       (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor,
+                       (const uint32_t*)f.nspill, (const uint32_t*)f.spill, f.surv, f.nsurv,
                        f.wgcnt);
   }
   SG_HIP(hipGetLastError());
@@ -2612,6 +2643,20 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   ctx->m0f_last = 1;
   *done = true;
   return SG_OK;
+}
+
+// the pass-2 digit plane of pass-1 entries (top byte of each), after a pass 1
+// that did not write it: 4 entries per thread and step
+__global__ void k_top_plane(const uint32_t* __restrict__ v1, uint64_t n, uint8_t* __restrict__ b1) {
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x * 4) {
+    if (i + 4 <= n && ((uintptr_t)(v1 + i) & 15) == 0) {
+      const uint4 q = *reinterpret_cast<const uint4*>(v1 + i);
+      *reinterpret_cast<uint32_t*>(b1 + i) = (q.x >> 24) | ((q.y >> 24) << 8) | ((q.z >> 24) << 16) | (q.w & 0xFF000000u);
+    } else {
+      for (uint64_t k = i; k < i + 4 && k < n; k++) b1[k] = (uint8_t)(v1[k] >> 24);
+    }
+  }
 }
 
 // queued records of a partitioned slice: one add per block
@@ -2683,11 +2728,16 @@ static int bucket_triage_one(sg_ctx* ctx, uint32_t* mwords, uint32_t* nwords, co
     return rc;
   }
   // the flags path with the M0 filter between the two partition passes
-  int rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 1);
+  // (pass 1 without the pass-2 digit plane: -0.88 GB of writes per C2 step;
+  // when the survivors overflow, the plane is made from the pass-1 entries)
+  int rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 1, false);
   if (rc) return rc;
   bool done = false;
   rc = m0_filter(ctx, bp, mwords, nwords, d_rec_new, &done);
   if (rc || done) return rc;
+  hipLaunchKernelGGL(k_top_plane, dim3((uint32_t)std::min<uint64_t>(4096, div_up(n, 1024))), dim3(256), 0,
+                     ctx->stream, (const uint32_t*)ws_at(ctx, bp.oV1), n, (uint8_t*)ws_at(ctx, bp.oB1));
+  SG_HIP(hipGetLastError());
   rc = partition_one(ctx, d_vals, d_off, n, nrec, 0, false, bp, trace, 2);
   if (!rc) rc = buckets_one(ctx, bp, mwords, nwords, d_rec_new, nullptr, n, nrec);
   if (!rc) rc = m0f_note_partitioned(ctx, d_rec_new, nrec);

@@ -109,6 +109,25 @@ def test_m0_filter_index_cap_and_overflow(C, ctx, ctx_option):
     hot = rng.random(vals.size) < 0.02  # ~15K entries in the dense slice: ~1/3 of them unproven by its index
     vals[hot] = dense[rng.integers(0, dense.size, size=int(hot.sum()))]
     _check(C, ctx, m0, vals, off, 1, "used")
+    # a few buckets past 15 values (their rest in the slice's spill list):
+    # entries on the spilled positions are proven there, not survivors
+    base = np.uint64(9) << np.uint64(16)  # slice 9
+    spilled = []
+    for j in range(12):
+        vs = np.sort(rng.choice(1 << 11, size=30, replace=False)).astype(np.uint64)
+        pos = (np.uint64(j * 37) << np.uint64(11)) | vs  # 24-bit position in the slice: b1 b3 b0
+        sig = ((pos >> np.uint64(16)) << np.uint64(8)) | ((pos >> np.uint64(8) & np.uint64(255)) << np.uint64(24)) \
+            | (pos & np.uint64(255)) | base
+        spilled.append(sig[15:].astype(np.uint32))
+    spilled = np.concatenate(spilled)
+    m0s = np.unique(np.concatenate([other, spilled]))
+    assert np.isin(spilled, m0s).all()
+    vals, off = _batch(rng, 20_000, other, 0.0)
+    hot = rng.random(vals.size) < 0.05
+    vals[hot] = spilled[rng.integers(0, spilled.size, size=int(hot.sum()))]
+    assert hot.sum() > 10_000
+    _check(C, ctx, m0s, vals, off, 1, "used")
+    assert ctx.counter("m0_filter_survivors") == 0
     # fresh: ~1.6M survivors > the cap
     vals, off = _batch(rng, 50_000, m0, 1.0, maxlen=80)
     assert vals.size > (1 << 20) + 200_000
