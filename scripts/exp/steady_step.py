@@ -46,7 +46,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         print(f"step {a.elapsed_time(e):.3f} ms, queued {int(rec_new.sum())}, "
-              f"filtered slices {ctx.counter('m0_filter_used')}", flush=True)
+              f"filtered slices {ctx.counter('m0_filter_used')}, survivors {ctx.counter('m0_filter_survivors')}", flush=True)
     call("sg_ctx_marker", ctx.h, 1, 9)
     kt = {}
     for name in ("p1_hist", "p1_scatter", "m0_index", "m0_filter", "m0_tail", "p2_hist", "p2_scatter", "bucket_triage"):

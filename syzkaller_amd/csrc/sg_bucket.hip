@@ -1925,6 +1925,11 @@ constexpr int kFThreads = 1024;
 #ifndef SG_FEH
 #define SG_FEH 4  // entries whose LDS reads are in flight together
 #endif
+#ifndef SG_FABL
+#define SG_FABL 0  // diagnostics builds (wrong results): 1 the entry stream only, 2 no overflow block reads,
+                   // 3 no entry stream past the first three steps, 4 overflow reads at random
+                   // blocks, independent of the header, 5 the same, mostly the dummy block
+#endif
 constexpr uint32_t kFParts = SG_FPARTS;                 // filter workgroups per slice
 constexpr uint32_t kFWgCap = 4 * kFSurvCap / (256 * kFParts);  // survivors per filter workgroup (its own region:
                                                               // 4x the mean share at the cap, 32 MiB in all)
@@ -2099,6 +2104,7 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
   auto load = [&](uint32_t q0, uint32_t(&en)[E]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
+      if (SG_FABL == 3 && q0 >= qa + 4 * tid + 3 * kStep) break;
       const uint32_t q = min(q0 + 4 * kFThreads * u, qlast);
       const v4u32 t = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(v1 + q));
       en[4 * u] = t[0];
@@ -2111,15 +2117,16 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
   // loads are in flight would wait for them): step i tests one while the
   // next two steps' loads land in the others.
   uint32_t bA[E], bB[E], bC[E];
-  auto step = [&](uint32_t q0, const uint32_t(&e)[E]) -> bool {
+  auto step = [&](uint32_t q0, const uint32_t(&e)[E]) {
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&wsurv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >
         kFWgCap)
-      return false;  // (overflowing: the partition goes on)
+      return;  // (overflowing: the partition goes on)
     // the entries inside [a, b): all of them unless the wave's step crosses
     // an end of the part (a uniform test)
     const uint32_t qw = (uint32_t)__builtin_amdgcn_readfirstlane((int)q0);  // lane 0's
     uint32_t vm = (1u << E) - 1;
-    if (!(qw >= a && qw + 4 * 63 + 3 + 4 * kFThreads * (U - 1) < b)) {
+    const bool full = qw >= a && qw + 4 * 63 + 3 + 4 * kFThreads * (U - 1) < b;
+    if (!full) {
       vm = 0;
 #pragma unroll
       for (int k = 0; k < E; k++)
@@ -2130,14 +2137,24 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
     // first block (a bucket past 15 values) is not proven here and survives
     // -- the tail re-checks every survivor against the bitmap.
     uint32_t hm = 0;  // bit k: entry k found
+    uint32_t sk = 0;  // the last entry not found (the only survivor of most lanes that have one)
 #pragma unroll
     for (int k0 = 0; k0 < E; k0 += EH) {
+      if (SG_FABL == 1) {
+#pragma unroll
+        for (int k = 0; k < EH; k++) hm |= (e[k0 + k] == 0x12345678u ? 0u : 1u) << (k0 + k);
+        continue;
+      }
       v4u32 h[EH];
 #pragma unroll
       for (int k = 0; k < EH; k++) h[k] = lds[kFOvBlocks + (e[k0 + k] >> (8 + kFRemBits))];
       v4u32 o[EH];
 #pragma unroll
-      for (int k = 0; k < EH; k++) o[k] = lds[__builtin_elementwise_sub_sat(h[k][3] >> 16, kFPad)];
+      for (int k = 0; k < EH; k++)
+        o[k] = SG_FABL == 2   ? h[k]
+               : SG_FABL == 4 ? lds[1 + ((e[k0 + k] >> 8) & 1023u)]
+               : SG_FABL == 5 ? lds[(e[k0 + k] & 0x80000000u) ? 1u : 0u]
+                              : lds[__builtin_elementwise_sub_sat(h[k][3] >> 16, kFPad)];
 #pragma unroll
       for (int kk = 0; kk < EH; kk++) {
         const uint32_t rep = ((e[k0 + kk] >> 8) & ((1u << kFRemBits) - 1)) * 0x10001u;
@@ -2145,11 +2162,40 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
                                                m0f_min16(h[kk][2] ^ rep, h[kk][3] ^ rep)),
                                      m0f_min16(m0f_min16(o[kk][0] ^ rep, o[kk][1] ^ rep),
                                                m0f_min16(o[kk][2] ^ rep, o[kk][3] ^ rep)));
-        hm |= (min(m & 0xFFFFu, m >> 16) == 0 ? 1u : 0u) << (k0 + kk);
+        const bool hit = min(m & 0xFFFFu, m >> 16) == 0;
+        hm |= (hit ? 1u : 0u) << (k0 + kk);
+        sk = hit ? sk : e[k0 + kk];
       }
     }
     uint32_t svm = vm & ~hm;  // bit k: entry k survives
-    if (__ballot(svm != 0)) {  // (rare in the steady state)
+    if (SG_FABL) svm = svm == 0x5A5Au ? 1u : 0u;
+    const uint64_t anysv = __ballot(svm != 0);
+    if (anysv && full && !__ballot(svm & (svm - 1))) {
+      // (rare in the steady state) at most one survivor per lane, entry sk:
+      // its position against the spill list (all lanes comparing their part
+      // of it, one survivor lane after the other), then one slot per survivor
+      bool sv = svm != 0;
+      if (nsp) {
+        const uint32_t key = (sk >> 8) & 0xFFFFFFu;
+        for (uint64_t bal = anysv; bal; bal &= bal - 1) {
+          const int l = __builtin_ctzll(bal);
+          const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, l);
+          bool f = false;
+#pragma unroll
+          for (int i = 0; i < (int)(kFSpill / 64); i++) f |= sp[i] == kl;
+          if (__ballot(f) && lane == (uint32_t)l) sv = false;
+        }
+      }
+      const uint64_t bal = __ballot(sv);
+      if (bal) {
+        const int first = __builtin_ctzll(bal);
+        uint32_t at = 0;
+        if (lane == (uint32_t)first) at = atomicAdd(&wsurv, (uint32_t)__popcll(bal));
+        at = (uint32_t)__shfl((int)at, first) + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        const uint32_t k = (uint32_t)__builtin_ctz(svm | 0x80000000u);
+        if (sv && at < kFWgCap) wsv[at] = make_uint2(q0 + 4 * kFThreads * (k >> 2) + (k & 3), d);
+      }
+    } else if (anysv) {  // several survivors in a lane, or a step across an end of the part
       if (nsp) {
         // each entry not found so far: its position against the spill list,
         // all lanes comparing their part of it
@@ -2180,21 +2226,33 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
         if (sv && at < kFWgCap) wsv[at] = make_uint2(p, d);
       }
     }
-    return true;
   };
+  // A wave-uniform loop with one exit, three steps per iteration (lane 0's
+  // position qw; every lane runs every step, the positions past b masked by
+  // vm, up to two steps past the end).  vmcnt counts in issue order, and the
+  // compiler's waits are merged over every path into the loop head: a
+  // per-lane exit (a divergent loop), an exit between steps, or the
+  // scheduler issuing bA's prologue loads last each made the first step wait
+  // for every load in flight.
   uint32_t q0 = qa + 4 * tid;
+  uint32_t qw = (uint32_t)__builtin_amdgcn_readfirstlane((int)q0);
   load(q0, bA);
+  __builtin_amdgcn_sched_barrier(0);
   load(q0 + kStep, bB);
-  while (q0 < b) {
-    load(q0 + 2 * kStep, bC);
-    if (!step(q0, bA)) break;
-    if ((q0 += kStep) >= b) break;
-    load(q0 + 2 * kStep, bA);
-    if (!step(q0, bB)) break;
-    if ((q0 += kStep) >= b) break;
-    load(q0 + 2 * kStep, bB);
-    if (!step(q0, bC)) break;
+  __builtin_amdgcn_sched_barrier(0);
+  load(q0 + 2 * kStep, bC);
+  __builtin_amdgcn_sched_barrier(0);
+  while (qw < b) {
+    step(q0, bA);
+    load(q0 + 3 * kStep, bA);  // (each buffer reloaded right after its step)
     q0 += kStep;
+    step(q0, bB);
+    load(q0 + 3 * kStep, bB);
+    q0 += kStep;
+    step(q0, bC);
+    load(q0 + 3 * kStep, bC);
+    q0 += kStep;
+    qw += 3 * kStep;
   }
   __syncthreads();
   if (tid == 0) {
