@@ -1917,7 +1917,7 @@ constexpr uint32_t kFSurvCap = 1u << 20;                // survivors per launch
 constexpr uint32_t kFTableBits = 21;                    // the tail's table: 2^21 u64 slots
 constexpr int kFThreads = 1024;
 #ifndef SG_FPARTS
-#define SG_FPARTS 2
+#define SG_FPARTS 8
 #endif
 #ifndef SG_FU
 #define SG_FU 4  // 16-B entry loads per thread per step
@@ -2078,7 +2078,13 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
   uint2* wsv = surv + (uint64_t)wg * kFWgCap;
   if (tid == 0) wsurv = 0;
   const v4u32* hsrc = reinterpret_cast<const v4u32*>(tab + (uint64_t)d * kFBuckets);
-  for (uint32_t i = tid; i < kFBuckets; i += kFThreads) lds[kFOvBlocks + i] = hsrc[i];
+  {
+    v4u32 t[kFBuckets / kFThreads];  // (all in flight, then stored)
+#pragma unroll
+    for (uint32_t u = 0; u < kFBuckets / kFThreads; u++) t[u] = hsrc[tid + u * kFThreads];
+#pragma unroll
+    for (uint32_t u = 0; u < kFBuckets / kFThreads; u++) lds[kFOvBlocks + tid + u * kFThreads] = t[u];
+  }
   const v4u32* osrc = reinterpret_cast<const v4u32*>(ovals + (uint64_t)d * kFOvBlocks * 8);
   for (uint32_t i = 1 + tid; i < nob; i += kFThreads) lds[i] = osrc[i];
   if (tid == 0) lds[0] = v4u32{kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u};  // dummy

@@ -83,10 +83,10 @@ def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option):
     # empty maxSignal: every entry survives (fewer than the cap)
     vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0)
     _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "used")
-    # ... all of them in one pass-1 slice (b2 = 0): past a filter workgroup's
-    # region (8192), so the partition goes on
+    # ... all of them in one pass-1 slice (b2 = 0): past the regions of its
+    # 8 filter workgroups (2048 each), so the partition goes on
     vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0, hi=1 << 16)
-    assert vals.size > 2 * 8192 + 1000
+    assert vals.size > 8 * 2048 + 1000
     _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "fallback")
     # empty records only / a batch without entries
     _check(C, ctx, m0, np.zeros(0, np.uint32), np.zeros(9, np.uint64), 1, None)
