@@ -36,6 +36,10 @@
 // exclusive scan + a scatter (tile in registers, LDS counting-rank, staged
 // by digit, written in digit runs).  No global atomics on the data path, no
 // random HBM access, no 16 GiB owner table.
+//   M0 filter (low-novelty batches, "M0 filter" below): between pass 1 and
+//           pass 2, each slice's run tested against a packed index of the
+//           slice's maxSignal in LDS; only the survivors go on, to a small
+//           exact tail, and pass 2 and the bucket stage do not run.
 #include "sg_internal.h"
 
 #include <algorithm>
