@@ -74,7 +74,10 @@ int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* laun
  * sg_triage_traces without diff lists): "host_copy_bytes", "host_copy_ns"
  * (pageable -> pinned copies), "host_wait_ns" (waits for a staging slot's DMA),
  * "host_copy_threads"; "cpu_quota_milli" (the CPUs this process may use,
- * x1000). */
+ * x1000); the M0 filter (the flags path's low-novelty regime): "m0_filter_used"
+ * and "m0_filter_fallback" (record slices it finished / that went on to pass
+ * 2), "m0_filter_survivors" (the last launch's), "m0_filter_queued_milli" (the
+ * queued fraction of the last partitioned slice, x1000, that auto reads). */
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
 /* Context options.  Every path is selected by its regime; an option only
  * forces one, for a test or a measurement, and no call reads the environment
@@ -95,6 +98,9 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
  *   "rpc_decode_blocks"    delta decode form (-1 by shape, 0 per list, 1 per block)
  *   "host_slice"           host ingest: entries per record slice (0: 64 Mi)
  *   "host_copy_threads"    host ingest: copy threads (0: half the CPU quota, 2..16)
+ *   "m0_filter"            the flags path's M0 filter (-1 auto: after a filtered
+ *                          slice, or a partitioned one that queued < 1/4 of its
+ *                          records; 1 always; 0 never)
  * Unknown keys and out-of-range values return SG_EINVAL. */
 int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value);
 int sg_ctx_get_option(sg_ctx* ctx, const char* key, int64_t* out);

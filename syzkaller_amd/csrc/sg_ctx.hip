@@ -660,8 +660,15 @@ int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value) {
     ctx->debug_part = value != 0;
     return SG_OK;
   }
+  // value ranges, in kOptNames' order (tri-state options: -1 the regime's choice)
+  static const int64_t kLo[kOptCount] = {0, 0, -1, 0, 0, 0, -1, -1, 0, 0, -1};
+  static const int64_t kHi[kOptCount] = {1 << 20, 1, 1, 1, 1 << 20, 1, 1, 1, 1ll << 40, 64, 1};
   for (int i = 0; i < kOptCount; i++)
     if (!strcmp(key, kOptNames[i])) {
+      if (value < kLo[i] || value > kHi[i]) {
+        set_error("sg_ctx_set_option: %s in %lld..%lld", key, (long long)kLo[i], (long long)kHi[i]);
+        return SG_EINVAL;
+      }
       ctx->opt[i] = value;
       return SG_OK;
     }

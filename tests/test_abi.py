@@ -115,7 +115,9 @@ def test_context_options(ctx):
     ctx.set_option("rpc_decode_blocks", 1)
     assert ctx.get_option("rpc_decode_blocks") == 1
     ctx.set_option("rpc_decode_blocks", -1)
-    for bad in (("no_such_option", 1), ("max_launch_records", (1 << 24) + 1), ("max_launch_records", -2)):
+    assert ctx.get_option("m0_filter") == -1
+    for bad in (("no_such_option", 1), ("max_launch_records", (1 << 24) + 1), ("max_launch_records", -2),
+                ("m0_filter", 2), ("m0_filter", -2), ("prefix_pairs", -1), ("host_copy_threads", 65)):
         with pytest.raises(SyzSigError) as e:
             ctx.set_option(*bad)
         assert e.value.rc == SG_EINVAL
