@@ -1945,7 +1945,7 @@ struct M0F {
   uint32_t* cursor;           // [slice] overflow blocks placed (may pass the pool)
   uint32_t* nspill;           // [slice] spilled positions (may pass kFSpill)
   uint32_t* spill;            // [slice][kFSpill] positions
-  uint32_t* nsurv;            // survivors; kFSurvCap + 1 when a workgroup's region overflowed
+  uint32_t* nsurv;            // [0] survivors in the regions that held theirs, [1] != 0: some region overflowed
   uint2* surv;                // (position, slice), kFWgCap per filter workgroup
   uint32_t* wgcnt;            // [filter workgroup] survivors in its region
   unsigned long long* table;  // signal << 32 | min record; kFEmpty between launches
@@ -2268,8 +2268,14 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
   if (tid == 0) {
     const uint32_t c = wsurv;
     wgcnt[wg] = c;
-    // the total (kFSurvCap + 1 past a region: the host then partitions)
-    atomicAdd(nsurv, c > kFWgCap ? kFSurvCap + 1 : c);
+    // the total, and a flag past a region (the host then partitions).  (Once
+    // the total for an overflowed region was kFSurvCap + 1: 4096 of them
+    // wrapped the 32-bit sum to a small count, the tail took the survivors
+    // for fitting, and its table filled -- a hang at 16 workgroups per slice.)
+    if (c > kFWgCap)
+      atomicOr(nsurv + 1, 1u);
+    else
+      atomicAdd(nsurv, c);
   }
 }
 
@@ -2297,7 +2303,9 @@ __global__ void k_m0_tail_insert(const uint2* __restrict__ surv, const uint32_t*
   const uint32_t rec = trec[last_le(goff1 + (uint64_t)q.y * T, 0, T, q.x)] + (e & 0xFFu);
   const unsigned long long key = ((unsigned long long)s << 32) | rec;
   constexpr uint32_t mask = (1u << kFTableBits) - 1;
-  for (uint32_t h = m0f_hash(s) & mask;; h = (h + 1) & mask) {
+  // (bounded: at most kFSurvCap keys in 2^21 slots, so a free or equal slot
+  // always comes first; the bound only keeps a broken invariant from hanging)
+  for (uint32_t h = m0f_hash(s) & mask, probe = 0; probe <= mask; h = (h + 1) & mask, probe++) {
     const unsigned long long old = atomicCAS(&table[h], kFEmpty, key);
     if (old == kFEmpty) break;
     if ((uint32_t)(old >> 32) == s) {
@@ -2688,11 +2696,12 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   }
   SG_HIP(hipGetLastError());
   // (the host ingest's pinned staging may be in a DMA now: a pageable read)
-  uint32_t ns = 0;
-  SG_HIP(hipMemcpyAsync(&ns, f.nsurv, 4, hipMemcpyDeviceToHost, ctx->stream));
+  uint32_t nsv[2] = {0, 0};
+  SG_HIP(hipMemcpyAsync(nsv, f.nsurv, 8, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->m0f_survivors = ns;
-  if (ns > kFSurvCap) {
+  const uint32_t ns = nsv[0];
+  ctx->m0f_survivors = nsv[1] ? kFSurvCap + 1 : ns;
+  if (nsv[1] || ns > kFSurvCap) {
     ctx->m0f_fallback++;
     ctx->m0f_last = 0;
     return SG_OK;
