@@ -79,18 +79,26 @@ def test_host_pipeline_slices_equal_device_path(ctx, ctx_option, trace):
     h_vals = d_vals.cpu().numpy().view(np.uint32)
     h_off = d_off.cpu().numpy().view(np.uint64)
     # default slices (one slice here), many slices, slices of about one record,
-    # and slices smaller than a record (each record then is a slice of its own)
-    for slice_entries in (None, 1 << 19, 1000, 300):
+    # and slices smaller than a record (each record then is a slice of its own);
+    # the M0 filter on its auto regime, and forced on / off for the first two
+    for slice_entries, mode in ((None, -1), (1 << 19, -1), (1000, -1), (300, -1), (None, 1), (1 << 19, 1),
+                                (1 << 19, 0)):
         ctx_option(ctx, "host_slice", slice_entries or 0)
+        ctx_option(ctx, "m0_filter", mode)
+        u0 = ctx.counter("m0_filter_used")
         ms, ns = C.SignalSet(ctx), C.SignalSet(ctx)
         C.SignalAdd(ms, m0)
         if trace:
             got = C.triage_traces(ms, ns, h_vals, h_off, ctx=ctx)
         else:
             got, _, _ = C.triage_batch(ms, ns, h_vals, h_off, want_diff=False, ctx=ctx)
-        assert np.array_equal(got, exp[0]), slice_entries
-        assert np.array_equal(ms.export(), exp[1]), slice_entries
-        assert np.array_equal(ns.export(), exp[2]), slice_entries
+        assert np.array_equal(got, exp[0]), (slice_entries, mode)
+        assert np.array_equal(ms.export(), exp[1]), (slice_entries, mode)
+        assert np.array_equal(ns.export(), exp[2]), (slice_entries, mode)
+        if (slice_entries, mode) == (1 << 19, 1):  # low-novelty slices: the filter's own tail ran
+            assert ctx.counter("m0_filter_used") > u0
+        if mode == 0:
+            assert ctx.counter("m0_filter_used") == u0
         ms.close()
         ns.close()
 
