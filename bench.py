@@ -21,7 +21,9 @@ Workloads (BASELINE.json configs):
   steady (N=1, reported under "steady_state"): the fuzzer's low-novelty steady
      state -- programs drawn from a fixed population of --npop programs,
      re-executed with flaky coverage (each PC replaced by a fresh draw with
-     probability --noise), against maxSignal = the population's signal.
+     probability --noise), against maxSignal = the population's signal.  The
+     flags path runs in its default auto regime, which takes these batches
+     through the M0 filter ("m0_filter" counts the slices).
   C3 (default at N>1): one batch of 128Ki programs per rank (the C2 recipe;
      N=8 is C3's 1Mi-program batch) triaged as ONE sequential loop over the
      whole batch, hash-sharded by signal across the ranks (syzkaller_amd/shard.py:
@@ -813,7 +815,10 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
         call("sg_set_copy", maxsig.h, m0set.h)
         triage(ctx, maxsig, newsig, b, rec_new)
     timed = batches[args.warmup:]
+    f0 = {k: ctx.counter("m0_filter_" + k) for k in ("used", "fallback")}
     wall, tri = timed_steps(ctx, maxsig, m0set, newsig, timed, rec_new, 1, tag=2)
+    m0f = {k: ctx.counter("m0_filter_" + k) - f0[k] for k in f0}
+    m0f["regime"] = "auto (option m0_filter -1)"
     kernels = kernel_table(ctx, STEP_KERNELS, args.steps)
     ctx.timing(False)
     units = sum(b.nvals for b in timed)
@@ -823,7 +828,7 @@ def run_steady(ctx, args, cfg, g, maxsig, newsig, m0set, rec_new):
            "value": units / wall, "unit": "PCs/s", "ms_per_step": wall * 1e3 / args.steps,
            "triage_ms_events": float(np.mean(tri)),
            "maxsignal_start": m0_count, "signal_per_step": units / args.steps, "gen_s": round(t_gen, 2),
-           "kernels": kernels}
+           "m0_filter": m0f, "kernels": kernels}
     if not args.no_account:
         diff_vals = torch.empty(maxnvals, dtype=torch.int32, device="cuda")
         diff_off = torch.empty(maxnrec + 1, dtype=torch.int64, device="cuda")
