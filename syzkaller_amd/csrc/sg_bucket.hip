@@ -2005,6 +2005,16 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
   const bool ok = ob && ost + ob <= kFOvBlocks;  // (else the rest is spilled)
   uint16_t* out = ovals + ((uint64_t)d * kFOvBlocks + ost) * 8;
   const uint32_t kin = n > 8 ? 7u : 8u;  // values in the header
+  // the spill list's slots for the rest (past 15 values, or past 7 with the
+  // pool full), one add per wave (past the index's capacity, an add per
+  // spilled value -- ~10^4-10^5 per slice on one counter -- took 3.7-14 ms at
+  // an 18-41M maxSignal)
+  const uint32_t kst = ok ? 15u : 7u, nsw = n > 8 && n > kst ? n - kst : 0u;
+  const uint32_t si = sgd::wave_incl_add(nsw);
+  const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)si, 63);
+  uint32_t sbase = 0;
+  if (lane == 0 && stot) sbase = atomicAdd(&nspill[d], stot);
+  sbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)sbase) + si - nsw;
   uint64_t lo = 0, hi = 0;               // fields 0..3, 4..7
   uint32_t k = 0;
 #pragma unroll
@@ -2024,7 +2034,7 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
         } else if (ok && k < 15) {
           out[k - 7] = (uint16_t)v;
         } else {  // (rare: past 15 values, or the pool full)
-          const uint32_t at = atomicAdd(&nspill[d], 1u);
+          const uint32_t at = sbase + k - kst;
           if (at < kFSpill) spill[(uint64_t)d * kFSpill + at] = (j << kFRemBits) | v;
         }
         k++;
@@ -2704,6 +2714,13 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   if (nsv[1] || ns > kFSurvCap) {
     ctx->m0f_fallback++;
     ctx->m0f_last = 0;
+    // auto: a fallback on a slice that was expected to filter (a maxSignal
+    // past the index's capacity, or a novelty burst) -- the next 1, 2, 4 ..
+    // 64 slices are not tried
+    if (ctx->opt[kOptM0Filter] < 0) {
+      ctx->m0f_backoff = ctx->m0f_backoff ? std::min<uint32_t>(2 * ctx->m0f_backoff, 64) : 1;
+      ctx->m0f_skip = ctx->m0f_backoff;
+    }
     return SG_OK;
   }
   if (ns) {
@@ -2718,6 +2735,7 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   SG_HIP(hipGetLastError());
   ctx->m0f_used++;
   ctx->m0f_last = 1;
+  ctx->m0f_backoff = ctx->m0f_skip = 0;
   *done = true;
   return SG_OK;
 }
@@ -2770,7 +2788,9 @@ static int m0f_note_partitioned(sg_ctx* ctx, const uint8_t* d_rec_new, uint64_t 
 // and after a partitioned slice whose queued fraction was below kFTryQueued
 // (in the steady state 9 % of the records are queued, in a fresh batch all:
 // fresh batches then never pay for it); on the context's first slice it is
-// tried.  A queued count still in flight keeps the previous choice.
+// tried.  A queued count still in flight keeps the previous choice.  After a
+// fallback it backs off (m0f_skip): a low-novelty batch whose maxSignal is
+// past the index's capacity would otherwise fall back on every slice.
 constexpr double kFTryQueued = 0.25;
 static bool m0f_try(sg_ctx* ctx) {
   const int64_t o = ctx->opt[kOptM0Filter];
@@ -2778,6 +2798,10 @@ static bool m0f_try(sg_ctx* ctx) {
   if (ctx->m0f_pending && hipEventQuery(ctx->m0f_ev) == hipSuccess) {
     ctx->m0f_pending = false;
     ctx->m0f_queued = (double)*ctx->m0f_host / (double)(ctx->m0f_nrec ? ctx->m0f_nrec : 1);
+  }
+  if (ctx->m0f_skip) {  // (backing off after fallbacks)
+    ctx->m0f_skip--;
+    return false;
   }
   if (ctx->m0f_last < 0) return true;
   if (ctx->m0f_last == 1) return true;

@@ -112,6 +112,7 @@ struct sg_ctx {
   uint64_t m0f_nrec = 0;
   double m0f_queued = -1;        // queued fraction of the last partitioned slice (-1 unknown)
   uint64_t m0f_used = 0, m0f_fallback = 0, m0f_survivors = 0;
+  uint32_t m0f_backoff = 0, m0f_skip = 0;  // auto: slices not to try after fallbacks (doubling, <= 64)
   // host CPUs this process may use (cgroup cpu.max quota, else the affinity
   // mask), read at creation: sizes the host ingest's copy threads
   double cpu_quota = 0;

@@ -138,9 +138,9 @@ def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
     """auto: tried after a slice it filtered; after a partitioned slice only
     when that slice queued under a quarter of its records (a fresh batch queues
     nearly all: the next one is partitioned, and its own low queued fraction
-    brings the filter back); record slices (a lowered per-launch record limit)
-    are filtered one by one, each against the maxSignal the slices before it
-    left."""
+    brings the filter back); after a fallback not for 1, 2, 4 .. slices;
+    record slices (a lowered per-launch record limit) are filtered one by one,
+    each against the maxSignal the slices before it left."""
     ctx = C.Context(0)
     try:
         rng = np.random.default_rng(6003)
@@ -157,6 +157,17 @@ def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
         assert ctx.counter("m0_filter_queued_milli") < 250
         _check(C, ctx, m0, vals, off, 0, "skip")  # never
         _check(C, ctx, m0, fresh, foff, -1, "fallback")
+        # after a fallback auto backs off: 1 slice, then (another fallback) 2,
+        # then a filtered slice resets it -- a maxSignal past the index's
+        # capacity falls back on every slice it tries
+        _check(C, ctx, m0, vals, off, -1, "skip")
+        _check(C, ctx, m0, fresh, foff, -1, "fallback")
+        _check(C, ctx, m0, vals, off, -1, "skip")
+        _check(C, ctx, m0, vals, off, -1, "skip")
+        _check(C, ctx, m0, vals, off, -1, "used")
+        _check(C, ctx, m0, fresh, foff, -1, "fallback")
+        _check(C, ctx, m0, vals, off, -1, "skip")
+        _check(C, ctx, m0, vals, off, -1, "used")
     finally:
         ctx.close()
 
