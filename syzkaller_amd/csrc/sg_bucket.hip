@@ -1916,7 +1916,9 @@ constexpr uint32_t kFBuckets = 1u << (24 - kFRemBits);  // 8192 per slice
 constexpr uint32_t kFOvBlocks = 1984;                   // overflow pool per slice: 8-value u16 blocks (31 KiB);
                                                         // block 0 the dummy
 constexpr uint32_t kFPad = 0x8000u;                     // an unused field (no position; >= it: a block link)
-constexpr uint32_t kFSpill = 512;                       // spill list per slice (8 registers per lane)
+constexpr uint32_t kFSpill = 512;                       // spill list per index part (8 registers per lane)
+constexpr uint32_t kFHMax = 4;                          // index parts per slice, at most (option m0_filter_halves)
+constexpr uint32_t kFIdx = 256 * kFHMax;                // index parts in all
 constexpr uint32_t kFSurvCap = 1u << 20;                // survivors per launch
 constexpr uint32_t kFTableBits = 21;                    // the tail's table: 2^21 u64 slots
 constexpr int kFThreads = 1024;
@@ -1940,34 +1942,35 @@ constexpr uint32_t kFWgCap = 4 * kFSurvCap / (256 * kFParts);  // survivors per 
 constexpr unsigned long long kFEmpty = ~0ull;
 
 struct M0F {
-  uint4* tab;                 // [slice][bucket] headers
-  uint16_t* ovals;            // [slice][8 kFOvBlocks] overflow pool
-  uint32_t* cursor;           // [slice] overflow blocks placed (may pass the pool)
-  uint32_t* nspill;           // [slice] spilled positions (may pass kFSpill)
-  uint32_t* spill;            // [slice][kFSpill] positions
-  uint32_t* nsurv;            // [0] survivors in the regions that held theirs, [1] != 0: some region overflowed
+  uint4* tab;                 // [index part][bucket] headers (part = slice << log H | half)
+  uint16_t* ovals;            // [index part][8 kFOvBlocks] overflow pool
+  uint32_t* cursor;           // [index part] overflow blocks placed (may pass the pool)
+  uint32_t* nspill;           // [index part] spilled positions (may pass kFSpill)
+  uint32_t* spill;            // [index part][kFSpill] positions in the slice
+  uint32_t* nsurv;            // [0] survivors in the regions that held theirs, [1] != 0: some region overflowed,
+                              // [2] != 0: some index part overflowed (values past its pool and spill list)
   uint2* surv;                // (position, slice), kFWgCap per filter workgroup
   uint32_t* wgcnt;            // [filter workgroup] survivors in its region
   unsigned long long* table;  // signal << 32 | min record; kFEmpty between launches
 };
 static size_t m0f_bytes() {
-  return 256ull * kFBuckets * 16 + 256ull * kFOvBlocks * 16 + 256 * 4 + 256 + 256 * 4 + 256ull * kFSpill * 4 +
-         256ull * kFParts * kFWgCap * 8 +
+  return (uint64_t)kFIdx * kFBuckets * 16 + (uint64_t)kFIdx * kFOvBlocks * 16 + kFIdx * 4 + 256 + kFIdx * 4 +
+         (uint64_t)kFIdx * kFSpill * 4 + 256ull * kFParts * kFWgCap * 8 +
          256ull * kFParts * 4 + (8ull << kFTableBits);
 }
 static M0F m0f_bind(sg_ctx* ctx) {
   char* b = (char*)ctx->m0f;
   M0F f;
   f.tab = (uint4*)b;
-  b += 256ull * kFBuckets * 16;
+  b += (uint64_t)kFIdx * kFBuckets * 16;
   f.ovals = (uint16_t*)b;
-  b += 256ull * kFOvBlocks * 16;
+  b += (uint64_t)kFIdx * kFOvBlocks * 16;
   f.cursor = (uint32_t*)b;
-  f.nsurv = f.cursor + 256;
-  f.nspill = f.cursor + 256 + 64;
-  b += 256 * 4 + 256 + 256 * 4;
+  f.nsurv = f.cursor + kFIdx;
+  f.nspill = f.cursor + kFIdx + 64;
+  b += kFIdx * 4 + 256 + kFIdx * 4;
   f.spill = (uint32_t*)b;
-  b += 256ull * kFSpill * 4;
+  b += (uint64_t)kFIdx * kFSpill * 4;
   f.surv = (uint2*)b;
   b += 256ull * kFParts * kFWgCap * 8;
   f.wgcnt = (uint32_t*)b;
@@ -1982,28 +1985,38 @@ static M0F m0f_bind(sg_ctx* ctx) {
 // list, whose blocks one cursor add per wave places.  (A wave per 64 buckets,
 // lane l holding word l of each, measured 0.40-0.45 ms per steady step: 128
 // wave scans per 64 buckets; this form 0.24 ms.)
+// kLogH: the slice's index in 2^kLogH parts (halves h of its positions, each
+// with its own 8192 buckets of 2^(11 - kLogH) positions, pool and spill list:
+// past ~14M signals of maxSignal one part no longer holds a slice); grid
+// (kFBuckets / 256, 256 << kLogH), blockIdx.y = slice << kLogH | h.
+template <int kLogH>
 __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ mwords, uint4* __restrict__ tab,
                                                    uint16_t* __restrict__ ovals, uint32_t* __restrict__ cursor,
-                                                   uint32_t* __restrict__ nspill, uint32_t* __restrict__ spill) {
-  const uint32_t d = blockIdx.y, lane = threadIdx.x & 63;
+                                                   uint32_t* __restrict__ nspill, uint32_t* __restrict__ spill,
+                                                   uint32_t* __restrict__ flags) {
+  constexpr int kQ = 16 >> kLogH;                // bitmap quads per bucket
+  constexpr uint32_t kRB = kFRemBits - kLogH;    // position bits in a bucket
+  const uint32_t dh = blockIdx.y, lane = threadIdx.x & 63;
+  const uint32_t d = dh >> kLogH, h = dh & ((1u << kLogH) - 1);
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  const uint4* src = reinterpret_cast<const uint4*>(mwords + ((uint64_t)d << 19) + ((uint64_t)j << 6));
-  uint4 q[16];
+  const uint4* src = reinterpret_cast<const uint4*>(mwords + ((uint64_t)d << 19) + ((uint64_t)h << (19 - kLogH)) +
+                                                    (uint64_t)j * (4 * kQ));
+  uint4 q[kQ];
 #pragma unroll
-  for (int i = 0; i < 16; i++) q[i] = src[i];
+  for (int i = 0; i < kQ; i++) q[i] = src[i];
   uint32_t n = 0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) n += __popc(q[i].x) + __popc(q[i].y) + __popc(q[i].z) + __popc(q[i].w);
+  for (int i = 0; i < kQ; i++) n += __popc(q[i].x) + __popc(q[i].y) + __popc(q[i].z) + __popc(q[i].w);
   // the overflow block of a bucket past 8 values
   const uint32_t ob = n > 8 ? 1u : 0u;
   const uint32_t oi = sgd::wave_incl_add(ob);
   const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane((int)oi, 63);
   uint32_t obase = 0;
-  if (lane == 0 && otot) obase = atomicAdd(&cursor[d], otot);
+  if (lane == 0 && otot) obase = atomicAdd(&cursor[dh], otot);
   obase = (uint32_t)__builtin_amdgcn_readfirstlane((int)obase);
   const uint32_t ost = 1 + obase + oi - ob;  // first block (block 0: none, the filter's dummy)
   const bool ok = ob && ost + ob <= kFOvBlocks;  // (else the rest is spilled)
-  uint16_t* out = ovals + ((uint64_t)d * kFOvBlocks + ost) * 8;
+  uint16_t* out = ovals + ((uint64_t)dh * kFOvBlocks + ost) * 8;
   const uint32_t kin = n > 8 ? 7u : 8u;  // values in the header
   // the spill list's slots for the rest (past 15 values, or past 7 with the
   // pool full), one add per wave (past the index's capacity, an add per
@@ -2013,12 +2026,13 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
   const uint32_t si = sgd::wave_incl_add(nsw);
   const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)si, 63);
   uint32_t sbase = 0;
-  if (lane == 0 && stot) sbase = atomicAdd(&nspill[d], stot);
+  if (lane == 0 && stot) sbase = atomicAdd(&nspill[dh], stot);
   sbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)sbase) + si - nsw;
+  if (nsw && sbase + nsw > kFSpill) flags[2] = 1u;  // (values past the part's capacity: a larger H would hold them)
   uint64_t lo = 0, hi = 0;               // fields 0..3, 4..7
   uint32_t k = 0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
+  for (int i = 0; i < kQ; i++) {
     const uint32_t wq[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -2035,7 +2049,7 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
           out[k - 7] = (uint16_t)v;
         } else {  // (rare: past 15 values, or the pool full)
           const uint32_t at = sbase + k - kst;
-          if (at < kFSpill) spill[(uint64_t)d * kFSpill + at] = (j << kFRemBits) | v;
+          if (at < kFSpill) spill[(uint64_t)dh * kFSpill + at] = (h << (24 - kLogH)) | (j << kRB) | v;
         }
         k++;
       }
@@ -2050,7 +2064,7 @@ __global__ __launch_bounds__(256) void k_m0_index(const uint32_t* __restrict__ m
   }
   if (ok)
     for (uint32_t t = n - 7; t < 8; t++) out[t] = (uint16_t)kFPad;  // the block's padding
-  tab[(uint64_t)d * kFBuckets + j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  tab[(uint64_t)dh * kFBuckets + j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 typedef unsigned short m0f_u16x2 __attribute__((ext_vector_type(2)));
@@ -2070,7 +2084,7 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
                                                           const uint32_t* __restrict__ nspill,
                                                           const uint32_t* __restrict__ spill,
                                                           uint2* __restrict__ surv, uint32_t* __restrict__ nsurv,
-                                                          uint32_t* __restrict__ wgcnt) {
+                                                          uint32_t* __restrict__ wgcnt, uint32_t logh) {
   // the overflow pool, then the headers (one array: both bases fit the
   // ds_read offset field)
   __shared__ v4u32 lds[kFOvBlocks + kFBuckets];
@@ -2079,19 +2093,24 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
   // wait for every load in flight, the next step's entries included; one
   // counter read by every wave each step measured 12 ms per C2 step)
   __shared__ uint32_t wsurv;
-  const uint32_t d = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  // grid (parts, 256, 2^logh): part x of slice d's run against index part hp
+  // (the positions p with p >> (24 - logh) == hp; the other entries pass as
+  // found -- each entry is tested by exactly one index part)
+  const uint32_t d = blockIdx.y, hp = blockIdx.z, dh = (d << logh) | hp, tid = threadIdx.x, lane = tid & 63;
   const uint32_t R0 = goff1[(uint64_t)d * T], R1 = goff1[(uint64_t)(d + 1) * T];
   const uint64_t len = R1 - R0;
   const uint32_t a = R0 + (uint32_t)(len * blockIdx.x / gridDim.x), b = R0 + (uint32_t)(len * (blockIdx.x + 1) / gridDim.x);
+  const uint32_t wg = dh * gridDim.x + blockIdx.x;
   if (a >= b) {
-    if (tid == 0) wgcnt[d * gridDim.x + blockIdx.x] = 0;
+    if (tid == 0) wgcnt[wg] = 0;
     return;
   }
-  const uint32_t nob = min(cursor[d] + 1, kFOvBlocks);
-  const uint32_t wg = d * gridDim.x + blockIdx.x;
+  const uint32_t rb = kFRemBits - logh;  // position bits in a bucket
+  const uint32_t topm = logh ? ~0u << (32 - logh) : 0u, toph = logh ? hp << (32 - logh) : 0u;  // (of an entry)
+  const uint32_t nob = min(cursor[dh] + 1, kFOvBlocks);
   uint2* wsv = surv + (uint64_t)wg * kFWgCap;
   if (tid == 0) wsurv = 0;
-  const v4u32* hsrc = reinterpret_cast<const v4u32*>(tab + (uint64_t)d * kFBuckets);
+  const v4u32* hsrc = reinterpret_cast<const v4u32*>(tab + (uint64_t)dh * kFBuckets);
   {
     v4u32 t[kFBuckets / kFThreads];  // (all in flight, then stored)
 #pragma unroll
@@ -2099,15 +2118,15 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
 #pragma unroll
     for (uint32_t u = 0; u < kFBuckets / kFThreads; u++) lds[kFOvBlocks + tid + u * kFThreads] = t[u];
   }
-  const v4u32* osrc = reinterpret_cast<const v4u32*>(ovals + (uint64_t)d * kFOvBlocks * 8);
+  const v4u32* osrc = reinterpret_cast<const v4u32*>(ovals + (uint64_t)dh * kFOvBlocks * 8);
   for (uint32_t i = 1 + tid; i < nob; i += kFThreads) lds[i] = osrc[i];
   if (tid == 0) lds[0] = v4u32{kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u, kFPad * 0x10001u};  // dummy
   // the spill list, entry 64 i + lane in sp[i] (~0u: none)
-  const uint32_t nsp = min(nspill[d], kFSpill);
+  const uint32_t nsp = min(nspill[dh], kFSpill);
   uint32_t sp[kFSpill / 64];
 #pragma unroll
   for (int i = 0; i < (int)(kFSpill / 64); i++)
-    sp[i] = 64 * i + lane < nsp ? spill[(uint64_t)d * kFSpill + 64 * i + lane] : ~0u;
+    sp[i] = 64 * i + lane < nsp ? spill[(uint64_t)dh * kFSpill + 64 * i + lane] : ~0u;
   __syncthreads();
   // 4 SG_FU entries per thread per step, two more steps in flight (one
   // 16-wave workgroup per CU holds the LDS index, so the stream's depth is
@@ -2167,7 +2186,7 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
       }
       v4u32 h[EH];
 #pragma unroll
-      for (int k = 0; k < EH; k++) h[k] = lds[kFOvBlocks + (e[k0 + k] >> (8 + kFRemBits))];
+      for (int k = 0; k < EH; k++) h[k] = lds[kFOvBlocks + ((e[k0 + k] >> (8 + rb)) & (kFBuckets - 1))];
       v4u32 o[EH];
 #pragma unroll
       for (int k = 0; k < EH; k++)
@@ -2177,12 +2196,12 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
                               : lds[__builtin_elementwise_sub_sat(h[k][3] >> 16, kFPad)];
 #pragma unroll
       for (int kk = 0; kk < EH; kk++) {
-        const uint32_t rep = ((e[k0 + kk] >> 8) & ((1u << kFRemBits) - 1)) * 0x10001u;
+        const uint32_t rep = ((e[k0 + kk] >> 8) & ((1u << rb) - 1)) * 0x10001u;
         const uint32_t m = m0f_min16(m0f_min16(m0f_min16(h[kk][0] ^ rep, h[kk][1] ^ rep),
                                                m0f_min16(h[kk][2] ^ rep, h[kk][3] ^ rep)),
                                      m0f_min16(m0f_min16(o[kk][0] ^ rep, o[kk][1] ^ rep),
                                                m0f_min16(o[kk][2] ^ rep, o[kk][3] ^ rep)));
-        const bool hit = min(m & 0xFFFFu, m >> 16) == 0;
+        const bool hit = min(m & 0xFFFFu, m >> 16) == 0 || (e[k0 + kk] & topm) != toph;
         hm |= (hit ? 1u : 0u) << (k0 + kk);
         sk = hit ? sk : e[k0 + kk];
       }
@@ -2690,24 +2709,36 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   }
   const M0F f = m0f_bind(ctx);
   const uint32_t T = (uint32_t)bp.T;
-  SG_HIP(hipMemsetAsync(f.cursor, 0, 256 * 4 + 256 + 256 * 4, ctx->stream));  // cursors, survivor and spill counts
+  SG_HIP(hipMemsetAsync(f.cursor, 0, kFIdx * 4 + 256 + kFIdx * 4, ctx->stream));  // cursors, survivor and spill counts
+  // the index in 2^logh parts per slice (auto: raised when a part overflowed
+  // and the survivors with it; the filter's workgroups stay 2048: kFParts >>
+  // logh per slice and part, each part's pass reading the whole slice run)
+  const int logh = ctx->opt[kOptM0Halves] >= 0 ? (int)ctx->opt[kOptM0Halves] : ctx->m0f_logh;
   {
     ScopedTimer tm(ctx, "m0_index");
-    hipLaunchKernelGGL(k_m0_index, dim3(kFBuckets / 256, 256), dim3(256), 0, ctx->stream, (const uint32_t*)mwords,
-                       f.tab, f.ovals, f.cursor, f.nspill, f.spill);
+    const dim3 ig(kFBuckets / 256, 256u << logh);
+    if (logh == 0)
+      hipLaunchKernelGGL(k_m0_index<0>, ig, dim3(256), 0, ctx->stream, (const uint32_t*)mwords, f.tab, f.ovals,
+                         f.cursor, f.nspill, f.spill, f.nsurv);
+    else if (logh == 1)
+      hipLaunchKernelGGL(k_m0_index<1>, ig, dim3(256), 0, ctx->stream, (const uint32_t*)mwords, f.tab, f.ovals,
+                         f.cursor, f.nspill, f.spill, f.nsurv);
+    else
+      hipLaunchKernelGGL(k_m0_index<2>, ig, dim3(256), 0, ctx->stream, (const uint32_t*)mwords, f.tab, f.ovals,
+                         f.cursor, f.nspill, f.spill, f.nsurv);
   }
   {
     ScopedTimer tm(ctx, "m0_filter");
-    hipLaunchKernelGGL(k_m0_filter, dim3(kFParts, 256), dim3(kFThreads), 0, ctx->stream,
+    hipLaunchKernelGGL(k_m0_filter, dim3(kFParts >> logh, 256, 1u << logh), dim3(kFThreads), 0, ctx->stream,
                        (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
                        (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor,
                        (const uint32_t*)f.nspill, (const uint32_t*)f.spill, f.surv, f.nsurv,
-                       f.wgcnt);
+                       f.wgcnt, (uint32_t)logh);
   }
   SG_HIP(hipGetLastError());
   // (the host ingest's pinned staging may be in a DMA now: a pageable read)
-  uint32_t nsv[2] = {0, 0};
-  SG_HIP(hipMemcpyAsync(nsv, f.nsurv, 8, hipMemcpyDeviceToHost, ctx->stream));
+  uint32_t nsv[3] = {0, 0, 0};
+  SG_HIP(hipMemcpyAsync(nsv, f.nsurv, 12, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   const uint32_t ns = nsv[0];
   ctx->m0f_survivors = nsv[1] ? kFSurvCap + 1 : ns;
@@ -2717,7 +2748,9 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
     // auto: a fallback on a slice that was expected to filter (a maxSignal
     // past the index's capacity, or a novelty burst) -- the next 1, 2, 4 ..
     // 64 slices are not tried
-    if (ctx->opt[kOptM0Filter] < 0) {
+    if (ctx->opt[kOptM0Halves] < 0 && nsv[2] && ctx->m0f_logh < 2) {
+      ctx->m0f_logh++;  // an index part overflowed: more parts, tried again at once
+    } else if (ctx->opt[kOptM0Filter] < 0) {
       ctx->m0f_backoff = ctx->m0f_backoff ? std::min<uint32_t>(2 * ctx->m0f_backoff, 64) : 1;
       ctx->m0f_skip = ctx->m0f_backoff;
     }

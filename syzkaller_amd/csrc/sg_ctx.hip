@@ -630,7 +630,7 @@ int sg_ctx_marker(sg_ctx* ctx, int end, uint32_t tag) {
 static const char* const kOptNames[kOptCount] = {
     "bucket_blocks",      "prefix_pairs",       "fold_map",         "minimize_filter",   "minimize_filter_ranks",
     "report_direct",      "rpc_encode_elems",   "rpc_decode_blocks", "host_slice",       "host_copy_threads",
-    "m0_filter"};
+    "m0_filter",          "m0_filter_halves"};
 
 int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return SG_EINVAL;
@@ -661,8 +661,8 @@ int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value) {
     return SG_OK;
   }
   // value ranges, in kOptNames' order (tri-state options: -1 the regime's choice)
-  static const int64_t kLo[kOptCount] = {0, 0, -1, 0, 0, 0, -1, -1, 0, 0, -1};
-  static const int64_t kHi[kOptCount] = {1 << 20, 1, 1, 1, 1 << 20, 1, 1, 1, 1ll << 40, 64, 1};
+  static const int64_t kLo[kOptCount] = {0, 0, -1, 0, 0, 0, -1, -1, 0, 0, -1, -1};
+  static const int64_t kHi[kOptCount] = {1 << 20, 1, 1, 1, 1 << 20, 1, 1, 1, 1ll << 40, 64, 1, 2};
   for (int i = 0; i < kOptCount; i++)
     if (!strcmp(key, kOptNames[i])) {
       if (value < kLo[i] || value > kHi[i]) {
@@ -727,6 +727,8 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out) {
     *out = ctx->m0f_survivors;
   else if (!strcmp(name, "m0_filter_queued_milli"))  // queued fraction x1000 of the last partitioned slice
     *out = ctx->m0f_queued < 0 ? ~0ull : (uint64_t)(ctx->m0f_queued * 1000.0 + 0.5);
+  else if (!strcmp(name, "m0_filter_halves_log"))  // the index's parts per slice (log2) the auto regime uses now
+    *out = (uint64_t)ctx->m0f_logh;
   else if (!strcmp(name, "cpu_quota_milli"))
     *out = (uint64_t)(ctx->cpu_quota * 1000.0 + 0.5);
   else {

@@ -93,12 +93,13 @@ enum SgOpt : int {
   kOptHostSlice,            // host ingest: entries per record slice (0: the default)
   kOptHostCopyThreads,      // host ingest: pageable -> pinned copy threads (0: from the CPU quota)
   kOptM0Filter,             // flags path: the M0 filter (sg_bucket.hip): -1 by the last batches, 0 never, 1 always tried
+  kOptM0Halves,             // the filter's index per slice in 2^k parts (-1 by its fill, 0..2 forced)
   kOptCount
 };
 
 struct sg_ctx {
   int device = 0;
-  int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0, -1};
+  int64_t opt[kOptCount] = {0, 0, -1, 1, 0, 0, -1, -1, 0, 0, -1, -1};
   // the M0 filter's buffers (lazy, sg_bucket.hip) and its regime state: the
   // last record slice's outcome (1 filtered, 0 partitioned), the queued
   // records of the last partitioned slice (counted on the device, read back
@@ -112,7 +113,8 @@ struct sg_ctx {
   uint64_t m0f_nrec = 0;
   double m0f_queued = -1;        // queued fraction of the last partitioned slice (-1 unknown)
   uint64_t m0f_used = 0, m0f_fallback = 0, m0f_survivors = 0;
-  uint32_t m0f_backoff = 0, m0f_skip = 0;  // auto: slices not to try after fallbacks (doubling, <= 64)
+  uint32_t m0f_backoff = 0, m0f_skip = 0;
+  int m0f_logh = 0;  // auto: the index in 2^m0f_logh parts per slice (raised when a slice's index overflows)  // auto: slices not to try after fallbacks (doubling, <= 64)
   // host CPUs this process may use (cgroup cpu.max quota, else the affinity
   // mask), read at creation: sizes the host ingest's copy threads
   double cpu_quota = 0;

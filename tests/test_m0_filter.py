@@ -64,8 +64,12 @@ def _check(C, ctx, m0, vals, off, mode, expect):
     return exp
 
 
-def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option):
+@pytest.mark.parametrize("halves", [0, 1, 2])
+def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option, halves):
+    """Also with the index in 2 and 4 parts per slice (option m0_filter_halves):
+    each entry tested by exactly one part."""
     ctx_option(ctx, "m0_filter", 1)
+    ctx_option(ctx, "m0_filter_halves", halves)
     rng = np.random.default_rng(6001)
     m0 = np.unique(rng.integers(0, 1 << 32, size=300_000, dtype=np.uint64).astype(np.uint32))
     m0 = np.unique(np.concatenate([m0, np.array([0, SENT], np.uint32)]))
@@ -84,7 +88,8 @@ def test_m0_filter_low_novelty_and_edges(C, ctx, ctx_option):
     vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0)
     _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "used")
     # ... all of them in one pass-1 slice (b2 = 0): past the regions of its
-    # 8 filter workgroups (2048 each), so the partition goes on
+    # 8 filter workgroups (2048 each), so the partition goes on (with the index
+    # in parts, a slice's values all sit in the first part: past its workgroups')
     vals, off = _batch(rng, 4_000, np.zeros(0, np.uint32), 1.0, hi=1 << 16)
     assert vals.size > 8 * 2048 + 1000
     _check(C, ctx, np.zeros(0, np.uint32), vals, off, 1, "fallback")
@@ -168,6 +173,31 @@ def test_m0_filter_auto_regime_and_record_slices(C, ctx_option):
         _check(C, ctx, m0, fresh, foff, -1, "fallback")
         _check(C, ctx, m0, vals, off, -1, "skip")
         _check(C, ctx, m0, vals, off, -1, "used")
+    finally:
+        ctx.close()
+
+
+def test_m0_filter_index_parts_auto(C):
+    """A slice whose maxSignal signals overflow one index part (its hot
+    entries then overflow the survivor regions): auto falls back once, takes
+    the index in two parts, and filters the same batch the next time."""
+    ctx = C.Context(0)
+    try:
+        rng = np.random.default_rng(6005)
+        low = rng.choice(1 << 24, size=100_000, replace=False).astype(np.uint64)  # slice 5, λ ≈ 12 per bucket
+        dense = np.unique(((low >> np.uint64(16)) << np.uint64(24)) | (np.uint64(5) << np.uint64(16))
+                          | (low & np.uint64(0xFFFF))).astype(np.uint32)
+        other = np.unique(rng.integers(0, 1 << 32, size=50_000, dtype=np.uint64).astype(np.uint32))
+        m0 = np.unique(np.concatenate([dense, other]))
+        vals, off = _batch(rng, 40_000, other, 1e-4)
+        hot = rng.random(vals.size) < 0.12  # ~140K entries in the dense slice, a third of them past one part
+        vals[hot] = dense[rng.integers(0, dense.size, size=int(hot.sum()))]
+        assert ctx.counter("m0_filter_halves_log") == 0
+        _check(C, ctx, m0, vals, off, 1, "fallback")
+        assert ctx.counter("m0_filter_halves_log") == 1
+        _check(C, ctx, m0, vals, off, 1, "used")
+        ctx.set_option("m0_filter_halves", 0)  # forced back to one part: the same fallback
+        _check(C, ctx, m0, vals, off, 1, "fallback")
     finally:
         ctx.close()
 
