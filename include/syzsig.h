@@ -77,7 +77,8 @@ int sg_ctx_kernel_time(sg_ctx* ctx, const char* name, double* ms, uint64_t* laun
  * x1000); the M0 filter (the flags path's low-novelty regime): "m0_filter_used"
  * and "m0_filter_fallback" (record slices it finished / that went on to pass
  * 2), "m0_filter_survivors" (the last launch's), "m0_filter_queued_milli" (the
- * queued fraction of the last partitioned slice, x1000, that auto reads). */
+ * queued fraction of the last partitioned slice, x1000, that auto reads),
+ * "m0_filter_halves_log" (the index parts per slice, log2, auto uses now). */
 int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
 /* Context options.  Every path is selected by its regime; an option only
  * forces one, for a test or a measurement, and no call reads the environment
@@ -100,7 +101,9 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
  *   "host_copy_threads"    host ingest: copy threads (0: half the CPU quota, 2..16)
  *   "m0_filter"            the flags path's M0 filter (-1 auto: after a filtered
  *                          slice, or a partitioned one that queued < 1/4 of its
- *                          records; 1 always; 0 never)
+ *                          records, backing off after fallbacks; 1 always; 0 never)
+ *   "m0_filter_halves"     its index in 2^k parts per slice (-1 auto: raised when a
+ *                          part overflows; 0..2 forced)
  * Unknown keys and out-of-range values return SG_EINVAL. */
 int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value);
 int sg_ctx_get_option(sg_ctx* ctx, const char* key, int64_t* out);
