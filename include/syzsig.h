@@ -102,7 +102,7 @@ int sg_ctx_counter(sg_ctx* ctx, const char* name, uint64_t* out);
  *   "m0_filter"            the flags path's M0 filter (-1 auto: after a filtered
  *                          slice, or a partitioned one that queued < 1/4 of its
  *                          records, backing off after fallbacks; 1 always; 0 never)
- *   "m0_filter_halves"     its index in 2^k parts per slice (-1 auto: raised when a
+ *   "m0_filter_halves"     its index in 2^k parts per slice (-1 auto: 2 parts once a
  *                          part overflows; 0..2 forced)
  * Unknown keys and out-of-range values return SG_EINVAL. */
 int sg_ctx_set_option(sg_ctx* ctx, const char* key, int64_t value);

@@ -2710,9 +2710,10 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   const M0F f = m0f_bind(ctx);
   const uint32_t T = (uint32_t)bp.T;
   SG_HIP(hipMemsetAsync(f.cursor, 0, kFIdx * 4 + 256 + kFIdx * 4, ctx->stream));  // cursors, survivor and spill counts
-  // the index in 2^logh parts per slice (auto: raised when a part overflowed
-  // and the survivors with it; the filter's workgroups stay 2048: kFParts >>
-  // logh per slice and part, each part's pass reading the whole slice run)
+  // the index in 2^logh parts per slice (auto: 1, or 2 after a part
+  // overflowed and the survivors with it; 4 only forced; the filter's
+  // workgroups stay 2048: kFParts >> logh per slice and part, each part's pass
+  // reading the whole slice run)
   const int logh = ctx->opt[kOptM0Halves] >= 0 ? (int)ctx->opt[kOptM0Halves] : ctx->m0f_logh;
   {
     ScopedTimer tm(ctx, "m0_index");
@@ -2748,8 +2749,12 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
     // auto: a fallback on a slice that was expected to filter (a maxSignal
     // past the index's capacity, or a novelty burst) -- the next 1, 2, 4 ..
     // 64 slices are not tried
-    if (ctx->opt[kOptM0Halves] < 0 && nsv[2] && ctx->m0f_logh < 2) {
-      ctx->m0f_logh++;  // an index part overflowed: more parts, tried again at once
+    if (ctx->opt[kOptM0Halves] < 0 && nsv[2] && ctx->m0f_logh < 1) {
+      // an index part overflowed: two parts, tried again at once (each part's
+      // pass streams the whole run: at 18M signals two parts filter in 1.6 ms
+      // against 2.8 ms of pass 2 and buckets; four, at 41M, took 3.9 ms --
+      // past two parts auto backs off to the partition instead)
+      ctx->m0f_logh++;
     } else if (ctx->opt[kOptM0Filter] < 0) {
       ctx->m0f_backoff = ctx->m0f_backoff ? std::min<uint32_t>(2 * ctx->m0f_backoff, 64) : 1;
       ctx->m0f_skip = ctx->m0f_backoff;
