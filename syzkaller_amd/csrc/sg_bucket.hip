@@ -2076,6 +2076,7 @@ __device__ __forceinline__ uint32_t m0f_min16(uint32_t a, uint32_t b) {  // v_pk
 // grid (kFParts, 256): part x of slice d's pass-1 run.  Per thread and step
 // 4 SG_FU entries, the next two steps' loads in flight while one is tested.
 // A survivor is written as (position, slice).
+template <int kLogH>
 __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restrict__ v1,
                                                           const uint32_t* __restrict__ goff1, uint32_t T,
                                                           const uint4* __restrict__ tab,
@@ -2084,7 +2085,8 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
                                                           const uint32_t* __restrict__ nspill,
                                                           const uint32_t* __restrict__ spill,
                                                           uint2* __restrict__ surv, uint32_t* __restrict__ nsurv,
-                                                          uint32_t* __restrict__ wgcnt, uint32_t logh) {
+                                                          uint32_t* __restrict__ wgcnt) {
+  constexpr uint32_t logh = kLogH;  // (a constant: as a kernel argument its shifts cost 0.1 ms per launch)
   // the overflow pool, then the headers (one array: both bases fit the
   // ds_read offset field)
   __shared__ v4u32 lds[kFOvBlocks + kFBuckets];
@@ -2106,7 +2108,8 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
     return;
   }
   const uint32_t rb = kFRemBits - logh;  // position bits in a bucket
-  const uint32_t topm = logh ? ~0u << (32 - logh) : 0u, toph = logh ? hp << (32 - logh) : 0u;  // (of an entry)
+  constexpr uint32_t topm = logh ? ~0u << (32 - logh) : 0u;  // (the part's bits of an entry)
+  const uint32_t toph = logh ? hp << ((32 - logh) & 31) : 0u;
   const uint32_t nob = min(cursor[dh] + 1, kFOvBlocks);
   uint2* wsv = surv + (uint64_t)wg * kFWgCap;
   if (tid == 0) wsurv = 0;
@@ -2201,7 +2204,7 @@ __global__ __launch_bounds__(kFThreads) void k_m0_filter(const uint32_t* __restr
                                                m0f_min16(h[kk][2] ^ rep, h[kk][3] ^ rep)),
                                      m0f_min16(m0f_min16(o[kk][0] ^ rep, o[kk][1] ^ rep),
                                                m0f_min16(o[kk][2] ^ rep, o[kk][3] ^ rep)));
-        const bool hit = min(m & 0xFFFFu, m >> 16) == 0 || (e[k0 + kk] & topm) != toph;
+        const bool hit = min(m & 0xFFFFu, m >> 16) == 0 || (logh && (e[k0 + kk] & topm) != toph);
         hm |= (hit ? 1u : 0u) << (k0 + kk);
         sk = hit ? sk : e[k0 + kk];
       }
@@ -2730,11 +2733,11 @@ static int m0_filter(sg_ctx* ctx, const BucketPlan& bp, uint32_t* mwords, uint32
   }
   {
     ScopedTimer tm(ctx, "m0_filter");
-    hipLaunchKernelGGL(k_m0_filter, dim3(kFParts >> logh, 256, 1u << logh), dim3(kFThreads), 0, ctx->stream,
+    auto kf = logh == 0 ? k_m0_filter<0> : logh == 1 ? k_m0_filter<1> : k_m0_filter<2>;
+    hipLaunchKernelGGL(kf, dim3(kFParts >> logh, 256, 1u << logh), dim3(kFThreads), 0, ctx->stream,
                        (const uint32_t*)ws_at(ctx, bp.oV1), (const uint32_t*)ws_at(ctx, bp.oO1), T,
                        (const uint4*)f.tab, (const uint16_t*)f.ovals, (const uint32_t*)f.cursor,
-                       (const uint32_t*)f.nspill, (const uint32_t*)f.spill, f.surv, f.nsurv,
-                       f.wgcnt, (uint32_t)logh);
+                       (const uint32_t*)f.nspill, (const uint32_t*)f.spill, f.surv, f.nsurv, f.wgcnt);
   }
   SG_HIP(hipGetLastError());
   // (the host ingest's pinned staging may be in a DMA now: a pageable read)
